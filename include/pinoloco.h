@@ -1,0 +1,170 @@
+/*
+ * pinoloco -- C-ABI of the MI355X-native batched MPC inner loop.
+ *
+ * Drop-in boundary for the reference's OSQP-SQP solve path
+ * (lukasmolnar/pino-locoman @ 2025-05-09).  Each entry point replaces a
+ * reference interface, cited as file:line of the reference:
+ *
+ *   pl_model_create       <- RobotWrapper.BuildFromURDF + buildReducedRobot
+ *                            (utils/robot.py:13-22); the host parser
+ *                            pinoloco/model.py produces the tables.
+ *   pl_ocp_create         <- make_ocp(dynamics, OCP_ARGS, robot, nodes, solver)
+ *                            (optimization/ocp_factory.py:8-27) + setup_problem
+ *                            (optimization/ocp.py:38-44): variable/row layout and
+ *                            the Jacobian sparsity of J_g (ocp.py:283, 305).
+ *   pl_ocp_set_params     <- opti.set_value(...) of every parameter
+ *                            (ocp.py:216-242, ocp_whole_body_rnea.py:204); the
+ *                            array is opti.p in declaration order (ocp.py:54-69).
+ *   pl_ocp_set_x          <- opti.set_initial(...) / warm_start()
+ *                            (ocp.py:161-163, ocp_whole_body_rnea.py:207-235).
+ *   pl_ocp_init_solver    <- OCP.init_solver() OSQP branch (ocp.py:265-313):
+ *                            constant Hessian diagonal, OSQP setup.
+ *   pl_ocp_solve          <- OCP.solve() OSQP branch minus retract
+ *                            (ocp.py:375-414): sqp_data, osqp.update/solve,
+ *                            _armijo_line_search, max violation.
+ *   pl_eval_sqp_data      <- the CasADi Function sqp_data(x, p) ->
+ *                            (grad_f, J_g, g, lbg, ubg) (ocp.py:287, 386).
+ *   pl_eval_f             <- f_data (ocp.py:289); g_data is the g/lbg/ubg part
+ *                            of pl_eval_sqp_data (ocp.py:290).
+ *   pl_mpc_*              <- run_mpc.mpc_loop OSQP branch (run_mpc.py:115-143)
+ *                            executed on the device for a whole batch.
+ *
+ * Conventions: all host arrays are caller-owned, C-contiguous float64,
+ * problem-major ([batch][len]).  The library copies them into device buffers
+ * it owns.  Functions return 0 on success and a negative value on error; the
+ * message is available from pl_last_error() (thread-local).  Per-problem
+ * solver failures are reported in pl_stats.status, never as a call failure.
+ * A handle is bound to one HIP device and stream and is not thread-safe.
+ * Calls are synchronous with respect to host buffers on return.
+ */
+#ifndef PINOLOCO_H_
+#define PINOLOCO_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pl_model pl_model;
+typedef struct pl_ocp pl_ocp;
+
+/* Joint types (JointModelFreeFlyer root + revolute joints, utils/robot.py:14). */
+#define PL_JOINT_FREEFLYER 1
+#define PL_JOINT_REVOLUTE 2
+
+/* Dynamics kinds (ocp_factory.py:9-15). centroidal_* stay on the CPU oracle. */
+#define PL_DYN_WHOLE_BODY_RNEA 0
+#define PL_DYN_WHOLE_BODY_ACC 1
+#define PL_DYN_WHOLE_BODY_ABA 2
+
+typedef struct {
+  int njoints;                 /* including the universe joint 0 */
+  int nq, nv;
+  const int* parent;           /* [njoints] */
+  const int* jtype;            /* [njoints] PL_JOINT_* (0 for universe) */
+  const double* axis;          /* [njoints*3] revolute axis in the joint frame */
+  const double* placement_R;   /* [njoints*9] jointPlacement rotation (row-major) */
+  const double* placement_p;   /* [njoints*3] */
+  const double* mass;          /* [njoints] body inertias (fixed children merged) */
+  const double* lever;         /* [njoints*3] CoM in the joint frame */
+  const double* inertia;       /* [njoints*9] rotational inertia at the CoM */
+  const double* gravity;       /* [3] */
+  int nframes;
+  const int* frame_parent;     /* [nframes] parent joint */
+  const double* frame_R;       /* [nframes*9] placement w.r.t. the parent joint */
+  const double* frame_p;       /* [nframes*3] */
+} pl_model_desc;
+
+typedef struct {
+  int dynamics;                /* PL_DYN_* */
+  int nodes;                   /* N */
+  int tau_nodes;               /* OCP_ARGS["whole_body_rnea"]["tau_nodes"] (ocp_args.py:16) */
+  int include_acc;             /* must be 1 (ocp_args.py:17) */
+  int include_base;            /* must be 1 for whole_body_acc (ocp_args.py:11) */
+  int n_feet;                  /* 4: FR, FL, RR, RL (utils/gait_sequence.py:7) */
+  int foot_frames[4];
+  int ext_force_frame;         /* -1: none */
+  int arm_ee_frame;            /* -1: none */
+  int base_frame;              /* "base_link" frame, -1 if absent (dynamics/dynamics.py:17) */
+  double mu;                   /* friction coefficient 0.7 (ocp.py:103) */
+  const double* q0;            /* [nq] reference pose (SRDF) */
+  const double* joint_pos_min; /* [nj] */
+  const double* joint_pos_max;
+  const double* joint_vel_max;
+  const double* joint_torque_max;
+  /* OSQP settings (ocp.py:267-273 + OSQP 0.6 defaults) */
+  double rho, sigma, alpha, eps_abs, eps_rel, eps_prim_inf, eps_dual_inf;
+  int max_iter, scaling, check_termination, warm_start;
+  /* gait used by the device-side MPC loop (utils/gait_sequence.py:5-24) */
+  int gait_type;               /* 0 trot, 1 walk, 2 stand */
+  double gait_period;
+} pl_ocp_desc;
+
+typedef struct {
+  int status;                  /* OSQP status code (1 solved, 2 inaccurate, -2 max iter, ...) */
+  int admm_iters;
+  int ls_accepted;             /* line search accepted a step (ocp.py:473-480) */
+  int ls_branch;               /* 1: g high & improving, 2: armijo, 3: filter */
+  int ls_trials;
+  int pad;
+  double ls_alpha;             /* accepted step length (a / a_decay, ocp.py:475) */
+  double viol_max;             /* _constraint_violation_max after the step (ocp.py:412-414) */
+  double pri_res, dua_res;
+  double f;                    /* objective at the returned point */
+} pl_stats;
+
+const char* pl_last_error(void);
+int pl_version(void);
+
+int pl_model_create(const pl_model_desc* desc, pl_model** out);
+void pl_model_destroy(pl_model* m);
+
+/* device = -1 builds a host-only handle (layout/pattern queries, no solves). */
+int pl_ocp_create(const pl_model* model, const pl_ocp_desc* desc, int batch, int device, pl_ocp** out);
+void pl_ocp_destroy(pl_ocp* o);
+
+/* n decision variables, m rows, np parameters, nnz Jacobian entries. */
+int pl_ocp_dims(const pl_ocp* o, int* n, int* m, int* np, int* nnz);
+/* Jacobian pattern in the library's entry order: global (row, col) per entry. */
+int pl_ocp_pattern(const pl_ocp* o, int* rows, int* cols);
+
+int pl_ocp_set_params(pl_ocp* o, const double* P);   /* [batch][np] */
+int pl_ocp_get_params(pl_ocp* o, double* P);
+int pl_ocp_set_x(pl_ocp* o, const double* X);        /* [batch][n] */
+int pl_ocp_get_x(pl_ocp* o, double* X);
+int pl_ocp_init_solver(pl_ocp* o);                   /* Hessian diag + reset ADMM iterates */
+/* One SQP iteration in place for the whole batch.  stats: [batch] or NULL;
+ * phase_ms: [4] (data, update+factor, admm, line search) or NULL. */
+int pl_ocp_solve(pl_ocp* o, pl_stats* stats, double* phase_ms);
+/* Evaluate sqp_data at the current x: any output may be NULL. */
+int pl_eval_sqp_data(pl_ocp* o, double* grad, double* Jvals, double* g, double* lbg, double* ubg);
+/* f_data value at the current x. */
+int pl_eval_f(pl_ocp* o, double* f);
+/* Scaled-QP diagnostics after a solve: step dx [batch][n] (unscaled OSQP solution). */
+int pl_ocp_get_step(pl_ocp* o, double* dx);
+
+/* Device-side MPC loop (run_mpc.py:127-143) for the whole batch:
+ * x_state [batch][nx] = x_init, t0 [batch] = gait time offset. */
+int pl_mpc_setup(pl_ocp* o, const double* x_state, const double* t0);
+/* One MPC step k: gait schedule at t0 + k*dt_min, x_init, warm start, solve,
+ * x_state <- integrate(x_state, DX[1]).  No host transfers. */
+int pl_mpc_step(pl_ocp* o, int k);
+int pl_mpc_get_state(pl_ocp* o, double* x_state);
+/* Copy the first control input row u_0 [batch][nu_0] and x_state into a
+ * caller-owned DEVICE buffer (for collectives): layout [batch][nu_0 + nx]. */
+int pl_mpc_export(pl_ocp* o, void* device_dst);
+int pl_ocp_sync(pl_ocp* o);
+
+/* Host-side state maps, x = [q, v], dx = [dq, dv]
+ * (DynamicsWholeBodyTorque.state_integrate / state_difference,
+ *  dynamics/dynamics_whole_body_torque.py:11-40). */
+int pl_state_integrate(const pl_model* m, const double* x, const double* dx, double* out);
+int pl_state_difference(const pl_model* m, const double* x0, const double* x1, double* dx);
+
+/* Test / parity access to internal per-problem arrays and the node table. */
+int pl_debug_get(pl_ocp* o, const char* name, double* out, long long count);
+int pl_debug_nodes(const pl_ocp* o, int* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PINOLOCO_H_ */

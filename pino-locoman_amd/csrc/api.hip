@@ -1,0 +1,857 @@
+// C-ABI of the batched MPC inner loop (include/pinoloco.h).
+//
+// Host side of the drop-in boundary: builds the variable / row / sparsity layout
+// the reference gets from CasADi Opti (optimization/ocp.py:38-44, 103-198, 283,
+// 305), owns the device buffers of a batch, and sequences the kernels of one SQP
+// iteration exactly as OCP.solve() sequences sqp_data -> osqp.update ->
+// osqp.solve -> line search (ocp.py:375-414).
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/pinoloco.h"
+#include "rows.h"
+#include "state.h"
+
+static thread_local char g_err[1024] = "";
+
+void pl_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+struct pl_model {
+  PlModel m;
+  int nframes;
+  std::vector<int> frame_parent;
+  std::vector<double> frame_R, frame_p;
+};
+
+struct pl_ocp {
+  PlOcpHandle h;
+  bool on_device;
+  std::vector<PlNode> nodes;
+  std::vector<int> colptr, rowidx, entcol, rowptr, rowent, cplrow, rownode, colnode;
+  std::vector<double> h_params;  // host copy of the parameters (B x np)
+  std::vector<void*> allocs;
+  hipEvent_t ev[5];
+};
+
+extern "C" const char* pl_last_error(void) { return g_err; }
+extern "C" int pl_version(void) { return 1; }
+
+// ---------------------------------------------------------------------------
+// model
+extern "C" int pl_model_create(const pl_model_desc* d, pl_model** out) {
+  if (!d || !out) { pl_set_error("null argument"); return -1; }
+  if (d->njoints > PL_MAXJ || d->nq > PL_MAXQ || d->nv > PL_MAXV) {
+    pl_set_error("model too large (njoints=%d nq=%d nv=%d)", d->njoints, d->nq, d->nv);
+    return -1;
+  }
+  pl_model* M = new pl_model();
+  PlModel& m = M->m;
+  memset(&m, 0, sizeof(m));
+  m.njoints = d->njoints;
+  m.nq = d->nq;
+  m.nv = d->nv;
+  int iq = 0, iv = 0;
+  m.total_mass = 0.0;
+  for (int j = 0; j < d->njoints; ++j) {
+    m.parent[j] = d->parent[j];
+    m.jtype[j] = d->jtype[j];
+    for (int k = 0; k < 3; ++k) m.axis[j][k] = d->axis[3 * j + k];
+    for (int k = 0; k < 9; ++k) m.jR[j][k] = d->placement_R[9 * j + k];
+    for (int k = 0; k < 3; ++k) m.jp[j][k] = d->placement_p[3 * j + k];
+    m.mass[j] = d->mass[j];
+    for (int k = 0; k < 3; ++k) m.lever[j][k] = d->lever[3 * j + k];
+    for (int k = 0; k < 9; ++k) m.Ic[j][k] = d->inertia[9 * j + k];
+    m.total_mass += d->mass[j];
+    if (j == 0) continue;
+    m.idx_q[j] = iq;
+    m.idx_v[j] = iv;
+    if (m.jtype[j] == PL_JT_FREEFLYER) {
+      if (j != 1) { pl_set_error("free-flyer must be joint 1"); delete M; return -1; }
+      iq += 7;
+      iv += 6;
+    } else if (m.jtype[j] == PL_JT_REVOLUTE) {
+      iq += 1;
+      iv += 1;
+      const double* a = m.axis[j];
+      if (a[0] == 1.0 && a[1] == 0.0 && a[2] == 0.0) m.axis_kind[j] = PL_AX_X;
+      else if (a[0] == 0.0 && a[1] == 1.0 && a[2] == 0.0) m.axis_kind[j] = PL_AX_Y;
+      else if (a[0] == 0.0 && a[1] == 0.0 && a[2] == 1.0) m.axis_kind[j] = PL_AX_Z;
+      else m.axis_kind[j] = PL_AX_GEN;
+    } else {
+      pl_set_error("unsupported joint type %d at joint %d", m.jtype[j], j);
+      delete M;
+      return -1;
+    }
+  }
+  if (iq != d->nq || iv != d->nv || d->jtype[1] != PL_JT_FREEFLYER) {
+    pl_set_error("inconsistent nq/nv or missing free-flyer root");
+    delete M;
+    return -1;
+  }
+  for (int k = 0; k < 3; ++k) m.gravity[k] = d->gravity[k];
+  // chains: every non-root joint's parent is the root or the previous joint, and
+  // only the root branches (utils/robot.py robots: 4 legs + optional arm)
+  std::vector<int> nchild(d->njoints, 0);
+  for (int j = 2; j < d->njoints; ++j) nchild[m.parent[j]]++;
+  m.nchains = 0;
+  for (int j = 2; j < d->njoints; ++j) {
+    const int p = m.parent[j];
+    if (p == 1) {
+      if (m.nchains >= PL_MAXCHAIN) { pl_set_error("too many chains"); delete M; return -1; }
+      m.chain_first[m.nchains] = j;
+      m.chain_len[m.nchains] = 1;
+      m.nchains++;
+    } else if (p == j - 1 && nchild[p] == 1 && m.nchains > 0) {
+      m.chain_len[m.nchains - 1]++;
+      if (m.chain_len[m.nchains - 1] > PL_MAXCL) { pl_set_error("chain too long"); delete M; return -1; }
+    } else {
+      pl_set_error("joint %d breaks the root+chains tree shape", j);
+      delete M;
+      return -1;
+    }
+  }
+  M->nframes = d->nframes;
+  M->frame_parent.assign(d->frame_parent, d->frame_parent + d->nframes);
+  M->frame_R.assign(d->frame_R, d->frame_R + 9 * d->nframes);
+  M->frame_p.assign(d->frame_p, d->frame_p + 3 * d->nframes);
+  *out = M;
+  return 0;
+}
+
+extern "C" void pl_model_destroy(pl_model* m) { delete m; }
+
+// ---------------------------------------------------------------------------
+// layout
+namespace {
+
+PlFrameRef frame_ref(const pl_model* M, int fid) {
+  PlFrameRef f;
+  memset(&f, 0, sizeof(f));
+  if (fid < 0 || fid >= M->nframes) { f.valid = 0; f.joint = -1; return f; }
+  f.valid = 1;
+  f.joint = M->frame_parent[fid];
+  for (int k = 0; k < 9; ++k) f.R[k] = M->frame_R[9 * fid + k];
+  for (int k = 0; k < 3; ++k) f.p[k] = M->frame_p[3 * fid + k];
+  return f;
+}
+
+void add_block(PlOcpConst& O, int type, int kind, int count, int arg = 0) {
+  PlRowBlock& B = O.blk[type][O.nblk[type]++];
+  B.kind = kind;
+  B.count = count;
+  B.arg = arg;
+  B.pad = 0;
+}
+
+// Row blocks per node type in the reference's subject_to order.
+void build_blocks(PlOcpConst& O, bool has_ext, bool has_arm) {
+  for (int type = 0; type < 3; ++type) {
+    O.nblk[type] = 0;
+    const bool first = (type == 0);
+    const bool tau = (O.dyn == PL_DYN_RNEA) && (type == 1 || (type == 0 && O.tau_nodes > 0));
+    if (first) add_block(O, type, PL_RB_INIT, O.ndx);
+    add_block(O, type, PL_RB_DYNQ, O.nv);
+    add_block(O, type, PL_RB_DYNV, O.nv);
+    if (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC) add_block(O, type, PL_RB_RNEA_BASE, 6);
+    if (tau) {
+      add_block(O, type, PL_RB_TAU_EQ, O.nj);
+      add_block(O, type, PL_RB_TAU_BND, O.nj);
+    }
+    for (int k = 0; k < O.nfeet; ++k) {
+      add_block(O, type, PL_RB_FZ, 1, k);
+      add_block(O, type, PL_RB_CONE, 1, k);
+      add_block(O, type, PL_RB_SWINGF, 3, k);
+      if (!first) {
+        add_block(O, type, PL_RB_FVXY, 2, k);
+        add_block(O, type, PL_RB_FVZ, 1, k);
+      }
+    }
+    if (has_ext) add_block(O, type, PL_RB_EXT, 3);
+    if (!first) {
+      if (has_arm) add_block(O, type, PL_RB_ARM, 3);
+      add_block(O, type, PL_RB_QJ, O.nj);
+      add_block(O, type, PL_RB_VJ, O.nj);
+    }
+    int rows = 0;
+    for (int b = 0; b < O.nblk[type]; ++b) rows += O.blk[type][b].count;
+    O.rows_of_type[type] = rows;
+  }
+}
+
+// velocity-index support of a frame on joint j (joints from j up to the root, root excluded)
+std::vector<int> support_v(const PlModel& M, int j) {
+  std::vector<int> s;
+  while (j > 1) {
+    s.push_back(M.idx_v[j]);
+    j = M.parent[j];
+  }
+  return s;
+}
+
+// Local-column dependency set of every row of node i (superset of the true
+// nonzeros; values of structurally-irrelevant entries evaluate to 0).
+std::vector<std::vector<int>> node_row_deps(const PlModel& M, const PlOcpConst& O, int i, int nu) {
+  const int type = pl::node_type(O, i);
+  const int nv = O.nv, nj = O.nj, nf = O.nf, ndx = O.ndx;
+  const int nw = ndx + nu;
+  auto DQ = [&](int k) { return k; };
+  auto DV = [&](int k) { return nv + k; };
+  auto U = [&](int k) { return ndx + k; };
+  auto DXN = [&](int k) { return nw + k; };
+  const int f_off = (O.dyn == PL_DYN_RNEA) ? O.na : (O.dyn == PL_DYN_ACC ? nv : nj);
+  auto F = [&](int k) { return U(f_off + k); };
+  std::vector<int> dynset;  // dependency set of the RNEA / ABA outputs
+  for (int k = 3; k < nv; ++k) dynset.push_back(DQ(k));
+  for (int k = 0; k < nv; ++k) dynset.push_back(DV(k));
+  if (O.dyn == PL_DYN_ABA) {
+    for (int k = 0; k < nj; ++k) dynset.push_back(U(k));
+  } else {
+    for (int k = 0; k < nv; ++k) dynset.push_back(U(k));
+  }
+  for (int k = 0; k < nf; ++k) dynset.push_back(F(k));
+  auto frame_deps = [&](const PlFrameRef& fr) {
+    std::vector<int> s;
+    for (int k = 3; k < 6; ++k) s.push_back(DQ(k));
+    for (int v : support_v(M, fr.joint)) s.push_back(DQ(v));
+    for (int k = 0; k < 6; ++k) s.push_back(DV(k));
+    for (int v : support_v(M, fr.joint)) s.push_back(DV(v));
+    return s;
+  };
+  std::vector<std::vector<int>> rows;
+  for (int b = 0; b < O.nblk[type]; ++b) {
+    const PlRowBlock& B = O.blk[type][b];
+    const int k = B.arg;
+    for (int r = 0; r < B.count; ++r) {
+      std::vector<int> s;
+      switch (B.kind) {
+        case PL_RB_INIT: s = {r}; break;
+        case PL_RB_DYNQ: s = {DQ(r), DV(r), DXN(r)}; break;
+        case PL_RB_DYNV:
+          if (O.dyn == PL_DYN_ABA) { s = dynset; s.push_back(DV(r)); s.push_back(DXN(nv + r)); }
+          else s = {DV(r), U(r), DXN(nv + r)};
+          break;
+        case PL_RB_RNEA_BASE: s = dynset; break;
+        case PL_RB_TAU_EQ: s = dynset; s.push_back(U(O.na + nf + r)); break;
+        case PL_RB_TAU_BND: s = {U(O.na + nf + r)}; break;
+        case PL_RB_FZ: s = {F(3 * k + 2)}; break;
+        case PL_RB_CONE: s = {F(3 * k), F(3 * k + 1), F(3 * k + 2)}; break;
+        case PL_RB_SWINGF: s = {F(3 * k + r)}; break;
+        case PL_RB_FVXY:
+        case PL_RB_FVZ: s = frame_deps(O.feet[k]); break;
+        case PL_RB_EXT: s = {F(3 * O.nfeet + r)}; break;
+        case PL_RB_ARM: s = frame_deps(O.arm); break;
+        case PL_RB_QJ: s = {DQ(6 + r)}; break;
+        case PL_RB_VJ: s = {DV(6 + r)}; break;
+      }
+      std::sort(s.begin(), s.end());
+      s.erase(std::unique(s.begin(), s.end()), s.end());
+      rows.push_back(s);
+    }
+  }
+  return rows;
+}
+
+int build_layout(pl_ocp* o) {
+  PlOcpHandle& h = o->h;
+  const PlOcpConst& O = h.oc;
+  const PlModel& M = h.model;
+  const int N = O.N, ndx = O.ndx;
+  o->nodes.assign(N + 1, PlNode());
+  o->colptr.clear();
+  o->rowidx.clear();
+  o->entcol.clear();
+  o->rowptr.clear();
+  o->rowent.clear();
+  o->cplrow.clear();
+  int x_off = 0, row_off = 0, ent_off = 0, s_off = 0;
+  h.nw_max = 0;
+  h.ncol_max = 0;
+  h.nrow_max = 0;
+  h.nunit_max = 0;
+  for (int i = 0; i <= N; ++i) {
+    PlNode& nd = o->nodes[i];
+    memset(&nd, 0, sizeof(nd));
+    const int nu = (i < N) ? pl::node_nu(O, i) : 0;
+    nd.nu = nu;
+    nd.nw = ndx + nu;
+    nd.x_off = x_off;
+    nd.row_off = row_off;
+    nd.ent_off = ent_off;
+    nd.colptr_off = (int)o->colptr.size();
+    nd.rowptr_off = (int)o->rowptr.size();
+    nd.csr_off = (int)o->rowent.size();
+    nd.cpl_off = (int)o->cplrow.size();
+    if (i < N) {
+      auto deps = node_row_deps(M, O, i, nu);
+      nd.nrow = (int)deps.size();
+      nd.ncol = nd.nw + ndx;
+      std::vector<std::vector<int>> cols(nd.ncol);
+      for (int r = 0; r < nd.nrow; ++r)
+        for (int c : deps[r]) cols[c].push_back(r);
+      int e = 0;
+      std::vector<std::vector<int>> rowents(nd.nrow);
+      for (int c = 0; c < nd.ncol; ++c) {
+        o->colptr.push_back(e);
+        for (int r : cols[c]) {
+          o->rowidx.push_back(r);
+          o->entcol.push_back(c);
+          rowents[r].push_back(e);
+          ++e;
+        }
+      }
+      o->colptr.push_back(e);
+      nd.nent = e;
+      int s = 0;
+      for (int r = 0; r < nd.nrow; ++r) {
+        o->rowptr.push_back(s);
+        bool cpl = false;
+        for (int ee : rowents[r]) {
+          o->rowent.push_back(ee);
+          if (o->entcol[ent_off + ee] >= nd.nw) cpl = true;
+          ++s;
+        }
+        if (cpl) o->cplrow.push_back(r);
+      }
+      o->rowptr.push_back(s);
+      nd.ncpl = (int)o->cplrow.size() - nd.cpl_off;
+    }
+    nd.ntile = (nd.nw + 7) / 8;
+    nd.nunit = nd.ntile * (nd.ntile + 1);
+    nd.s_off = s_off;
+    s_off += nd.nunit * 32;
+    x_off += nd.nw;
+    row_off += nd.nrow;
+    ent_off += nd.nent;
+    h.nw_max = std::max(h.nw_max, nd.nw);
+    h.ncol_max = std::max(h.ncol_max, nd.ncol);
+    h.nrow_max = std::max(h.nrow_max, nd.nrow);
+    h.nunit_max = std::max(h.nunit_max, nd.nunit);
+  }
+  h.n = x_off;
+  h.m = row_off;
+  h.nnz = ent_off;
+  h.S_stride = s_off;
+  if (h.nw_max > 112) {
+    pl_set_error("node block %d > 112 variables is not supported by the factor kernel", h.nw_max);
+    return -1;
+  }
+  o->rownode.assign(h.m, 0);
+  o->colnode.assign(h.n, 0);
+  for (int i = 0; i <= N; ++i) {
+    const PlNode& nd = o->nodes[i];
+    for (int r = 0; r < nd.nrow; ++r) o->rownode[nd.row_off + r] = i;
+    for (int c = 0; c < nd.nw; ++c) o->colnode[nd.x_off + c] = i;
+  }
+  return 0;
+}
+
+template <class T>
+int dalloc(pl_ocp* o, T** p, size_t count) {
+  void* q = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc(&q, count * sizeof(T));
+  if (e != hipSuccess) {
+    pl_set_error("hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
+    return -2;
+  }
+  hipMemset(q, 0, count * sizeof(T));
+  o->allocs.push_back(q);
+  *p = (T*)q;
+  return 0;
+}
+
+template <class T>
+int upload(pl_ocp* o, T** p, const std::vector<T>& v) {
+  if (dalloc(o, p, v.size())) return -2;
+  if (!v.empty()) PL_CHECK_HIP(hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int batch, int device, pl_ocp** out) {
+  if (!model || !d || !out || batch <= 0) { pl_set_error("bad arguments"); return -1; }
+  if (d->dynamics < 0 || d->dynamics > 2) { pl_set_error("Unknown dynamics type: %d", d->dynamics); return -1; }
+  if (d->dynamics == PL_DYN_WHOLE_BODY_RNEA && !d->include_acc) {
+    pl_set_error("whole_body_rnea requires include_acc=True on this path");
+    return -1;
+  }
+  if (d->dynamics == PL_DYN_WHOLE_BODY_ACC && !d->include_base) {
+    pl_set_error("whole_body_acc requires include_base=True on this path");
+    return -1;
+  }
+  if (d->nodes < 2 || d->n_feet != 4) { pl_set_error("need nodes >= 2 and 4 feet"); return -1; }
+  pl_ocp* o = new pl_ocp();
+  PlOcpHandle& h = o->h;
+  memset(&h, 0, sizeof(h));
+  h.model = model->m;
+  PlOcpConst& O = h.oc;
+  memset(&O, 0, sizeof(O));
+  const PlModel& M = h.model;
+  O.dyn = d->dynamics;
+  O.N = d->nodes;
+  O.nq = M.nq;
+  O.nv = M.nv;
+  O.nj = M.nq - 7;
+  O.nfeet = 4;
+  const bool has_ext = d->ext_force_frame >= 0;
+  const bool has_arm = d->arm_ee_frame >= 0;
+  O.nf = 12 + (has_ext ? 3 : 0);
+  O.nee = 4 + (has_ext ? 1 : 0);
+  O.nx = M.nq + M.nv;
+  O.ndx = 2 * M.nv;
+  O.na = (O.dyn == PL_DYN_ABA) ? 0 : M.nv;
+  O.tau_nodes = (O.dyn == PL_DYN_RNEA) ? d->tau_nodes : 0;
+  O.mu = d->mu;
+  for (int k = 0; k < 4; ++k) O.feet[k] = frame_ref(model, d->foot_frames[k]);
+  O.ext = frame_ref(model, d->ext_force_frame);
+  O.arm = frame_ref(model, d->arm_ee_frame);
+  O.base = frame_ref(model, d->base_frame);
+  if (has_arm && !O.base.valid) { pl_set_error("arm velocity needs the base_link frame"); delete o; return -1; }
+  for (int k = 0; k < M.nq; ++k) O.q0[k] = d->q0[k];
+  for (int k = 0; k < O.nj; ++k) {
+    O.pos_min[k] = d->joint_pos_min[k];
+    O.pos_max[k] = d->joint_pos_max[k];
+    O.vel_max[k] = d->joint_vel_max[k];
+    O.tau_max[k] = d->joint_torque_max[k];
+  }
+  build_blocks(O, has_ext, has_arm);
+  // parameter layout (Opti declaration order)
+  int off = 0;
+  auto take = [&](int len) { int r = off; off += len; return r; };
+  const int nu0 = pl::node_nu(O, 0);
+  O.P.x_init = take(O.nx);
+  O.P.dt_min = take(1);
+  O.P.dt_max = take(1);
+  O.P.contact = take(4 * O.N);
+  O.P.swing = take(4 * O.N);
+  O.P.n_contacts = take(1);
+  O.P.swing_period = take(1);
+  O.P.swing_height = take(1);
+  O.P.swing_vel_limits = take(2);
+  O.P.Q_diag = take(O.ndx);
+  O.P.R_diag = take(nu0);
+  O.P.base_vel_des = take(6);
+  O.P.ext_force_des = take(3);
+  O.P.arm_vel_des = take(3);
+  if (O.dyn == PL_DYN_RNEA) {
+    O.P.tau_prev = take(O.nj);
+    O.P.W_diag = take(O.nj);
+  } else {
+    O.P.tau_prev = O.P.W_diag = -1;
+  }
+  O.P.np = off;
+  if (build_layout(o)) { delete o; return -1; }
+  O.n = h.n;
+  O.m = h.m;
+  h.B = batch;
+  h.N = O.N;
+  h.np = O.P.np;
+  h.nx = O.nx;
+  h.ndx = O.ndx;
+  h.set.rho = d->rho;
+  h.set.sigma = d->sigma;
+  h.set.alpha = d->alpha;
+  h.set.eps_abs = d->eps_abs;
+  h.set.eps_rel = d->eps_rel;
+  h.set.eps_prim_inf = d->eps_prim_inf;
+  h.set.eps_dual_inf = d->eps_dual_inf;
+  h.set.max_iter = d->max_iter;
+  h.set.scaling = d->scaling;
+  h.set.check_termination = d->check_termination;
+  h.set.warm_start = d->warm_start;
+  h.gait_type = d->gait_type;
+  h.gait_period = d->gait_period;
+  h.swing_period = d->gait_type == 0 ? 0.5 * d->gait_period : (d->gait_type == 1 ? 0.25 * d->gait_period : d->gait_period);
+  o->h_params.assign((size_t)batch * h.np, 0.0);
+  o->on_device = device >= 0;
+  h.device = device;
+  if (!o->on_device) { *out = o; return 0; }
+
+  if (hipSetDevice(device) != hipSuccess) { pl_set_error("hipSetDevice(%d) failed", device); delete o; return -2; }
+  if (hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking) != hipSuccess) {
+    pl_set_error("hipStreamCreate failed");
+    delete o;
+    return -2;
+  }
+  for (int k = 0; k < 5; ++k) hipEventCreate(&o->ev[k]);
+  PlDev& D = h.d;
+  const size_t B = batch;
+  int rc = 0;
+  rc |= dalloc(o, &D.model, 1);
+  rc |= dalloc(o, &D.oc, 1);
+  rc |= upload(o, &D.nodes, o->nodes);
+  rc |= upload(o, &D.colptr, o->colptr);
+  rc |= upload(o, &D.rowidx, o->rowidx);
+  rc |= upload(o, &D.entcol, o->entcol);
+  rc |= upload(o, &D.rowptr, o->rowptr);
+  rc |= upload(o, &D.rowent, o->rowent);
+  rc |= upload(o, &D.cplrow, o->cplrow);
+  rc |= upload(o, &D.rownode, o->rownode);
+  rc |= upload(o, &D.colnode, o->colnode);
+  const size_t n = h.n, m = h.m, nnz = h.nnz;
+  rc |= dalloc(o, &D.p, B * h.np);
+  rc |= dalloc(o, &D.x, B * n);
+  rc |= dalloc(o, &D.x0, B * n);
+  rc |= dalloc(o, &D.g, B * m);
+  rc |= dalloc(o, &D.lbg, B * m);
+  rc |= dalloc(o, &D.ubg, B * m);
+  rc |= dalloc(o, &D.grad, B * n);
+  rc |= dalloc(o, &D.Araw, B * nnz);
+  rc |= dalloc(o, &D.P, B * n);
+  rc |= dalloc(o, &D.As, B * nnz);
+  rc |= dalloc(o, &D.qs, B * n);
+  rc |= dalloc(o, &D.ls, B * m);
+  rc |= dalloc(o, &D.us, B * m);
+  rc |= dalloc(o, &D.rho, B * m);
+  rc |= dalloc(o, &D.D, B * n);
+  rc |= dalloc(o, &D.E, B * m);
+  rc |= dalloc(o, &D.cs, B);
+  rc |= dalloc(o, &D.Ps, B * n);
+  rc |= dalloc(o, &D.xa, B * n);
+  rc |= dalloc(o, &D.za, B * m);
+  rc |= dalloc(o, &D.ya, B * m);
+  rc |= dalloc(o, &D.rhs, B * n);
+  rc |= dalloc(o, &D.bt, B * n);
+  rc |= dalloc(o, &D.dxs, B * n);
+  rc |= dalloc(o, &D.dys, B * m);
+  rc |= dalloc(o, &D.aty, B * n);
+  rc |= dalloc(o, &D.step, B * n);
+  rc |= dalloc(o, &D.S, B * (size_t)h.S_stride);
+  rc |= dalloc(o, &D.Kc, B * (size_t)h.ndx * h.nw_max);
+  rc |= dalloc(o, &D.Uc, B * (size_t)h.ndx * h.nw_max);
+  rc |= dalloc(o, &D.Cs, B * (size_t)h.ndx * h.ndx);
+  rc |= dalloc(o, &D.work, B * 8);
+  rc |= dalloc(o, &D.info, B);
+  rc |= dalloc(o, &D.t0, B);
+  rc |= dalloc(o, &D.xstate, B * (size_t)h.nx);
+  if (rc) { pl_ocp_destroy(o); return -2; }
+  if (hipMemcpy(D.model, &h.model, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(D.oc, &h.oc, sizeof(PlOcpConst), hipMemcpyHostToDevice) != hipSuccess) {
+    pl_set_error("upload of model tables failed");
+    pl_ocp_destroy(o);
+    return -2;
+  }
+  *out = o;
+  return 0;
+}
+
+extern "C" void pl_ocp_destroy(pl_ocp* o) {
+  if (!o) return;
+  if (o->on_device) {
+    hipSetDevice(o->h.device);
+    hipStreamSynchronize(o->h.stream);
+    for (void* p : o->allocs) hipFree(p);
+    for (int k = 0; k < 5; ++k) hipEventDestroy(o->ev[k]);
+    hipStreamDestroy(o->h.stream);
+  }
+  delete o;
+}
+
+extern "C" int pl_ocp_dims(const pl_ocp* o, int* n, int* m, int* np, int* nnz) {
+  if (!o) { pl_set_error("null handle"); return -1; }
+  if (n) *n = o->h.n;
+  if (m) *m = o->h.m;
+  if (np) *np = o->h.np;
+  if (nnz) *nnz = o->h.nnz;
+  return 0;
+}
+
+extern "C" int pl_ocp_pattern(const pl_ocp* o, int* rows, int* cols) {
+  if (!o || !rows || !cols) { pl_set_error("null argument"); return -1; }
+  const int N = o->h.N;
+  for (int i = 0; i < N; ++i) {
+    const PlNode& nd = o->nodes[i];
+    for (int e = 0; e < nd.nent; ++e) {
+      const int lc = o->entcol[nd.ent_off + e];
+      rows[nd.ent_off + e] = nd.row_off + o->rowidx[nd.ent_off + e];
+      cols[nd.ent_off + e] = lc < nd.nw ? nd.x_off + lc : o->nodes[i + 1].x_off + (lc - nd.nw);
+    }
+  }
+  return 0;
+}
+
+#define REQUIRE_DEVICE(o)                                              \
+  do {                                                                 \
+    if (!(o) || !(o)->on_device) {                                     \
+      pl_set_error("handle has no device (created with device = -1)"); \
+      return -1;                                                       \
+    }                                                                  \
+    hipSetDevice((o)->h.device);                                       \
+  } while (0)
+
+extern "C" int pl_ocp_set_params(pl_ocp* o, const double* P) {
+  REQUIRE_DEVICE(o);
+  const size_t len = (size_t)o->h.B * o->h.np;
+  memcpy(o->h_params.data(), P, len * sizeof(double));
+  PL_CHECK_HIP(hipMemcpyAsync(o->h.d.p, P, len * sizeof(double), hipMemcpyHostToDevice, o->h.stream));
+  PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
+  return 0;
+}
+
+extern "C" int pl_ocp_get_params(pl_ocp* o, double* P) {
+  REQUIRE_DEVICE(o);
+  PL_CHECK_HIP(hipMemcpyAsync(P, o->h.d.p, (size_t)o->h.B * o->h.np * sizeof(double), hipMemcpyDeviceToHost,
+                              o->h.stream));
+  PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
+  return 0;
+}
+
+extern "C" int pl_ocp_set_x(pl_ocp* o, const double* X) {
+  REQUIRE_DEVICE(o);
+  PL_CHECK_HIP(hipMemcpyAsync(o->h.d.x, X, (size_t)o->h.B * o->h.n * sizeof(double), hipMemcpyHostToDevice,
+                              o->h.stream));
+  PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
+  return 0;
+}
+
+extern "C" int pl_ocp_get_x(pl_ocp* o, double* X) {
+  REQUIRE_DEVICE(o);
+  PL_CHECK_HIP(hipMemcpyAsync(X, o->h.d.x, (size_t)o->h.B * o->h.n * sizeof(double), hipMemcpyDeviceToHost,
+                              o->h.stream));
+  PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
+  return 0;
+}
+
+extern "C" int pl_ocp_get_step(pl_ocp* o, double* dx) {
+  REQUIRE_DEVICE(o);
+  PL_CHECK_HIP(hipMemcpyAsync(dx, o->h.d.step, (size_t)o->h.B * o->h.n * sizeof(double), hipMemcpyDeviceToHost,
+                              o->h.stream));
+  PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
+  return 0;
+}
+
+extern "C" int pl_ocp_init_solver(pl_ocp* o) {
+  REQUIRE_DEVICE(o);
+  launch_hess(&o->h);
+  launch_reset_iterates(&o->h);
+  launch_reset_info(&o->h);
+  PL_CHECK_HIP(hipGetLastError());
+  PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
+  return 0;
+}
+
+static int enqueue_solve(pl_ocp* o, bool timed) {
+  PlOcpHandle* h = &o->h;
+  if (timed) hipEventRecord(o->ev[0], h->stream);
+  // sqp_data(x, p): grad_f, J_g, g, lbg, ubg (ocp.py:386)
+  launch_eval_values(h, h->d.x);
+  launch_eval_jac(h);
+  launch_objective(h);
+  if (timed) hipEventRecord(o->ev[1], h->stream);
+  // osqp.update(q, Ax, l, u): rescale + refactor (ocp.py:391-395)
+  launch_qp_setup(h);
+  launch_factor(h);
+  if (timed) hipEventRecord(o->ev[2], h->stream);
+  // osqp.solve() (ocp.py:401)
+  launch_reset_info(h);
+  if (!h->set.warm_start) launch_reset_iterates(h);
+  launch_admm_init(h);
+  const int ct = h->set.check_termination > 0 ? h->set.check_termination : h->set.max_iter;
+  int it = 0;
+  while (it < h->set.max_iter) {
+    const int nit = std::min(ct, h->set.max_iter - it);
+    it += nit;
+    const bool final = it >= h->set.max_iter;
+    const bool at_check = (h->set.check_termination > 0 && it % h->set.check_termination == 0);
+    launch_admm(h, nit, (at_check || final) ? 1 : 0, it - nit);
+    if (at_check || final) launch_check(h, it, final ? 1 : 0);
+  }
+  launch_unscale(h);
+  if (timed) hipEventRecord(o->ev[3], h->stream);
+  // _armijo_line_search (ocp.py:406, 430-480)
+  launch_line_search(h);
+  if (timed) hipEventRecord(o->ev[4], h->stream);
+  return 0;
+}
+
+static int fetch_stats(pl_ocp* o, pl_stats* stats) {
+  if (!stats) return 0;
+  std::vector<PlProbInfo> info(o->h.B);
+  PL_CHECK_HIP(hipMemcpyAsync(info.data(), o->h.d.info, o->h.B * sizeof(PlProbInfo), hipMemcpyDeviceToHost,
+                              o->h.stream));
+  PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
+  for (int b = 0; b < o->h.B; ++b) {
+    pl_stats& s = stats[b];
+    memset(&s, 0, sizeof(s));
+    s.status = info[b].status;
+    s.admm_iters = info[b].iter;
+    s.ls_accepted = info[b].ls_accepted;
+    s.ls_branch = info[b].ls_branch;
+    s.ls_trials = info[b].ls_trials;
+    s.ls_alpha = info[b].ls_alpha;
+    s.viol_max = info[b].viol_max;
+    s.pri_res = info[b].pri_res;
+    s.dua_res = info[b].dua_res;
+    s.f = info[b].f;
+  }
+  return 0;
+}
+
+extern "C" int pl_ocp_solve(pl_ocp* o, pl_stats* stats, double* phase_ms) {
+  REQUIRE_DEVICE(o);
+  enqueue_solve(o, phase_ms != nullptr);
+  PL_CHECK_HIP(hipGetLastError());
+  PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
+  if (phase_ms) {
+    for (int k = 0; k < 4; ++k) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, o->ev[k], o->ev[k + 1]);
+      phase_ms[k] = ms;
+    }
+  }
+  return fetch_stats(o, stats);
+}
+
+extern "C" int pl_eval_sqp_data(pl_ocp* o, double* grad, double* Jvals, double* g, double* lbg, double* ubg) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  launch_eval_values(h, h->d.x);
+  launch_eval_jac(h);
+  launch_objective(h);
+  PL_CHECK_HIP(hipGetLastError());
+  const size_t B = h->B;
+  if (grad) PL_CHECK_HIP(hipMemcpyAsync(grad, h->d.grad, B * h->n * 8, hipMemcpyDeviceToHost, h->stream));
+  if (Jvals) PL_CHECK_HIP(hipMemcpyAsync(Jvals, h->d.Araw, B * h->nnz * 8, hipMemcpyDeviceToHost, h->stream));
+  if (g) PL_CHECK_HIP(hipMemcpyAsync(g, h->d.g, B * h->m * 8, hipMemcpyDeviceToHost, h->stream));
+  if (lbg) PL_CHECK_HIP(hipMemcpyAsync(lbg, h->d.lbg, B * h->m * 8, hipMemcpyDeviceToHost, h->stream));
+  if (ubg) PL_CHECK_HIP(hipMemcpyAsync(ubg, h->d.ubg, B * h->m * 8, hipMemcpyDeviceToHost, h->stream));
+  PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int pl_eval_f(pl_ocp* o, double* f) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  launch_objective(h);
+  std::vector<double> w((size_t)h->B * 8);
+  PL_CHECK_HIP(hipMemcpyAsync(w.data(), h->d.work, w.size() * 8, hipMemcpyDeviceToHost, h->stream));
+  PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+  for (int b = 0; b < h->B; ++b) f[b] = w[(size_t)b * 8];
+  return 0;
+}
+
+extern "C" int pl_mpc_setup(pl_ocp* o, const double* x_state, const double* t0) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  PL_CHECK_HIP(hipMemcpyAsync(h->d.xstate, x_state, (size_t)h->B * h->nx * 8, hipMemcpyHostToDevice, h->stream));
+  PL_CHECK_HIP(hipMemcpyAsync(h->d.t0, t0, (size_t)h->B * 8, hipMemcpyHostToDevice, h->stream));
+  PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int pl_mpc_step(pl_ocp* o, int k) {
+  REQUIRE_DEVICE(o);
+  launch_mpc_prepare(&o->h, k);
+  enqueue_solve(o, false);
+  launch_mpc_finish(&o->h);
+  PL_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int pl_mpc_get_state(pl_ocp* o, double* x_state) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  PL_CHECK_HIP(hipMemcpyAsync(x_state, h->d.xstate, (size_t)h->B * h->nx * 8, hipMemcpyDeviceToHost, h->stream));
+  PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int pl_mpc_export(pl_ocp* o, void* device_dst) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  const int nu0 = o->nodes[0].nu;
+  const size_t row = (size_t)nu0 + h->nx;
+  char* dst = (char*)device_dst;
+  for (int b = 0; b < h->B; ++b) {
+    PL_CHECK_HIP(hipMemcpyAsync(dst + b * row * 8, h->d.x + (size_t)b * h->n + h->ndx, nu0 * 8,
+                                hipMemcpyDeviceToDevice, h->stream));
+    PL_CHECK_HIP(hipMemcpyAsync(dst + (b * row + nu0) * 8, h->d.xstate + (size_t)b * h->nx, h->nx * 8,
+                                hipMemcpyDeviceToDevice, h->stream));
+  }
+  PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int pl_ocp_sync(pl_ocp* o) {
+  REQUIRE_DEVICE(o);
+  PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
+  return 0;
+}
+
+// Debug / parity access to internal per-problem arrays (tests only).
+extern "C" int pl_debug_get(pl_ocp* o, const char* name, double* out, long long count) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  const size_t B = h->B;
+  struct Item { const char* n; double* p; size_t len; } items[] = {
+      {"As", h->d.As, B * h->nnz}, {"Araw", h->d.Araw, B * h->nnz}, {"qs", h->d.qs, B * h->n},
+      {"ls", h->d.ls, B * h->m},   {"us", h->d.us, B * h->m},       {"rho", h->d.rho, B * h->m},
+      {"D", h->d.D, B * h->n},     {"E", h->d.E, B * h->m},         {"cs", h->d.cs, B},
+      {"Ps", h->d.Ps, B * h->n},   {"P", h->d.P, B * h->n},         {"xa", h->d.xa, B * h->n},
+      {"za", h->d.za, B * h->m},   {"ya", h->d.ya, B * h->m},       {"S", h->d.S, B * (size_t)h->S_stride},
+      {"rhs", h->d.rhs, B * h->n}, {"step", h->d.step, B * h->n},   {"grad", h->d.grad, B * h->n},
+      {"g", h->d.g, B * h->m},     {"xstate", h->d.xstate, B * h->nx}};
+  for (auto& it : items) {
+    if (strcmp(it.n, name) == 0) {
+      if ((size_t)count < it.len) { pl_set_error("buffer too small for %s (%zu)", name, it.len); return -1; }
+      PL_CHECK_HIP(hipMemcpyAsync(out, it.p, it.len * 8, hipMemcpyDeviceToHost, h->stream));
+      PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+      return (int)0;
+    }
+  }
+  pl_set_error("unknown array %s", name);
+  return -1;
+}
+
+// Node table (tests): per node [nw, nu, x_off, row_off, nrow, ncol, ent_off, nent, ntile, nunit, s_off, ncpl]
+extern "C" int pl_debug_nodes(const pl_ocp* o, int* out) {
+  for (size_t i = 0; i < o->nodes.size(); ++i) {
+    const PlNode& nd = o->nodes[i];
+    int* r = out + 12 * i;
+    r[0] = nd.nw; r[1] = nd.nu; r[2] = nd.x_off; r[3] = nd.row_off; r[4] = nd.nrow; r[5] = nd.ncol;
+    r[6] = nd.ent_off; r[7] = nd.nent; r[8] = nd.ntile; r[9] = nd.nunit; r[10] = nd.s_off; r[11] = nd.ncpl;
+  }
+  return 0;
+}
+
+// Host entry points of the Lie-group state maps (DynamicsWholeBodyTorque.state_integrate /
+// state_difference, dynamics_whole_body_torque.py:11-40), same code as the kernels.
+extern "C" int pl_state_integrate(const pl_model* model, const double* x, const double* dx, double* out) {
+  if (!model || !x || !dx || !out) { pl_set_error("null argument"); return -1; }
+  const PlModel& M = model->m;
+  pl::VecIn<double> acc{dx, nullptr, 0.0, -1};
+  double q[PL_MAXQ];
+  pl::integrate_q<double>(M, x, acc, q);
+  for (int k = 0; k < M.nq; ++k) out[k] = q[k];
+  for (int k = 0; k < M.nv; ++k) out[M.nq + k] = x[M.nq + k] + dx[M.nv + k];
+  return 0;
+}
+
+extern "C" int pl_state_difference(const pl_model* model, const double* x0, const double* x1, double* dx) {
+  if (!model || !x0 || !x1 || !dx) { pl_set_error("null argument"); return -1; }
+  const PlModel& M = model->m;
+  pl::difference_q(M, x0, x1, dx);
+  for (int k = 0; k < M.nv; ++k) dx[M.nv + k] = x1[M.nq + k] - x0[M.nq + k];
+  return 0;
+}
+
+// Raw copies of the host-built descriptors (tests: host build of the device math).
+extern "C" int pl_debug_consts(const pl_ocp* o, void* model_out, void* oc_out, int* sizes) {
+  if (!o) { pl_set_error("null handle"); return -1; }
+  if (sizes) { sizes[0] = (int)sizeof(PlModel); sizes[1] = (int)sizeof(PlOcpConst); }
+  if (model_out) memcpy(model_out, &o->h.model, sizeof(PlModel));
+  if (oc_out) memcpy(oc_out, &o->h.oc, sizeof(PlOcpConst));
+  return 0;
+}

@@ -1,0 +1,408 @@
+// Node evaluation kernels: constraint values, constraint Jacobian (forward-mode
+// dual numbers), objective value + gradient, Hessian diagonal.
+//
+// Replaces the CasADi functions sqp_data / f_data / g_data / hess_data
+// (optimization/ocp.py:283-296, 386, 441-452).  One horizon node of one problem
+// is the unit of work: values use one thread per (problem, node); the Jacobian
+// uses one workgroup per (problem, node) and one thread per local column, each
+// thread seeding the tangent of its column and writing the column's entries of
+// the fixed sparsity pattern (CSC order inside the node).
+#include "state.h"
+#include "targets.h"
+
+using pl::VecIn;
+
+namespace {
+
+struct ValueEmit {
+  double* g;
+  double* lb;
+  double* ub;
+  int r;
+  __device__ void operator()(double v, double l, double u) {
+    g[r] = v;
+    lb[r] = l;
+    ub[r] = u;
+    ++r;
+  }
+};
+
+struct JacEmit {
+  const int* rowidx;  // local rows of this column's entries (sorted)
+  double* out;        // entry values of this column
+  int ptr, end, r;
+  __device__ void operator()(const Dual& v, double, double) {
+    if (ptr < end && rowidx[ptr] == r) {
+      out[ptr] = v.d;
+      ++ptr;
+    }
+    ++r;
+  }
+};
+
+__device__ inline void node_inputs(const PlDev& d, const PlNode& nd, const PlNode& nn, const double* x,
+                                   const double* step, double alpha, int seed, VecIn<double>* dx, VecIn<double>* u,
+                                   VecIn<double>* dxn, int ndx) {
+  *dx = VecIn<double>{x + nd.x_off, step ? step + nd.x_off : nullptr, alpha, -1};
+  *u = VecIn<double>{x + nd.x_off + ndx, step ? step + nd.x_off + ndx : nullptr, alpha, -1};
+  *dxn = VecIn<double>{x + nn.x_off, step ? step + nn.x_off : nullptr, alpha, -1};
+}
+
+}  // namespace
+
+// g, lbg, ubg at xsrc for every (problem, node).
+template <int DYN>
+__global__ void k_eval_values(PlDev d, int B, int N, int n, int m, int np, const double* __restrict__ xsrc) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= B * N) return;
+  const int b = tid / N, i = tid - b * N;
+  const PlOcpConst& O = *d.oc;
+  const PlModel& M = *d.model;
+  const PlNode nd = d.nodes[i];
+  const PlNode nn = d.nodes[i + 1];
+  const double* x = xsrc + (size_t)b * n;
+  const double* p = d.p + (size_t)b * np;
+  VecIn<double> dx, u, dxn;
+  node_inputs(d, nd, nn, x, nullptr, 0.0, -1, &dx, &u, &dxn, O.ndx);
+  ValueEmit e{d.g + (size_t)b * m + nd.row_off, d.lbg + (size_t)b * m + nd.row_off,
+              d.ubg + (size_t)b * m + nd.row_off, 0};
+  pl::node_rows<double, DYN>(M, O, i, p, dx, u, dxn, e);
+}
+
+// Constraint Jacobian values on the fixed pattern.  Block = (problem, node),
+// thread = local column.
+template <int DYN>
+__global__ __launch_bounds__(256) void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz) {
+  const int b = blockIdx.x / N, i = blockIdx.x - (blockIdx.x / N) * N;
+  const PlNode nd = d.nodes[i];
+  const int lc = threadIdx.x;
+  if (lc >= nd.ncol) return;
+  const int* cp = d.colptr + nd.colptr_off;
+  const int e0 = cp[lc], e1 = cp[lc + 1];
+  if (e0 == e1) return;
+  const PlOcpConst& O = *d.oc;
+  const PlModel& M = *d.model;
+  const PlNode nn = d.nodes[i + 1];
+  const double* x = d.x + (size_t)b * n;
+  const double* p = d.p + (size_t)b * np;
+  const int ndx = O.ndx;
+  VecIn<Dual> dx{x + nd.x_off, nullptr, 0.0, lc};
+  VecIn<Dual> u{x + nd.x_off + ndx, nullptr, 0.0, lc - ndx};
+  VecIn<Dual> dxn{x + nn.x_off, nullptr, 0.0, lc - nd.nw};
+  JacEmit e{d.rowidx + nd.ent_off, d.Araw + (size_t)b * nnz + nd.ent_off, e0, e1, 0};
+  pl::node_rows<Dual, DYN>(M, O, i, p, dx, u, dxn, e);
+}
+
+// Objective f and gradient at d.x (ocp.py:80-101; ocp_whole_body_rnea.py:108-136).
+// One workgroup per problem.  f is written to work[b * 8 + 0].
+template <bool kGrad>
+__device__ double objective_wg(const PlDev& d, int b, int N, int n, int np, const double* x, const double* step,
+                               double alpha, double* grad) {
+  const PlOcpConst& O = *d.oc;
+  const PlModel& M = *d.model;
+  const double* p = d.p + (size_t)b * np;
+  __shared__ double dxd[2 * PL_MAXV];
+  __shared__ double red[256];
+  if (threadIdx.x == 0) pl::compute_dx_des(M, O, p, dxd);
+  __syncthreads();
+  const int ndx = O.ndx;
+  const double* Q = p + O.P.Q_diag;
+  const double* R = p + O.P.R_diag;
+  double acc = 0.0;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const int i = d.colnode[j];
+    const int lc = j - d.nodes[i].x_off;
+    const double xj = step ? x[j] + alpha * step[j] : x[j];
+    double gj;
+    if (lc < ndx) {
+      double e = xj - dxd[lc];
+      acc += e * (Q[lc] * e);
+      gj = 2.0 * Q[lc] * e;
+    } else {
+      int k = lc - ndx;
+      double e = xj - pl::u_des(M, O, p, k);
+      acc += e * (R[k] * e);
+      gj = 2.0 * R[k] * e;
+      if (O.dyn == PL_DYN_RNEA && i == 0 && k >= O.na + O.nf) {
+        int t = k - O.na - O.nf;
+        double W = p[O.P.W_diag + t];
+        double et = xj - p[O.P.tau_prev + t];
+        acc += et * (W * et);
+        gj += 2.0 * W * et;
+      }
+    }
+    if (kGrad) grad[j] = gj;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  double f = red[0];
+  __syncthreads();
+  return f;
+}
+
+__global__ __launch_bounds__(256) void k_objective(PlDev d, int N, int n, int np) {
+  const int b = blockIdx.x;
+  double f = objective_wg<true>(d, b, N, n, np, d.x + (size_t)b * n, nullptr, 0.0, d.grad + (size_t)b * n);
+  if (threadIdx.x == 0) d.work[(size_t)b * 8 + 0] = f;
+}
+
+// Constant Hessian diagonal (ocp.py:293-296): 2Q on states, 2R on inputs,
+// + 2W on tau_0 (rnea).
+__global__ __launch_bounds__(256) void k_hess(PlDev d, int N, int n, int np) {
+  const int b = blockIdx.x;
+  const PlOcpConst& O = *d.oc;
+  const double* p = d.p + (size_t)b * np;
+  double* P = d.P + (size_t)b * n;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const int i = d.colnode[j];
+    const int lc = j - d.nodes[i].x_off;
+    double h;
+    if (lc < O.ndx) {
+      h = 2.0 * p[O.P.Q_diag + lc];
+    } else {
+      int k = lc - O.ndx;
+      h = 2.0 * p[O.P.R_diag + k];
+      if (O.dyn == PL_DYN_RNEA && i == 0 && k >= O.na + O.nf) h += 2.0 * p[O.P.W_diag + k - O.na - O.nf];
+    }
+    P[j] = h;
+  }
+}
+
+#define PL_DISPATCH_DYN(dyn, KERNEL, ...)                                          \
+  switch (dyn) {                                                                    \
+    case PL_DYN_RNEA: hipLaunchKernelGGL(KERNEL<PL_DYN_RNEA>, __VA_ARGS__); break; \
+    case PL_DYN_ACC: hipLaunchKernelGGL(KERNEL<PL_DYN_ACC>, __VA_ARGS__); break;   \
+    default: hipLaunchKernelGGL(KERNEL<PL_DYN_ABA>, __VA_ARGS__); break;           \
+  }
+
+void launch_eval_values(PlOcpHandle* h, const double* xsrc) {
+  const int total = h->B * h->N;
+  const int bs = 64;
+  PL_DISPATCH_DYN(h->oc.dyn, k_eval_values, dim3((total + bs - 1) / bs), dim3(bs), 0, h->stream, h->d, h->B, h->N,
+                  h->n, h->m, h->np, xsrc);
+}
+
+void launch_eval_jac(PlOcpHandle* h) {
+  PL_DISPATCH_DYN(h->oc.dyn, k_eval_jac, dim3(h->B * h->N), dim3(h->ncol_max <= 192 ? 192 : 256), 0, h->stream,
+                  h->d, h->B, h->N, h->n, h->np, h->nnz);
+}
+
+void launch_objective(PlOcpHandle* h) {
+  hipLaunchKernelGGL(k_objective, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->np);
+}
+
+void launch_hess(PlOcpHandle* h) {
+  hipLaunchKernelGGL(k_hess, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->np);
+}
+
+// ---------------------------------------------------------------------------
+// Armijo / filter line search (ocp.py:430-480), fused: one workgroup per
+// problem evaluates f and the constraint-violation metric at each trial point
+// x + a*dx (nodes on threads) and applies the reference's acceptance rules,
+// including the quirk that f and g_metric are overwritten by every rejected
+// trial (ocp.py:470-471).  Also records the max violation at the returned point
+// (ocp.py:412-414).
+namespace {
+struct ViolEmit {
+  double ss, mx;
+  __device__ void operator()(double v, double l, double u) {
+    double a = fmax(0.0, l - v), c = fmax(0.0, v - u);
+    ss += a * a + c * c;
+    mx = fmax(mx, fmax(a, c));
+  }
+};
+
+__device__ void block_sum_max(double& s, double& mx, double* red) {
+  red[threadIdx.x] = s;
+  red[256 + threadIdx.x] = mx;
+  __syncthreads();
+  for (int k = blockDim.x / 2; k > 0; k >>= 1) {
+    if (threadIdx.x < k) {
+      red[threadIdx.x] += red[threadIdx.x + k];
+      red[256 + threadIdx.x] = fmax(red[256 + threadIdx.x], red[256 + threadIdx.x + k]);
+    }
+    __syncthreads();
+  }
+  s = red[0];
+  mx = red[256];
+  __syncthreads();
+}
+
+template <int DYN>
+__device__ void violation_at(const PlDev& d, int b, int N, int n, int np, const double* x, const double* step,
+                             double alpha, double* red, double* metric, double* vmax) {
+  const PlOcpConst& O = *d.oc;
+  const PlModel& M = *d.model;
+  ViolEmit e{0.0, 0.0};
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const PlNode nd = d.nodes[i];
+    const PlNode nn = d.nodes[i + 1];
+    VecIn<double> dx{x + nd.x_off, step ? step + nd.x_off : nullptr, alpha, -1};
+    VecIn<double> u{x + nd.x_off + O.ndx, step ? step + nd.x_off + O.ndx : nullptr, alpha, -1};
+    VecIn<double> dxn{x + nn.x_off, step ? step + nn.x_off : nullptr, alpha, -1};
+    pl::node_rows<double, DYN>(M, O, i, d.p + (size_t)b * np, dx, u, dxn, e);
+  }
+  double s = e.ss, mx = e.mx;
+  block_sum_max(s, mx, red);
+  *metric = sqrt(s);
+  *vmax = mx;
+}
+}  // namespace
+
+template <int DYN>
+__global__ __launch_bounds__(256) void k_line_search(PlDev d, int N, int n, int m, int np) {
+  const int b = blockIdx.x;
+  __shared__ double red[512];
+  __shared__ int s_flag;
+  double* x = d.x + (size_t)b * n;
+  const double* dxs = d.step + (size_t)b * n;
+  PlProbInfo* info = d.info + b;
+  // NaN step (infeasible QP): every comparison is false -> "didn't converge"
+  if (threadIdx.x == 0) s_flag = 0;
+  __syncthreads();
+  for (int j = threadIdx.x; j < n; j += blockDim.x)
+    if (isnan(dxs[j])) s_flag = 1;
+  __syncthreads();
+  const bool nan_step = s_flag != 0;
+  // f, grad_f, g metric at the current x (ocp.py:441-445)
+  double f = objective_wg<false>(d, b, N, n, np, x, nullptr, 0.0, nullptr);
+  double gm, vmax0;
+  violation_at<DYN>(d, b, N, n, np, x, nullptr, 0.0, red, &gm, &vmax0);
+  double arm = 0.0;
+  {
+    const double* gr = d.grad + (size_t)b * n;
+    double s = 0.0, dummy = 0.0;
+    for (int j = threadIdx.x; j < n; j += blockDim.x) s += gr[j] * dxs[j];
+    block_sum_max(s, dummy, red);
+    arm = s;
+  }
+  const double armijo_factor = 1e-4, a_min = 1e-4, a_decay = 0.5, g_max = 1e-3, g_min = 1e-5, gamma = 1e-5;
+  double a = 1.0;
+  bool accepted = false;
+  int branch = 0, trials = 0;
+  double new_f = f, new_gm = gm, vmax = vmax0;
+  if (nan_step) {
+    trials = 14;
+  } else {
+    while (!accepted && a > a_min) {
+      new_f = objective_wg<false>(d, b, N, n, np, x, dxs, a, nullptr);
+      violation_at<DYN>(d, b, N, n, np, x, dxs, a, red, &new_gm, &vmax);
+      ++trials;
+      if (new_gm > g_max) {
+        if (new_gm < (1.0 - gamma) * gm) { accepted = true; branch = 1; }
+      } else if (fmax(new_gm, gm) < g_min && arm < 0.0) {
+        if (new_f <= f + armijo_factor * arm) { accepted = true; branch = 2; }
+      } else if (new_f <= f - gamma * new_gm || new_gm < (1.0 - gamma) * gm) {
+        accepted = true;
+        branch = 3;
+      }
+      a *= a_decay;
+      f = new_f;
+      gm = new_gm;
+    }
+  }
+  const double a_acc = a / a_decay;
+  if (accepted) {
+    for (int j = threadIdx.x; j < n; j += blockDim.x) x[j] = x[j] + a_acc * dxs[j];
+  }
+  if (threadIdx.x == 0) {
+    info->ls_accepted = accepted ? 1 : 0;
+    info->ls_branch = branch;
+    info->ls_trials = trials;
+    info->ls_alpha = accepted ? a_acc : 0.0;
+    info->viol_max = accepted ? vmax : vmax0;
+    info->f = accepted ? new_f : f;
+  }
+}
+
+void launch_line_search(PlOcpHandle* h) {
+  PL_DISPATCH_DYN(h->oc.dyn, k_line_search, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->np);
+}
+
+// ---------------------------------------------------------------------------
+// Device-side MPC loop glue (run_mpc.py:127-143).
+// Gait schedule (utils/gait_sequence.py:26-77) for one problem.
+__device__ void gait_schedule(const PlOcpConst& O, int gait_type, double period, double swing_period, double t_cur,
+                              const double* p, double* contact, double* swing) {
+  const int N = O.N;
+  double t = t_cur;
+  for (int i = 0; i < N; ++i) {
+    if (i > 0) t += pl::node_dt(O, p, i - 1);
+    for (int f = 0; f < 4; ++f) {
+      contact[4 * i + f] = 1.0;
+      swing[4 * i + f] = 0.0;
+    }
+    if (gait_type == 2) continue;
+    double gp = fmod(t, period) / period;
+    double sp = fmod(t, swing_period) / swing_period;
+    int f0 = -1, f1 = -1;
+    if (gait_type == 0) {
+      if (gp < 0.5) { f0 = 0; f1 = 3; } else { f0 = 1; f1 = 2; }
+    } else {
+      f0 = gp < 0.25 ? 1 : gp < 0.5 ? 2 : gp < 0.75 ? 0 : 3;
+    }
+    contact[4 * i + f0] = 0.0;
+    swing[4 * i + f0] = sp;
+    if (f1 >= 0) {
+      contact[4 * i + f1] = 0.0;
+      swing[4 * i + f1] = sp;
+    }
+  }
+}
+
+// MPC step k, before the solve: parameters (x_init, gait schedule at
+// t0 + k dt_min) and warm start (forces <- f_des masked by the new schedule;
+// ocp_whole_body_rnea.py:207-235).  k == 0 keeps the initial guess.
+__global__ __launch_bounds__(64) void k_mpc_prepare(PlDev d, int k, int N, int n, int np, int nx, int gait_type,
+                                                    double period, double swing_period) {
+  const int b = blockIdx.x;
+  const PlOcpConst& O = *d.oc;
+  const PlModel& M = *d.model;
+  double* p = d.p + (size_t)b * np;
+  for (int j = threadIdx.x; j < nx; j += blockDim.x) p[O.P.x_init + j] = d.xstate[(size_t)b * nx + j];
+  if (threadIdx.x == 0) {
+    double t = d.t0[b] + k * p[O.P.dt_min];
+    gait_schedule(O, gait_type, period, swing_period, t, p, p + O.P.contact, p + O.P.swing);
+  }
+  __syncthreads();
+  if (k == 0) return;
+  double* x = d.x + (size_t)b * n;
+  const int fo = pl::u_force_off(O);
+  for (int i = 0; i < N; ++i) {
+    const int base = d.nodes[i].x_off + O.ndx + fo;
+    for (int c = threadIdx.x; c < O.nf; c += blockDim.x) {
+      int foot = c / 3;
+      double fd = pl::f_des_comp(M, O, p, c);
+      if (foot < 4 && p[O.P.contact + 4 * i + foot] == 0.0) fd = 0.0;
+      x[base + c] = fd;
+    }
+  }
+}
+
+// After the solve: x_state <- integrate(x_state, DX_prev[1]) (run_mpc.py:142).
+__global__ void k_mpc_finish(PlDev d, int B, int n, int nx) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const PlOcpConst& O = *d.oc;
+  const PlModel& M = *d.model;
+  double* xs = d.xstate + (size_t)b * nx;
+  const double* dx1 = d.x + (size_t)b * n + d.nodes[1].x_off;
+  double qn[PL_MAXQ];
+  VecIn<double> acc{dx1, nullptr, 0.0, -1};
+  pl::integrate_q<double>(M, xs, acc, qn);
+  for (int k = 0; k < O.nq; ++k) xs[k] = qn[k];
+  for (int k = 0; k < O.nv; ++k) xs[O.nq + k] += dx1[O.nv + k];
+}
+
+void launch_mpc_prepare(PlOcpHandle* h, int k) {
+  hipLaunchKernelGGL(k_mpc_prepare, dim3(h->B), dim3(64), 0, h->stream, h->d, k, h->N, h->n, h->np, h->nx,
+                     h->gait_type, h->gait_period, h->swing_period);
+}
+
+void launch_mpc_finish(PlOcpHandle* h) {
+  hipLaunchKernelGGL(k_mpc_finish, dim3((h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n, h->nx);
+}

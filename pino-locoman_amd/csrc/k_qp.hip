@@ -1,0 +1,904 @@
+// QP kernels: OSQP-0.6-equivalent scaling, KKT factorisation and ADMM.
+//
+// Replaces osqp.update(q, Ax, l, u) + osqp.solve() (optimization/ocp.py:391-401;
+// OSQP settings ocp.py:267-273).  The KKT system OSQP factors with QDLDL,
+//     [P + sigma I, A^T; A, -diag(rho)^-1],
+// is solved here in its reduced SPD form K = P + sigma I + A^T diag(rho) A, which
+// is block tridiagonal over the horizon (rows of node i touch w_i = [dx_i, u_i]
+// and dx_{i+1}).  The factorisation keeps, per node, the EXPLICIT inverse
+// S_i = Ktilde_ii^-1 of the Schur-complemented diagonal block (symmetric, lower
+// 8x8 tiles only), so each ADMM iteration is two block sweeps that read S_i once
+// each:
+//     forward : bt_i = rhs_i - K_{i,i-1} w_{i-1},    w_i = S_i bt_i
+//     backward: x_i  = S_i (bt_i - K_{i+1,i}^T x_{i+1})
+// with the off-diagonal products applied directly from the (sparse) scaled A.
+// z~ = A x~ and the z / y / rhs updates of the rows of node i are fused into the
+// backward sweep, so A is read once per iteration.
+//
+// Layout of a node's factor block: work unit u = (lower tile t, half h) covers the
+// 8x4 sub-block rows 0..7, cols 4h..4h+3 of tile t; element pair k (0..15) of
+// unit u lives at s_off + (k * nunit + u) * 2 -> every 16-byte load instruction of
+// a wave is one contiguous 1 KiB segment.
+#include "state.h"
+
+#define PL_OSQP_INFTY 1e30
+#define PL_MIN_SCALING 1e-4
+#define PL_MAX_SCALING 1e4
+#define PL_RHO_MIN 1e-6
+#define PL_RHO_TOL 1e-4
+#define PL_RHO_EQ_OVER_INEQ 1e3
+#define PL_DIV_TOL 1e-30
+
+enum {
+  PL_ST_SOLVED = 1,
+  PL_ST_SOLVED_INACCURATE = 2,
+  PL_ST_MAX_ITER = -2,
+  PL_ST_PRIMAL_INF = -3,
+  PL_ST_PRIMAL_INF_INACC = 3,
+  PL_ST_DUAL_INF = -4,
+  PL_ST_DUAL_INF_INACC = 4,
+  PL_ST_NON_CVX = -7,
+  PL_ST_UNSOLVED = -10
+};
+
+namespace {
+
+__device__ __forceinline__ double limit_scaling(double v) {
+  v = v < PL_MIN_SCALING ? 1.0 : v;
+  return v > PL_MAX_SCALING ? PL_MAX_SCALING : v;
+}
+
+__device__ __forceinline__ int gcol(const PlNode* nodes, int i, int lc) {
+  const PlNode& nd = nodes[i];
+  return lc < nd.nw ? nd.x_off + lc : nodes[i + 1].x_off + (lc - nd.nw);
+}
+
+// block reductions over 256 threads
+__device__ double block_max(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  double r = red[0];
+  __syncthreads();
+  return r;
+}
+__device__ double block_sum(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// Iterate the entries of global column j: fn(entry index in the problem's A
+// array, global row).
+template <class F>
+__device__ void for_col_entries(const PlDev& d, int N, int j, F fn) {
+  const int i = d.colnode[j];
+  const PlNode* nodes = d.nodes;
+  const int lc = j - nodes[i].x_off;
+  if (i < N) {
+    const PlNode& nd = nodes[i];
+    const int* cp = d.colptr + nd.colptr_off;
+    for (int e = cp[lc]; e < cp[lc + 1]; ++e) fn(nd.ent_off + e, nd.row_off + d.rowidx[nd.ent_off + e]);
+  }
+  if (i > 0 && lc < d.oc->ndx) {
+    const PlNode& np_ = nodes[i - 1];
+    const int* cp = d.colptr + np_.colptr_off;
+    const int c = np_.nw + lc;
+    for (int e = cp[c]; e < cp[c + 1]; ++e) fn(np_.ent_off + e, np_.row_off + d.rowidx[np_.ent_off + e]);
+  }
+}
+
+// Iterate the entries of global row r: fn(entry index, global column).
+template <class F>
+__device__ void for_row_entries(const PlDev& d, int r, F fn) {
+  const int i = d.rownode[r];
+  const PlNode& nd = d.nodes[i];
+  const int lr = r - nd.row_off;
+  const int* rp = d.rowptr + nd.rowptr_off;
+  const int* re = d.rowent + nd.csr_off;
+  for (int s = rp[lr]; s < rp[lr + 1]; ++s) {
+    const int e = re[s];
+    fn(nd.ent_off + e, gcol(d.nodes, i, d.entcol[nd.ent_off + e]));
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// OSQP data update + Ruiz equilibration (osqp_update_lin_cost / _bounds / _A and
+// scale_data, OSQP 0.6 src/scaling.c), one workgroup per problem.
+__global__ __launch_bounds__(256) void k_qp_setup(PlDev d, int N, int n, int m, int nnz, PlSettings st) {
+  const int b = blockIdx.x;
+  __shared__ double red[256];
+  __shared__ double s_c;
+  const double* A = d.Araw + (size_t)b * nnz;
+  const double* P = d.P + (size_t)b * n;
+  const double* q = d.grad + (size_t)b * n;
+  double* D = d.D + (size_t)b * n;
+  double* E = d.E + (size_t)b * m;
+  double* Dt = d.dxs + (size_t)b * n;  // scratch
+  double* Et = d.dys + (size_t)b * m;  // scratch
+  for (int j = threadIdx.x; j < n; j += blockDim.x) D[j] = 1.0;
+  for (int r = threadIdx.x; r < m; r += blockDim.x) E[r] = 1.0;
+  if (threadIdx.x == 0) s_c = 1.0;
+  __syncthreads();
+  for (int pass = 0; pass < st.scaling; ++pass) {
+    const double c = s_c;
+    // inf-norms of the columns of [P; A] and of the rows of A (scaled data)
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+      double mx = 0.0;
+      for_col_entries(d, N, j, [&](int e, int r) { mx = fmax(mx, fabs(A[e]) * E[r]); });
+      double dj = D[j];
+      Dt[j] = fmax(c * dj * dj * fabs(P[j]), dj * mx);
+    }
+    for (int r = threadIdx.x; r < m; r += blockDim.x) {
+      double mx = 0.0;
+      for_row_entries(d, r, [&](int e, int j) { mx = fmax(mx, fabs(A[e]) * D[j]); });
+      Et[r] = E[r] * mx;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += blockDim.x) D[j] *= 1.0 / sqrt(limit_scaling(Dt[j]));
+    for (int r = threadIdx.x; r < m; r += blockDim.x) E[r] *= 1.0 / sqrt(limit_scaling(Et[r]));
+    __syncthreads();
+    // cost normalisation: c_temp = max(mean |P_jj|, ||q||_inf) on the scaled data
+    double sum = 0.0, qmax = 0.0;
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+      double dj = D[j];
+      sum += c * dj * dj * fabs(P[j]);
+      qmax = fmax(qmax, fabs(c * dj * q[j]));
+    }
+    sum = block_sum(sum, red);
+    qmax = block_max(qmax, red);
+    if (threadIdx.x == 0) {
+      double ct = fmax(sum / (double)n, limit_scaling(qmax));
+      ct = limit_scaling(ct);
+      s_c = c * (1.0 / ct);
+    }
+    __syncthreads();
+  }
+  const double c = s_c;
+  if (threadIdx.x == 0) d.cs[b] = c;
+  // scaled problem data
+  double* As = d.As + (size_t)b * nnz;
+  for (int i = 0; i < N; ++i) {
+    const PlNode nd = d.nodes[i];
+    for (int e = threadIdx.x; e < nd.nent; e += blockDim.x) {
+      const int r = nd.row_off + d.rowidx[nd.ent_off + e];
+      const int j = gcol(d.nodes, i, d.entcol[nd.ent_off + e]);
+      As[nd.ent_off + e] = E[r] * A[nd.ent_off + e] * D[j];
+    }
+  }
+  double* qs = d.qs + (size_t)b * n;
+  double* Ps = d.Ps + (size_t)b * n;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    qs[j] = c * D[j] * q[j];
+    Ps[j] = c * D[j] * D[j] * P[j];
+  }
+  const double* g = d.g + (size_t)b * m;
+  const double* lbg = d.lbg + (size_t)b * m;
+  const double* ubg = d.ubg + (size_t)b * m;
+  double* ls = d.ls + (size_t)b * m;
+  double* us = d.us + (size_t)b * m;
+  double* rho = d.rho + (size_t)b * m;
+  for (int r = threadIdx.x; r < m; r += blockDim.x) {
+    double l = fmax(lbg[r] - g[r], -PL_OSQP_INFTY);
+    double u = fmin(ubg[r] - g[r], PL_OSQP_INFTY);
+    double lsr = E[r] * l, usr = E[r] * u;
+    ls[r] = lsr;
+    us[r] = usr;
+    double rr;
+    if (lsr < -PL_OSQP_INFTY * PL_MIN_SCALING && usr > PL_OSQP_INFTY * PL_MIN_SCALING) rr = PL_RHO_MIN;
+    else if (usr - lsr < PL_RHO_TOL) rr = PL_RHO_EQ_OVER_INEQ * st.rho;
+    else rr = st.rho;
+    rho[r] = rr;
+  }
+}
+
+void launch_qp_setup(PlOcpHandle* h) {
+  hipLaunchKernelGGL(k_qp_setup, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz, h->set);
+}
+
+// ---------------------------------------------------------------------------
+// Block factorisation: for i = 0..N
+//   Kt_ii = diag(P + sigma) + sum_{rows of node i} rho a a^T |_{w_i}
+//         + sum_{coupling rows of node i-1} rho a a^T |_{dx_i} - C_i
+//   S_i = Kt_ii^-1 (Gauss-Jordan, register-blocked 7x7 per thread)
+//   Kc  = K_{i+1,i} (coupling rows of node i),  U = Kc S_i,  C_{i+1} = U Kc^T.
+// One workgroup (256 threads = 16 x 16 blocks of 7x7) per problem.
+#define FB 7
+#define FG 16
+#define FCH 16  // rows per assembly chunk
+
+namespace {
+
+// Fill the dense chunk buf[s][c - c0] (c in [c0, c0 + W)) with the scaled A
+// entries of rows rows[s] of node i; rw[s] = rho of the row.
+__device__ void fill_chunk(const PlDev& d, const double* As, const double* rho, int i, const int* rows, int nr,
+                           int c0, int W, double* buf, double* rw) {
+  const PlNode& nd = d.nodes[i];
+  for (int t = threadIdx.x; t < FCH * W; t += blockDim.x) buf[t] = 0.0;
+  __syncthreads();
+  const int* rp = d.rowptr + nd.rowptr_off;
+  const int* re = d.rowent + nd.csr_off;
+  for (int s = threadIdx.x / 16; s < nr; s += blockDim.x / 16) {
+    const int lr = rows[s];
+    for (int q = rp[lr] + (threadIdx.x & 15); q < rp[lr + 1]; q += 16) {
+      const int e = re[q];
+      const int lc = d.entcol[nd.ent_off + e];
+      if (lc >= c0 && lc < c0 + W) buf[s * W + (lc - c0)] = As[nd.ent_off + e];
+    }
+    if ((threadIdx.x & 15) == 0) rw[s] = rho[nd.row_off + lr];
+  }
+  __syncthreads();
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_factor(PlDev d, int N, int n, int m, int nnz, int ndx, int S_stride,
+                                                int nw_max, double sigma) {
+  const int b = blockIdx.x;
+  extern __shared__ double lds[];
+  double* big = lds;                          // nw_max^2 (S) or FCH * ncol chunk
+  double* C = big + nw_max * nw_max;          // ndx^2
+  double* rk = C + ndx * ndx;                 // 2 x 112
+  double* ck = rk + 2 * 112;                  // 2 x 112
+  double* rw = ck + 2 * 112;                  // FCH
+  __shared__ int rows_s[FCH];
+  const int ty = threadIdx.x / FG, tx = threadIdx.x % FG;
+  const double* As = d.As + (size_t)b * nnz;
+  const double* rho = d.rho + (size_t)b * m;
+  const double* Ps = d.Ps + (size_t)b * n;
+  double* Sg = d.S + (size_t)b * S_stride;
+  double* Kc = d.Kc + (size_t)b * ndx * nw_max;
+  double* Uc = d.Uc + (size_t)b * ndx * nw_max;
+
+  for (int i = 0; i <= N; ++i) {
+    const PlNode nd = d.nodes[i];
+    const int nw = nd.nw;
+    // ---- coupling block Kc = K_{i+1,i}[a][c] = sum_{coupling rows} rho a_{nw+a} a_c
+    if (i < N) {
+      const int W = nd.ncol;
+      for (int el = threadIdx.x; el < ndx * nw; el += blockDim.x) Kc[el] = 0.0;
+      for (int r0 = 0; r0 < nd.ncpl; r0 += FCH) {
+        const int nr = min(FCH, nd.ncpl - r0);
+        __syncthreads();
+        if (threadIdx.x < nr) rows_s[threadIdx.x] = d.cplrow[nd.cpl_off + r0 + threadIdx.x];
+        __syncthreads();
+        fill_chunk(d, As, rho, i, rows_s, nr, 0, W, big, rw);
+        for (int el = threadIdx.x; el < ndx * nw; el += blockDim.x) {
+          const int aa = el / nw, cc = el - aa * nw;
+          double acc = Kc[el];
+          for (int s = 0; s < nr; ++s) acc += rw[s] * big[s * W + nw + aa] * big[s * W + cc];
+          Kc[el] = acc;
+        }
+        __syncthreads();
+      }
+    }
+    double Kr[FB][FB];
+    // ---- diagonal, padding, Schur complement from node i-1
+#pragma unroll
+    for (int rr = 0; rr < FB; ++rr)
+#pragma unroll
+      for (int cc = 0; cc < FB; ++cc) {
+        const int gi = FB * ty + rr, gj = FB * tx + cc;
+        double v = 0.0;
+        if (gi == gj) v = (gi < nw) ? Ps[nd.x_off + gi] + sigma : 1.0;
+        if (i > 0 && gi < ndx && gj < ndx) v -= C[gi * ndx + gj];
+        Kr[rr][cc] = v;
+      }
+    __syncthreads();  // C consumed
+    // ---- rows of node i on the w_i columns
+    if (i < N) {
+      const int W = nd.ncol;
+      for (int r0 = 0; r0 < nd.nrow; r0 += FCH) {
+        const int nr = min(FCH, nd.nrow - r0);
+        if (threadIdx.x < nr) rows_s[threadIdx.x] = r0 + threadIdx.x;
+        __syncthreads();
+        fill_chunk(d, As, rho, i, rows_s, nr, 0, W, big, rw);
+        for (int s = 0; s < nr; ++s) {
+          const double* a = big + s * W;
+          const double w = rw[s];
+          double ar[FB], ac[FB];
+#pragma unroll
+          for (int k = 0; k < FB; ++k) {
+            const int gi = FB * ty + k, gj = FB * tx + k;
+            ar[k] = gi < nw ? w * a[gi] : 0.0;
+            ac[k] = gj < nw ? a[gj] : 0.0;
+          }
+#pragma unroll
+          for (int rr = 0; rr < FB; ++rr)
+#pragma unroll
+            for (int cc = 0; cc < FB; ++cc) Kr[rr][cc] += ar[rr] * ac[cc];
+        }
+        __syncthreads();
+      }
+    }
+    // ---- coupling rows of node i-1 on dx_i
+    if (i > 0) {
+      const PlNode pv = d.nodes[i - 1];
+      for (int r0 = 0; r0 < pv.ncpl; r0 += FCH) {
+        const int nr = min(FCH, pv.ncpl - r0);
+        if (threadIdx.x < nr) rows_s[threadIdx.x] = d.cplrow[pv.cpl_off + r0 + threadIdx.x];
+        __syncthreads();
+        fill_chunk(d, As, rho, i - 1, rows_s, nr, pv.nw, ndx, big, rw);
+        for (int s = 0; s < nr; ++s) {
+          const double* a = big + s * ndx;
+          const double w = rw[s];
+          double ar[FB], ac[FB];
+#pragma unroll
+          for (int k = 0; k < FB; ++k) {
+            const int gi = FB * ty + k, gj = FB * tx + k;
+            ar[k] = gi < ndx ? w * a[gi] : 0.0;
+            ac[k] = gj < ndx ? a[gj] : 0.0;
+          }
+#pragma unroll
+          for (int rr = 0; rr < FB; ++rr)
+#pragma unroll
+            for (int cc = 0; cc < FB; ++cc) Kr[rr][cc] += ar[rr] * ac[cc];
+        }
+        __syncthreads();
+      }
+    }
+    // ---- in-place Gauss-Jordan inversion (SPD, no pivoting)
+    for (int k = 0; k < nw; ++k) {
+      double* rkb = rk + (k & 1) * 112;
+      double* ckb = ck + (k & 1) * 112;
+      const int kb = k / FB, kr = k - kb * FB;
+      if (ty == kb) {
+#pragma unroll
+        for (int rr = 0; rr < FB; ++rr)
+          if (rr == kr)
+#pragma unroll
+            for (int cc = 0; cc < FB; ++cc) rkb[FB * tx + cc] = Kr[rr][cc];
+      }
+      if (tx == kb) {
+#pragma unroll
+        for (int cc = 0; cc < FB; ++cc)
+          if (cc == kr)
+#pragma unroll
+            for (int rr = 0; rr < FB; ++rr) ckb[FB * ty + rr] = Kr[rr][cc];
+      }
+      __syncthreads();
+      const double pinv = 1.0 / rkb[k];
+      double cv[FB], rv[FB];
+#pragma unroll
+      for (int q = 0; q < FB; ++q) {
+        cv[q] = ckb[FB * ty + q];
+        rv[q] = rkb[FB * tx + q];
+      }
+#pragma unroll
+      for (int rr = 0; rr < FB; ++rr)
+#pragma unroll
+        for (int cc = 0; cc < FB; ++cc) {
+          const int gi = FB * ty + rr, gj = FB * tx + cc;
+          double v = Kr[rr][cc];
+          if (gi == k && gj == k) v = pinv;
+          else if (gi == k) v = rv[cc] * pinv;
+          else if (gj == k) v = -cv[rr] * pinv;
+          else v = v - cv[rr] * (rv[cc] * pinv);
+          Kr[rr][cc] = v;
+        }
+    }
+    __syncthreads();
+    // ---- store S_i: tiled global layout + dense copy in LDS (stride nw)
+    {
+      const int nunit = nd.nunit;
+      double* Sn = Sg + nd.s_off;
+#pragma unroll
+      for (int rr = 0; rr < FB; ++rr)
+#pragma unroll
+        for (int cc = 0; cc < FB; ++cc) {
+          const int gi = FB * ty + rr, gj = FB * tx + cc;
+          const int I = gi >> 3, J = gj >> 3;
+          if (I < nd.ntile && J <= I) {
+            const double v = (gi < nw && gj < nw) ? Kr[rr][cc] : 0.0;
+            const int t = I * (I + 1) / 2 + J;
+            const int h = (gj & 7) >> 2;
+            const int u = 2 * t + h;
+            const int pos = (gi & 7) * 4 + (gj & 3);
+            Sn[((pos >> 1) * nunit + u) * 2 + (pos & 1)] = v;
+          }
+          if (gi < nw && gj < nw) big[gi * nw + gj] = Kr[rr][cc];
+        }
+    }
+    __syncthreads();
+    if (i == N) break;
+    // ---- U = Kc S (ndx x nw), then C = U Kc^T (ndx x ndx)
+    for (int el = threadIdx.x; el < ndx * nw; el += blockDim.x) {
+      const int aa = el / nw, cc = el - aa * nw;
+      const double* kr = Kc + aa * nw;
+      double acc = 0.0;
+      for (int k = 0; k < nw; ++k) acc += kr[k] * big[k * nw + cc];
+      Uc[el] = acc;
+    }
+    __syncthreads();
+    for (int el = threadIdx.x; el < ndx * ndx; el += blockDim.x) {
+      const int aa = el / ndx, bb = el - aa * ndx;
+      const double* ur = Uc + aa * nw;
+      const double* kr = Kc + bb * nw;
+      double acc = 0.0;
+      for (int k = 0; k < nw; ++k) acc += ur[k] * kr[k];
+      C[el] = acc;
+    }
+    __syncthreads();
+  }
+}
+
+void launch_factor(PlOcpHandle* h) {
+  const size_t lds = sizeof(double) * ((size_t)h->nw_max * h->nw_max + (size_t)h->ndx * h->ndx + 4 * 112 + FCH);
+  hipLaunchKernelGGL(k_factor, dim3(h->B), dim3(256), lds, h->stream, h->d, h->N, h->n, h->m, h->nnz, h->ndx,
+                     h->S_stride, h->nw_max, h->set.sigma);
+}
+
+// ---------------------------------------------------------------------------
+// ADMM (OSQP 0.6 osqp_solve loop).  One workgroup per problem runs `niter`
+// iterations; the last one stores delta_x / delta_y for the termination check.
+namespace {
+
+struct AdmmLds {
+  double* v;      // mat-vec input (padded to 8 * ntile)
+  double* y;      // mat-vec output / w_i
+  double* xn;     // x~ of node i+1 (dx part)
+  double* trow;   // per local row temporaries (coupling t_r, s_r)
+  double* dpart;  // [nunit][8]
+  double* tpart;  // [nunit][4]
+};
+
+// y[0..nw) = S v for the node's tiled block; v must hold zeros past nw.
+__device__ void sym_matvec(const double* __restrict__ Sn, int nunit, int ntile, int nw, const double* v,
+                           double* y, double* dpart, double* tpart) {
+  const int u = threadIdx.x;
+  if (u < nunit) {
+    double2 T[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) T[k] = reinterpret_cast<const double2*>(Sn)[k * nunit + u];
+    const int t = u >> 1, h = u & 1;
+    int I = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+    while (I * (I + 1) / 2 > t) --I;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    const int J = t - I * (I + 1) / 2;
+    double vj[4], vi[8];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) vj[c] = v[8 * J + 4 * h + c];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) vi[r] = v[8 * I + r];
+    double tp[4] = {0.0, 0.0, 0.0, 0.0};
+    // element (r, c) is pair (r*4+c)/2, slot (r*4+c)&1
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const double e0 = T[2 * r].x, e1 = T[2 * r].y, e2 = T[2 * r + 1].x, e3 = T[2 * r + 1].y;
+      dpart[u * 8 + r] = e0 * vj[0] + e1 * vj[1] + e2 * vj[2] + e3 * vj[3];
+      tp[0] += e0 * vi[r];
+      tp[1] += e1 * vi[r];
+      tp[2] += e2 * vi[r];
+      tp[3] += e3 * vi[r];
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) tpart[u * 4 + c] = (I != J) ? tp[c] : 0.0;
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < nw; o += blockDim.x) {
+    const int I = o >> 3, r = o & 7;
+    double acc = 0.0;
+    for (int J = 0; J <= I; ++J) {
+      const int t = I * (I + 1) / 2 + J;
+      acc += dpart[(2 * t) * 8 + r] + dpart[(2 * t + 1) * 8 + r];
+    }
+    for (int Ip = I + 1; Ip < ntile; ++Ip) {
+      const int t = Ip * (Ip + 1) / 2 + I;
+      acc += tpart[(2 * t + (r >> 2)) * 4 + (r & 3)];
+    }
+    y[o] = acc;
+  }
+  __syncthreads();
+}
+
+}  // namespace
+
+// rhs = sigma x - q + A^T (rho z - y)   (before the first iteration of a solve)
+__global__ __launch_bounds__(256) void k_admm_init(PlDev d, int N, int n, int m, int nnz, double sigma) {
+  const int b = blockIdx.x;
+  if (d.info[b].done) return;
+  const double* As = d.As + (size_t)b * nnz;
+  const double* za = d.za + (size_t)b * m;
+  const double* ya = d.ya + (size_t)b * m;
+  const double* rho = d.rho + (size_t)b * m;
+  const double* xa = d.xa + (size_t)b * n;
+  const double* qs = d.qs + (size_t)b * n;
+  double* rhs = d.rhs + (size_t)b * n;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    double acc = sigma * xa[j] - qs[j];
+    for_col_entries(d, N, j, [&](int e, int r) { acc += As[e] * (rho[r] * za[r] - ya[r]); });
+    rhs[j] = acc;
+  }
+}
+
+void launch_admm_init(PlOcpHandle* h) {
+  hipLaunchKernelGGL(k_admm_init, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz,
+                     h->set.sigma);
+}
+
+__global__ __launch_bounds__(256) void k_admm(PlDev d, int N, int n, int m, int nnz, int ndx, int S_stride,
+                                              int nw_max, int nunit_max, int nrow_max, int niter, int check,
+                                              double sigma, double alpha) {
+  const int b = blockIdx.x;
+  PlProbInfo* info = d.info + b;
+  if (info->done) return;
+  extern __shared__ double lds[];
+  const int vpad = ((nw_max + 7) / 8) * 8;
+  AdmmLds L;
+  L.v = lds;
+  L.y = L.v + vpad;
+  L.xn = L.y + vpad;
+  L.trow = L.xn + vpad;
+  L.dpart = L.trow + nrow_max;
+  L.tpart = L.dpart + 8 * nunit_max;
+  const double* As = d.As + (size_t)b * nnz;
+  const double* rho = d.rho + (size_t)b * m;
+  const double* ls = d.ls + (size_t)b * m;
+  const double* us = d.us + (size_t)b * m;
+  const double* qs = d.qs + (size_t)b * n;
+  const double* Sg = d.S + (size_t)b * S_stride;
+  double* za = d.za + (size_t)b * m;
+  double* ya = d.ya + (size_t)b * m;
+  double* xa = d.xa + (size_t)b * n;
+  double* rhs = d.rhs + (size_t)b * n;
+  double* bt = d.bt + (size_t)b * n;
+  double* dxs = d.dxs + (size_t)b * n;
+  double* dys = d.dys + (size_t)b * m;
+  const PlNode* nodes = d.nodes;
+
+  for (int it = 0; it < niter; ++it) {
+    const bool store_delta = check && (it == niter - 1);
+    // ================= forward sweep
+    for (int i = 0; i <= N; ++i) {
+      const PlNode nd = nodes[i];
+      const int nw = nd.nw;
+      // coupling t_r = rho_r * a_r(w_{i-1}) . w_{i-1} for coupling rows of node i-1
+      if (i > 0) {
+        const PlNode pv = nodes[i - 1];
+        const int* rp = d.rowptr + pv.rowptr_off;
+        const int* re = d.rowent + pv.csr_off;
+        for (int s = threadIdx.x; s < pv.ncpl; s += blockDim.x) {
+          const int lr = d.cplrow[pv.cpl_off + s];
+          double acc = 0.0;
+          for (int q = rp[lr]; q < rp[lr + 1]; ++q) {
+            const int e = re[q];
+            const int lc = d.entcol[pv.ent_off + e];
+            if (lc < pv.nw) acc += As[pv.ent_off + e] * L.y[lc];
+          }
+          L.trow[lr] = rho[pv.row_off + lr] * acc;
+        }
+        __syncthreads();
+      }
+      // bt_i = rhs_i - K_{i,i-1} w_{i-1}
+      for (int c = threadIdx.x; c < ((nw + 7) & ~7); c += blockDim.x) {
+        double v = 0.0;
+        if (c < nw) {
+          v = rhs[nd.x_off + c];
+          if (i > 0 && c < ndx) {
+            const PlNode pv = nodes[i - 1];
+            const int* cp = d.colptr + pv.colptr_off;
+            const int col = pv.nw + c;
+            double acc = 0.0;
+            for (int e = cp[col]; e < cp[col + 1]; ++e) acc += As[pv.ent_off + e] * L.trow[d.rowidx[pv.ent_off + e]];
+            v -= acc;
+          }
+          bt[nd.x_off + c] = v;
+        }
+        L.v[c] = v;
+      }
+      __syncthreads();
+      sym_matvec(Sg + nd.s_off, nd.nunit, nd.ntile, nw, L.v, L.y, L.dpart, L.tpart);
+      // zero the coupling temporaries of node i-1 rows that were written
+      if (i > 0) {
+        const PlNode pv = nodes[i - 1];
+        for (int s = threadIdx.x; s < pv.ncpl; s += blockDim.x) L.trow[d.cplrow[pv.cpl_off + s]] = 0.0;
+      }
+      __syncthreads();
+    }
+    // ================= backward sweep
+    for (int i = N; i >= 0; --i) {
+      const PlNode nd = nodes[i];
+      const int nw = nd.nw;
+      // coupling t_r = rho_r * a_r(dx_{i+1}) . x~_{i+1}
+      if (i < N) {
+        const int* rp = d.rowptr + nd.rowptr_off;
+        const int* re = d.rowent + nd.csr_off;
+        for (int s = threadIdx.x; s < nd.ncpl; s += blockDim.x) {
+          const int lr = d.cplrow[nd.cpl_off + s];
+          double acc = 0.0;
+          for (int q = rp[lr]; q < rp[lr + 1]; ++q) {
+            const int e = re[q];
+            const int lc = d.entcol[nd.ent_off + e];
+            if (lc >= nw) acc += As[nd.ent_off + e] * L.xn[lc - nw];
+          }
+          L.trow[lr] = rho[nd.row_off + lr] * acc;
+        }
+        __syncthreads();
+      }
+      // v = bt_i - K_{i+1,i}^T x~_{i+1}
+      for (int c = threadIdx.x; c < ((nw + 7) & ~7); c += blockDim.x) {
+        double v = 0.0;
+        if (c < nw) {
+          v = bt[nd.x_off + c];
+          if (i < N) {
+            const int* cp = d.colptr + nd.colptr_off;
+            double acc = 0.0;
+            for (int e = cp[c]; e < cp[c + 1]; ++e) acc += As[nd.ent_off + e] * L.trow[d.rowidx[nd.ent_off + e]];
+            v -= acc;
+          }
+        }
+        L.v[c] = v;
+      }
+      __syncthreads();
+      if (i < N) {
+        for (int s = threadIdx.x; s < nd.ncpl; s += blockDim.x) L.trow[d.cplrow[nd.cpl_off + s]] = 0.0;
+      }
+      sym_matvec(Sg + nd.s_off, nd.nunit, nd.ntile, nw, L.v, L.y, L.dpart, L.tpart);
+      // L.y = x~_i.  Rows of node i: z~ = A x~, relaxed z / y updates (update_z, update_y)
+      for (int lr = threadIdx.x; lr < nd.nrow; lr += blockDim.x) {
+        const int r = nd.row_off + lr;
+        const int* rp = d.rowptr + nd.rowptr_off;
+        const int* re = d.rowent + nd.csr_off;
+        double zt = 0.0;
+        for (int q = rp[lr]; q < rp[lr + 1]; ++q) {
+          const int e = re[q];
+          const int lc = d.entcol[nd.ent_off + e];
+          zt += As[nd.ent_off + e] * (lc < nw ? L.y[lc] : L.xn[lc - nw]);
+        }
+        const double zp = za[r], yv = ya[r], rr = rho[r];
+        const double zrel = alpha * zt + (1.0 - alpha) * zp;
+        double zn = zrel + (1.0 / rr) * yv;
+        zn = fmin(fmax(zn, ls[r]), us[r]);
+        const double dy = rr * (zrel - zn);
+        const double yn = yv + dy;
+        za[r] = zn;
+        ya[r] = yn;
+        if (store_delta) dys[r] = dy;
+        L.trow[lr] = rr * zn - yn;  // s_r for the next rhs
+      }
+      __syncthreads();
+      // x update and next-iteration rhs contributions of the rows of node i
+      for (int c = threadIdx.x; c < nw; c += blockDim.x) {
+        const int j = nd.x_off + c;
+        const double xp = xa[j];
+        const double xn = alpha * L.y[c] + (1.0 - alpha) * xp;
+        xa[j] = xn;
+        if (store_delta) dxs[j] = xn - xp;
+        double acc = sigma * xn - qs[j];
+        if (i < N) {
+          const int* cp = d.colptr + nd.colptr_off;
+          for (int e = cp[c]; e < cp[c + 1]; ++e) acc += As[nd.ent_off + e] * L.trow[d.rowidx[nd.ent_off + e]];
+        }
+        rhs[j] = acc;
+      }
+      if (i < N) {
+        const int* cp = d.colptr + nd.colptr_off;
+        for (int c = threadIdx.x; c < ndx; c += blockDim.x) {
+          double acc = 0.0;
+          for (int e = cp[nw + c]; e < cp[nw + c + 1]; ++e) acc += As[nd.ent_off + e] * L.trow[d.rowidx[nd.ent_off + e]];
+          rhs[nodes[i + 1].x_off + c] += acc;
+        }
+      }
+      __syncthreads();
+      for (int c = threadIdx.x; c < ndx; c += blockDim.x) L.xn[c] = L.y[c];
+      for (int lr = threadIdx.x; lr < nd.nrow; lr += blockDim.x) L.trow[lr] = 0.0;
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) info->iter += niter;
+}
+
+void launch_admm(PlOcpHandle* h, int niter, int check, int it_base) {
+  (void)it_base;
+  const int vpad = ((h->nw_max + 7) / 8) * 8;
+  const size_t lds = sizeof(double) * (3 * (size_t)vpad + h->nrow_max + 12 * (size_t)h->nunit_max);
+  hipLaunchKernelGGL(k_admm, dim3(h->B), dim3(256), lds, h->stream, h->d, h->N, h->n, h->m, h->nnz, h->ndx,
+                     h->S_stride, h->nw_max, h->nunit_max, h->nrow_max, niter, check, h->set.sigma, h->set.alpha);
+}
+
+// ---------------------------------------------------------------------------
+// Termination (OSQP 0.6 update_info + check_termination, incl. infeasibility
+// certificates and the x10 "approximate" check at max_iter).
+__global__ __launch_bounds__(256) void k_check(PlDev d, int N, int n, int m, int nnz, PlSettings st, int final_check) {
+  const int b = blockIdx.x;
+  PlProbInfo* info = d.info + b;
+  if (info->done) return;
+  __shared__ double red[256];
+  const double* As = d.As + (size_t)b * nnz;
+  const double* za = d.za + (size_t)b * m;
+  const double* ya = d.ya + (size_t)b * m;
+  const double* xa = d.xa + (size_t)b * n;
+  const double* qs = d.qs + (size_t)b * n;
+  const double* Ps = d.Ps + (size_t)b * n;
+  const double* D = d.D + (size_t)b * n;
+  const double* E = d.E + (size_t)b * m;
+  const double* ls = d.ls + (size_t)b * m;
+  const double* us = d.us + (size_t)b * m;
+  const double* dxs = d.dxs + (size_t)b * n;
+  const double* dys = d.dys + (size_t)b * m;
+  const double c = d.cs[b], cinv = 1.0 / c;
+  // primal: ||E^-1 (A x - z)||, ||E^-1 z||, ||E^-1 A x||
+  double pri = 0.0, nz = 0.0, nax = 0.0;
+  for (int r = threadIdx.x; r < m; r += blockDim.x) {
+    double ax = 0.0;
+    for_row_entries(d, r, [&](int e, int j) { ax += As[e] * xa[j]; });
+    const double ei = 1.0 / E[r];
+    pri = fmax(pri, fabs(ei * (ax - za[r])));
+    nz = fmax(nz, fabs(ei * za[r]));
+    nax = fmax(nax, fabs(ei * ax));
+  }
+  pri = block_max(pri, red);
+  nz = block_max(nz, red);
+  nax = block_max(nax, red);
+  // dual: c^-1 ||D^-1 (P x + q + A^T y)||, ||D^-1 q||, ||D^-1 A^T y||, ||D^-1 P x||
+  double dua = 0.0, nq = 0.0, naty = 0.0, npx = 0.0;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    double aty = 0.0;
+    for_col_entries(d, N, j, [&](int e, int r) { aty += As[e] * ya[r]; });
+    const double di = 1.0 / D[j];
+    const double px = Ps[j] * xa[j];
+    dua = fmax(dua, fabs(di * (px + qs[j] + aty)));
+    nq = fmax(nq, fabs(di * qs[j]));
+    naty = fmax(naty, fabs(di * aty));
+    npx = fmax(npx, fabs(di * px));
+  }
+  dua = cinv * block_max(dua, red);
+  nq = block_max(nq, red);
+  naty = block_max(naty, red);
+  npx = block_max(npx, red);
+  __shared__ int s_status;
+  for (int pass = 0; pass < (final_check ? 2 : 1); ++pass) {
+    const bool approx = (pass == 1);
+    const double mul = approx ? 10.0 : 1.0;
+    const double eps_abs = st.eps_abs * mul, eps_rel = st.eps_rel * mul;
+    const double eps_pinf = st.eps_prim_inf * mul, eps_dinf = st.eps_dual_inf * mul;
+    int status = PL_ST_UNSOLVED;
+    if (pri > PL_OSQP_INFTY || dua > PL_OSQP_INFTY) {
+      status = PL_ST_NON_CVX;
+    } else {
+      const double eps_pri = eps_abs + eps_rel * fmax(nz, nax);
+      const double eps_dua = eps_abs + eps_rel * cinv * fmax(nq, fmax(naty, npx));
+      const bool prim_ok = pri < eps_pri;
+      const bool dual_ok = dua < eps_dua;
+      bool prim_inf = false, dual_inf = false;
+      if (!prim_ok) {
+        // project delta_y onto the polar of the recession cone, ||E dy||
+        double ndy = 0.0, ineq = 0.0;
+        for (int r = threadIdx.x; r < m; r += blockDim.x) {
+          double dy = dys[r];
+          const bool uinf = us[r] > PL_OSQP_INFTY * PL_MIN_SCALING, linf = ls[r] < -PL_OSQP_INFTY * PL_MIN_SCALING;
+          if (uinf && linf) dy = 0.0;
+          else if (uinf) dy = fmin(dy, 0.0);
+          else if (linf) dy = fmax(dy, 0.0);
+          ndy = fmax(ndy, fabs(E[r] * dy));
+          ineq += us[r] * fmax(dy, 0.0) + ls[r] * fmin(dy, 0.0);
+        }
+        ndy = block_max(ndy, red);
+        ineq = block_sum(ineq, red);
+        if (ndy > PL_DIV_TOL && ineq < eps_pinf * ndy) {
+          double natdy = 0.0;
+          for (int j = threadIdx.x; j < n; j += blockDim.x) {
+            double s = 0.0;
+            for_col_entries(d, N, j, [&](int e, int r) {
+              double dy = dys[r];
+              const bool uinf = us[r] > PL_OSQP_INFTY * PL_MIN_SCALING, linf = ls[r] < -PL_OSQP_INFTY * PL_MIN_SCALING;
+              if (uinf && linf) dy = 0.0;
+              else if (uinf) dy = fmin(dy, 0.0);
+              else if (linf) dy = fmax(dy, 0.0);
+              s += As[e] * dy;
+            });
+            natdy = fmax(natdy, fabs(s / D[j]));
+          }
+          natdy = block_max(natdy, red);
+          prim_inf = natdy < eps_pinf * ndy;
+        }
+      }
+      if (!dual_ok) {
+        double ndx_ = 0.0, qdx = 0.0, npdx = 0.0;
+        for (int j = threadIdx.x; j < n; j += blockDim.x) {
+          ndx_ = fmax(ndx_, fabs(D[j] * dxs[j]));
+          qdx += qs[j] * dxs[j];
+          npdx = fmax(npdx, fabs(Ps[j] * dxs[j] / D[j]));
+        }
+        ndx_ = block_max(ndx_, red);
+        qdx = block_sum(qdx, red);
+        npdx = block_max(npdx, red);
+        if (ndx_ > PL_DIV_TOL && qdx < c * eps_dinf * ndx_ && npdx < c * eps_dinf * ndx_) {
+          int bad = 0;
+          for (int r = threadIdx.x; r < m; r += blockDim.x) {
+            double adx = 0.0;
+            for_row_entries(d, r, [&](int e, int j) { adx += As[e] * dxs[j]; });
+            adx /= E[r];
+            if ((us[r] < PL_OSQP_INFTY * PL_MIN_SCALING && adx > eps_dinf * ndx_) ||
+                (ls[r] > -PL_OSQP_INFTY * PL_MIN_SCALING && adx < -eps_dinf * ndx_))
+              bad = 1;
+          }
+          dual_inf = block_max((double)bad, red) == 0.0;
+        }
+      }
+      if (prim_ok && dual_ok) status = approx ? PL_ST_SOLVED_INACCURATE : PL_ST_SOLVED;
+      else if (prim_inf) status = approx ? PL_ST_PRIMAL_INF_INACC : PL_ST_PRIMAL_INF;
+      else if (dual_inf) status = approx ? PL_ST_DUAL_INF_INACC : PL_ST_DUAL_INF;
+    }
+    if (threadIdx.x == 0) {
+      info->pri_res = pri;
+      info->dua_res = dua;
+      if (status != PL_ST_UNSOLVED) {
+        info->status = status;
+        info->done = 1;
+      } else if (approx) {
+        info->status = PL_ST_MAX_ITER;
+        info->done = 1;
+      }
+      s_status = info->done;
+    }
+    __syncthreads();
+    if (s_status) break;
+  }
+}
+
+void launch_check(PlOcpHandle* h, int it, int final_check) {
+  (void)it;
+  hipLaunchKernelGGL(k_check, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz, h->set,
+                     final_check);
+}
+
+// Unscaled solution dx = D x (store_solution); NaN + cold start on infeasibility.
+__global__ __launch_bounds__(256) void k_unscale(PlDev d, int n, int m) {
+  const int b = blockIdx.x;
+  const PlProbInfo info = d.info[b];
+  const bool bad = info.status == PL_ST_PRIMAL_INF || info.status == PL_ST_PRIMAL_INF_INACC ||
+                   info.status == PL_ST_DUAL_INF || info.status == PL_ST_DUAL_INF_INACC || info.status == PL_ST_NON_CVX;
+  double* step = d.step + (size_t)b * n;
+  double* xa = d.xa + (size_t)b * n;
+  const double* D = d.D + (size_t)b * n;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    step[j] = bad ? __builtin_nan("") : D[j] * xa[j];
+    if (bad) xa[j] = 0.0;
+  }
+  if (bad) {
+    for (int r = threadIdx.x; r < m; r += blockDim.x) {
+      d.za[(size_t)b * m + r] = 0.0;
+      d.ya[(size_t)b * m + r] = 0.0;
+    }
+  }
+}
+
+void launch_unscale(PlOcpHandle* h) {
+  hipLaunchKernelGGL(k_unscale, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, h->m);
+}
+
+__global__ void k_reset_info(PlDev d, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  PlProbInfo& I = d.info[b];
+  I.status = PL_ST_UNSOLVED;
+  I.iter = 0;
+  I.done = 0;
+}
+
+void launch_reset_info(PlOcpHandle* h) {
+  hipLaunchKernelGGL(k_reset_info, dim3((h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B);
+}
+
+// Cold start of the ADMM iterates (OSQP setup state: x = z = y = 0).
+__global__ void k_zero(double* p, size_t len) {
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < len; t += (size_t)gridDim.x * blockDim.x) p[t] = 0.0;
+}
+
+void launch_reset_iterates(PlOcpHandle* h) {
+  hipLaunchKernelGGL(k_zero, dim3(1024), dim3(256), 0, h->stream, h->d.xa, (size_t)h->B * h->n);
+  hipLaunchKernelGGL(k_zero, dim3(1024), dim3(256), 0, h->stream, h->d.za, (size_t)h->B * h->m);
+  hipLaunchKernelGGL(k_zero, dim3(1024), dim3(256), 0, h->stream, h->d.ya, (size_t)h->B * h->m);
+}

@@ -1,0 +1,172 @@
+// Per-node constraint rows of the OCP, templated on the scalar (double / Dual).
+//
+// Emits g, lbg, ubg of one horizon node in the reference's subject_to order:
+//   node 0 starts with DX_0 == 0                          (optimization/ocp.py:109)
+//   setup_dynamics_constraints(i)                          (ocp_whole_body_rnea.py:138-171,
+//                                                           ocp_whole_body_acc.py:90-112,
+//                                                           ocp_whole_body_aba.py:86-106)
+//   per foot FR, FL, RR, RL: friction cone, swing force, no-slip, swing height
+//                                                          (ocp.py:121-157)
+//   external force, arm velocity, joint limits             (ocp.py:165-190)
+// The block list per node type is built on the host (api.cpp: build_blocks) so
+// the row order has one definition shared by the layout code and this emitter.
+#pragma once
+#include "rbd.h"
+
+namespace pl {
+
+// OCS2 cubic swing spline (utils/gait_sequence.py:96-133), evaluated in double
+// (it depends on parameters only).
+PL_HD double spline_vel_z(double phase, double period, double h_max, double v_lo, double v_td) {
+  double mid = period / 2.0;
+  double t = phase * period;
+  double t0, dt, c1, c2, c3;
+  if (phase < 0.5) {
+    t0 = 0.0; dt = mid - 0.0;
+    double p0 = 0.0, v0 = v_lo, p1 = h_max, v1 = 0.0;
+    double dpos = p1 - p0, dvel = v1 - v0;
+    c1 = v0 * dt; c2 = -(3.0 * v0 + dvel) * dt + 3.0 * dpos; c3 = (2.0 * v0 + dvel) * dt - 2.0 * dpos;
+  } else {
+    t0 = mid; dt = period - mid;
+    double p0 = h_max, v0 = 0.0, p1 = 0.0, v1 = v_td;
+    double dpos = p1 - p0, dvel = v1 - v0;
+    c1 = v0 * dt; c2 = -(3.0 * v0 + dvel) * dt + 3.0 * dpos; c3 = (2.0 * v0 + dvel) * dt - 2.0 * dpos;
+  }
+  double tn = (t - t0) / dt;
+  return (3.0 * c3 * tn * tn + 2.0 * c2 * tn + c1) / dt;
+}
+
+PL_HD int node_type(const PlOcpConst& O, int i) { return i == 0 ? 0 : (i < O.tau_nodes ? 1 : 2); }
+PL_HD int node_nu(const PlOcpConst& O, int i) {
+  if (O.dyn == PL_DYN_RNEA) return O.na + O.nf + (i < O.tau_nodes ? O.nj : 0);
+  if (O.dyn == PL_DYN_ACC) return O.nv + O.nf;
+  return O.nj + O.nf;
+}
+
+// Geometric step size dt_i (ocp.py:71-74).
+PL_HD double node_dt(const PlOcpConst& O, const double* p, int i) {
+  double dt_min = p[O.P.dt_min], dt_max = p[O.P.dt_max];
+  double gamma = pow(dt_max / dt_min, 1.0 / (double)(O.N - 1));
+  return dt_min * pow(gamma, (double)i);
+}
+
+#define PL_INF (__builtin_inf())
+
+// Input accessor over the node's local columns: x (+ alpha * step) with an
+// optional dual seed.  dx = cols [0, ndx), u = [ndx, nw), dx_{i+1} = [nw, nw+ndx).
+template <class S> struct VecIn;
+template <> struct VecIn<double> {
+  const double* x;
+  const double* step;
+  double alpha;
+  int seed;
+  PL_HD double operator[](int k) const { return step ? x[k] + alpha * step[k] : x[k]; }
+};
+template <> struct VecIn<Dual> {
+  const double* x;
+  const double* step;
+  double alpha;
+  int seed;
+  PL_HD Dual operator[](int k) const { return Dual(x[k], k == seed ? 1.0 : 0.0); }
+};
+template <class S> PL_HD VecIn<S> sub_in(const VecIn<S>& a, int off) {
+  VecIn<S> r = a;
+  r.x = a.x + off;
+  if (a.step) r.step = a.step + off;
+  r.seed = a.seed - off;
+  return r;
+}
+
+template <class S, int DYN, class Emit>
+PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double* p, const VecIn<S>& dx,
+                     const VecIn<S>& u, const VecIn<S>& dxn, Emit& emit) {
+  const int nv = O.nv, nq = O.nq, nj = O.nj;
+  const double* xi = p + O.P.x_init;
+  const double dt = node_dt(O, p, i);
+  const int type = node_type(O, i);
+  // state: q = integrate(x_init.q, dq), v = x_init.v + dv   (ocp_whole_body_rnea.py:173-181)
+  S q[PL_MAXQ], v[PL_MAXV];
+  integrate_q<S>(M, xi, dx, q);
+  for (int k = 0; k < nv; ++k) v[k] = xi[nq + k] + dx[nv + k];
+  const int f_off = (DYN == PL_DYN_RNEA) ? O.na : (DYN == PL_DYN_ACC ? nv : nj);
+  const VecIn<S> a = u;                                   // rnea / acc: a = u[0:nv]
+  const VecIn<S> forces = sub_in(u, f_off);
+  const VecIn<S> tau_j = sub_in(u, DYN == PL_DYN_RNEA ? O.na + O.nf : 0);
+  const bool state_rows = (type != 0);
+  NodeKin<S> kin;
+  constexpr bool want_tau = (DYN != PL_DYN_ABA);
+  if (want_tau || state_rows) tree_pass<S>(M, O, q, v, a, forces, want_tau, state_rows, kin);
+  S aba_a[DYN == PL_DYN_ABA ? PL_MAXV : 1];
+  if constexpr (DYN == PL_DYN_ABA) aba_forward<S>(M, O, q, v, tau_j, forces, aba_a);
+
+  const int nb = O.nblk[type];
+  for (int bi = 0; bi < nb; ++bi) {
+    const PlRowBlock B = O.blk[type][bi];
+    const int k = B.arg;
+    switch (B.kind) {
+      case PL_RB_INIT:
+        for (int r = 0; r < O.ndx; ++r) emit(dx[r], 0.0, 0.0);
+        break;
+      case PL_RB_DYNQ:
+        for (int r = 0; r < nv; ++r) emit(dxn[r] - (dx[r] + v[r] * dt), 0.0, 0.0);
+        break;
+      case PL_RB_DYNV:
+        for (int r = 0; r < nv; ++r) {
+          S ar;
+          if constexpr (DYN == PL_DYN_ABA) ar = aba_a[r];
+          else ar = a[r];
+          emit(dxn[nv + r] - (dx[nv + r] + ar * dt), 0.0, 0.0);
+        }
+        break;
+      case PL_RB_RNEA_BASE:
+        for (int r = 0; r < 6; ++r) emit(kin.tau[r], 0.0, 0.0);
+        break;
+      case PL_RB_TAU_EQ:
+        for (int r = 0; r < nj; ++r) emit(kin.tau[6 + r] - tau_j[r], 0.0, 0.0);
+        break;
+      case PL_RB_TAU_BND:
+        for (int r = 0; r < nj; ++r) emit(tau_j[r], -O.tau_max[r], O.tau_max[r]);
+        break;
+      case PL_RB_FZ: {
+        double c = p[O.P.contact + 4 * i + k];
+        emit(c * forces[3 * k + 2], 0.0, PL_INF);
+      } break;
+      case PL_RB_CONE: {
+        double c = p[O.P.contact + 4 * i + k];
+        S f0 = forces[3 * k], f1 = forces[3 * k + 1], f2 = forces[3 * k + 2];
+        emit(c * (f0 * f0 + f1 * f1) - (c * O.mu * O.mu) * (f2 * f2), -PL_INF, 0.0);
+      } break;
+      case PL_RB_SWINGF: {
+        double c = p[O.P.contact + 4 * i + k];
+        for (int r = 0; r < 3; ++r) emit((1.0 - c) * forces[3 * k + r], 0.0, 0.0);
+      } break;
+      case PL_RB_FVXY: {
+        double c = p[O.P.contact + 4 * i + k];
+        emit(c * kin.foot_vel[k][0], 0.0, 0.0);
+        emit(c * kin.foot_vel[k][1], 0.0, 0.0);
+      } break;
+      case PL_RB_FVZ: {
+        double c = p[O.P.contact + 4 * i + k];
+        double ph = p[O.P.swing + 4 * i + k];
+        double vz_des = spline_vel_z(ph, p[O.P.swing_period], p[O.P.swing_height], p[O.P.swing_vel_limits],
+                                     p[O.P.swing_vel_limits + 1]);
+        S vz = kin.foot_vel[k][2];
+        emit(c * vz + (1.0 - c) * (vz - vz_des), 0.0, 0.0);
+      } break;
+      case PL_RB_EXT:
+        for (int r = 0; r < 3; ++r) emit(forces[3 * O.nfeet + r] - p[O.P.ext_force_des + r], 0.0, 0.0);
+        break;
+      case PL_RB_ARM:
+        for (int r = 0; r < 3; ++r) emit(kin.arm_vel[r] - p[O.P.arm_vel_des + r], 0.0, 0.0);
+        break;
+      case PL_RB_QJ:
+        for (int r = 0; r < nj; ++r) emit(q[7 + r], O.pos_min[r], O.pos_max[r]);
+        break;
+      case PL_RB_VJ:
+        for (int r = 0; r < nj; ++r) emit(v[6 + r], -O.vel_max[r], O.vel_max[r]);
+        break;
+    }
+  }
+}
+
+}  // namespace pl

@@ -1,0 +1,151 @@
+// Internal state of a batched OCP handle (not part of the C-ABI).
+//
+// Memory layout in HBM: every per-problem array is problem-major ([B][len]) so a
+// workgroup that owns one problem streams contiguous memory; structure arrays
+// (sparsity pattern, node tables) are shared by the whole batch and stay in L2.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "model.h"
+
+#define PL_SIGMA_DEFAULT 1e-6
+
+// Per-node structure, identical for every problem of the batch.
+struct PlNode {
+  int nw;          // variables owned by the node: dx_i + u_i (i < N) or dx_N
+  int nu;
+  int x_off;       // global column of dx_i
+  int row_off;     // global row of the node's first row
+  int nrow;        // rows of the node (node 0 includes the DX_0 == 0 rows)
+  int ncol;        // local columns: nw + ndx (dx_{i+1}); 0 for node N
+  int ent_off;     // first entry of the node in the entry arrays
+  int nent;
+  int colptr_off;  // into colptr (ncol + 1 values, relative to ent_off)
+  int rowptr_off;  // into rowptr (nrow + 1 values, relative to the node's CSR list)
+  int csr_off;     // into rowent
+  int ntile;       // 8x8 tiles per dimension of the node's KKT block
+  int nunit;       // (lower tile, half) work units = 2 * ntile (ntile + 1) / 2
+  int s_off;       // offset (doubles) of the node's factor block inside a problem's factor
+  int cpl_off;     // coupling rows (rows with a dx_{i+1} entry): offset into cplrow
+  int ncpl;
+  int pad[2];
+};
+
+struct PlSettings {
+  double rho, sigma, alpha, eps_abs, eps_rel, eps_prim_inf, eps_dual_inf;
+  int max_iter, scaling, check_termination, warm_start;
+};
+
+// Per-problem status/info written by the solver kernels.
+struct PlProbInfo {
+  int status;        // OSQP status code
+  int iter;          // ADMM iterations run
+  int done;          // ADMM terminated
+  int ls_accepted;
+  int ls_branch;
+  int ls_trials;
+  double ls_alpha;
+  double pri_res, dua_res;
+  double eps_pri, eps_dua;
+  double f;          // objective at the returned point
+  double viol_max;   // max bound violation at the returned point (ocp.py:412-414)
+  double norm_dy, norm_dx;  // scratch for infeasibility checks
+};
+
+struct PlDev {
+  // shared structure
+  PlModel* model;
+  PlOcpConst* oc;
+  PlNode* nodes;     // N + 1
+  int* colptr;
+  int* rowidx;       // local row of each entry (CSC order)
+  int* entcol;       // local column of each entry
+  int* rowptr;
+  int* rowent;       // CSR: entry index (local to the node) per row slot
+  int* cplrow;       // coupling rows (local row ids)
+  int* rownode;      // global row -> node
+  int* colnode;      // global column -> node
+  // per problem [B][*]
+  double* p;         // params
+  double* x;         // SQP iterate (decision vector)
+  double* x0;        // SQP iterate at the start of a solve (line search base)
+  double* g;
+  double* lbg;
+  double* ubg;
+  double* grad;
+  double* Araw;      // constraint Jacobian values (nnz)
+  double* P;         // Hessian diagonal (constant, ocp.py:293-296)
+  double* As;        // scaled A
+  double* qs;
+  double* ls;
+  double* us;
+  double* rho;
+  double* D;
+  double* E;
+  double* cs;        // cost scaling c (1 per problem)
+  double* Ps;        // scaled P diagonal
+  double* xa;        // ADMM x (scaled, persistent warm start)
+  double* za;
+  double* ya;
+  double* rhs;
+  double* bt;
+  double* dxs;       // delta x (check iterations)
+  double* dys;       // delta y
+  double* aty;       // A^T y scratch (check iterations)
+  double* step;      // unscaled QP step dx
+  double* S;         // factor blocks (tiled)
+  double* Kc;        // coupling scratch (ndx x nw_max) per problem
+  double* Uc;        // U = Kc S scratch
+  double* Cs;        // Schur complement carried to the next node (ndx x ndx)
+  double* work;      // generic reductions scratch
+  PlProbInfo* info;
+  // MPC (device loop)
+  double* t0;        // per-problem gait time offset
+  double* xstate;    // per-problem current state x_init (nx)
+};
+
+struct PlOcpHandle {
+  int device;
+  hipStream_t stream;
+  int B;
+  int N, n, m, np, nnz, nx, ndx, nw_max, ncol_max, nrow_max, S_stride;
+  int nunit_max;
+  PlSettings set;
+  PlModel model;
+  PlOcpConst oc;
+  int gait_type;     // 0 trot, 1 walk, 2 stand
+  double gait_period, swing_period;
+  double f_des[PL_MAXNU];
+  PlDev d;
+  // host copies of the structure
+  int* h_nodes_raw;
+};
+
+// ---- kernel launchers (defined in the k_*.hip translation units)
+void launch_eval_values(PlOcpHandle* h, const double* xsrc);
+void launch_eval_jac(PlOcpHandle* h);
+void launch_objective(PlOcpHandle* h);
+void launch_hess(PlOcpHandle* h);
+void launch_qp_setup(PlOcpHandle* h);
+void launch_factor(PlOcpHandle* h);
+void launch_admm_init(PlOcpHandle* h);
+void launch_admm(PlOcpHandle* h, int niter, int check, int it_base);
+void launch_check(PlOcpHandle* h, int it, int final_check);
+void launch_unscale(PlOcpHandle* h);
+void launch_line_search(PlOcpHandle* h);
+void launch_mpc_prepare(PlOcpHandle* h, int k);
+void launch_mpc_finish(PlOcpHandle* h);
+void launch_reset_info(PlOcpHandle* h);
+void launch_reset_iterates(PlOcpHandle* h);
+
+#define PL_CHECK_HIP(expr)                                                        \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      pl_set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr, hipGetErrorString(_e)); \
+      return -2;                                                                  \
+    }                                                                             \
+  } while (0)
+
+void pl_set_error(const char* fmt, ...);

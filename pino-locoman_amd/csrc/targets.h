@@ -1,0 +1,45 @@
+// Tracking targets and objective terms (host+device, doubles).
+//
+// x_des = [q0, base_vel_des, 0], dx_des = difference(x_init, x_des)
+//   (ocp_whole_body_rnea.py:91-94, ocp_whole_body_acc.py:73-76, ocp_whole_body_aba.py:69-72);
+// f_des = 0.8 / 1.2 * m g / n_contacts on front / rear feet, 0 on the end effector,
+// u_des = [0_a, f_des, 0_tau] (ocp_whole_body_rnea.py:96-106 and siblings);
+// objective sum_i |dx_i - dx_des|_Q^2 + |u_i - u_des|_R^2 (+ |tau_0 - tau_prev|_W^2)
+//   + |dx_N - dx_des|_Q^2 (ocp.py:80-101, ocp_whole_body_rnea.py:108-136).
+#pragma once
+#include "rbd.h"
+#include "rows.h"
+
+namespace pl {
+
+PL_HD void compute_dx_des(const PlModel& M, const PlOcpConst& O, const double* p, double* dxd) {
+  const double* xi = p + O.P.x_init;
+  difference_q(M, xi, O.q0, dxd);
+  for (int k = 0; k < O.nv; ++k) {
+    double vd = (k < 6) ? p[O.P.base_vel_des + k] : 0.0;
+    dxd[O.nv + k] = vd - xi[O.nq + k];
+  }
+}
+
+// Force target of component c (0..nf-1) of the stacked end-effector forces.
+PL_HD double f_des_comp(const PlModel& M, const PlOcpConst& O, const double* p, int c) {
+  int foot = c / 3, ax = c % 3;
+  if (foot >= O.nfeet || ax != 2) return 0.0;
+  double fg = 9.81 * M.total_mass;
+  double nc = p[O.P.n_contacts];
+  return (foot < 2 ? 0.8 : 1.2) * fg / nc;
+}
+
+// Offset of the forces inside u for the dynamics kind.
+PL_HD int u_force_off(const PlOcpConst& O) {
+  return (O.dyn == PL_DYN_RNEA) ? O.na : (O.dyn == PL_DYN_ACC ? O.nv : O.nj);
+}
+
+// u_des[k] (k indexes the padded input of length nu_0).
+PL_HD double u_des(const PlModel& M, const PlOcpConst& O, const double* p, int k) {
+  int fo = u_force_off(O);
+  if (k >= fo && k < fo + O.nf) return f_des_comp(M, O, p, k - fo);
+  return 0.0;
+}
+
+}  // namespace pl

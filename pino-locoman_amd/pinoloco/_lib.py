@@ -1,0 +1,170 @@
+"""ctypes binding of libpinoloco.so (include/pinoloco.h).
+
+Loads the in-tree HIP extension and fails loudly when it is missing: there is no
+CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpinoloco.so")
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+
+
+class ModelDesc(C.Structure):
+    _fields_ = [("njoints", C.c_int), ("nq", C.c_int), ("nv", C.c_int),
+                ("parent", _ip), ("jtype", _ip), ("axis", _dp), ("placement_R", _dp), ("placement_p", _dp),
+                ("mass", _dp), ("lever", _dp), ("inertia", _dp), ("gravity", _dp),
+                ("nframes", C.c_int), ("frame_parent", _ip), ("frame_R", _dp), ("frame_p", _dp)]
+
+
+class OcpDesc(C.Structure):
+    _fields_ = [("dynamics", C.c_int), ("nodes", C.c_int), ("tau_nodes", C.c_int), ("include_acc", C.c_int),
+                ("include_base", C.c_int), ("n_feet", C.c_int), ("foot_frames", C.c_int * 4),
+                ("ext_force_frame", C.c_int), ("arm_ee_frame", C.c_int), ("base_frame", C.c_int),
+                ("mu", C.c_double), ("q0", _dp), ("joint_pos_min", _dp), ("joint_pos_max", _dp),
+                ("joint_vel_max", _dp), ("joint_torque_max", _dp),
+                ("rho", C.c_double), ("sigma", C.c_double), ("alpha", C.c_double), ("eps_abs", C.c_double),
+                ("eps_rel", C.c_double), ("eps_prim_inf", C.c_double), ("eps_dual_inf", C.c_double),
+                ("max_iter", C.c_int), ("scaling", C.c_int), ("check_termination", C.c_int),
+                ("warm_start", C.c_int), ("gait_type", C.c_int), ("gait_period", C.c_double)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("status", C.c_int), ("admm_iters", C.c_int), ("ls_accepted", C.c_int), ("ls_branch", C.c_int),
+                ("ls_trials", C.c_int), ("pad", C.c_int), ("ls_alpha", C.c_double), ("viol_max", C.c_double),
+                ("pri_res", C.c_double), ("dua_res", C.c_double), ("f", C.c_double)]
+
+
+EXPORTS = {
+    "pl_last_error": (C.c_char_p, []),
+    "pl_version": (C.c_int, []),
+    "pl_model_create": (C.c_int, [C.POINTER(ModelDesc), C.POINTER(C.c_void_p)]),
+    "pl_model_destroy": (None, [C.c_void_p]),
+    "pl_ocp_create": (C.c_int, [C.c_void_p, C.POINTER(OcpDesc), C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    "pl_ocp_destroy": (None, [C.c_void_p]),
+    "pl_ocp_dims": (C.c_int, [C.c_void_p, _ip, _ip, _ip, _ip]),
+    "pl_ocp_pattern": (C.c_int, [C.c_void_p, _ip, _ip]),
+    "pl_ocp_set_params": (C.c_int, [C.c_void_p, _dp]),
+    "pl_ocp_get_params": (C.c_int, [C.c_void_p, _dp]),
+    "pl_ocp_set_x": (C.c_int, [C.c_void_p, _dp]),
+    "pl_ocp_get_x": (C.c_int, [C.c_void_p, _dp]),
+    "pl_ocp_init_solver": (C.c_int, [C.c_void_p]),
+    "pl_ocp_solve": (C.c_int, [C.c_void_p, C.POINTER(Stats), _dp]),
+    "pl_eval_sqp_data": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),
+    "pl_eval_f": (C.c_int, [C.c_void_p, _dp]),
+    "pl_ocp_get_step": (C.c_int, [C.c_void_p, _dp]),
+    "pl_mpc_setup": (C.c_int, [C.c_void_p, _dp, _dp]),
+    "pl_mpc_step": (C.c_int, [C.c_void_p, C.c_int]),
+    "pl_mpc_get_state": (C.c_int, [C.c_void_p, _dp]),
+    "pl_mpc_export": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pl_ocp_sync": (C.c_int, [C.c_void_p]),
+    "pl_state_integrate": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
+    "pl_state_difference": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
+    "pl_debug_get": (C.c_int, [C.c_void_p, C.c_char_p, _dp, C.c_longlong]),
+    "pl_debug_nodes": (C.c_int, [C.c_void_p, _ip]),
+}
+
+_lib = None
+
+
+class PinolocoError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libpinoloco.so (building it first if only the sources are present)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        from . import build as _build
+        try:
+            _build.build()
+        except Exception as exc:  # noqa: BLE001
+            raise PinolocoError(f"HIP extension {LIB_PATH} is missing and could not be built: {exc}") from exc
+    L = C.CDLL(LIB_PATH)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise PinolocoError(lib().pl_last_error().decode())
+    return rc
+
+
+def dptr(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_dp)
+
+
+def iptr(a: np.ndarray):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_ip)
+
+
+class ModelHandle:
+    """pl_model built from a pinoloco.model.Model."""
+
+    def __init__(self, model):
+        from .model import JT_FREEFLYER, JT_REVOLUTE
+        nj = model.njoints
+        self._keep = []
+
+        def arr(x, dt=np.float64):
+            a = np.ascontiguousarray(np.asarray(x, dtype=dt))
+            self._keep.append(a)
+            return a
+
+        parent = arr([j.parent for j in model.joints], np.int32)
+        jtype = arr([j.jtype for j in model.joints], np.int32)
+        axis = arr(np.concatenate([j.axis for j in model.joints]))
+        pR = arr(np.concatenate([j.placement.R.ravel() for j in model.joints]))
+        pp = arr(np.concatenate([j.placement.p for j in model.joints]))
+        mass = arr([Y.mass for Y in model.inertias])
+        lever = arr(np.concatenate([Y.lever for Y in model.inertias]))
+        inertia = arr(np.concatenate([Y.I.ravel() for Y in model.inertias]))
+        grav = arr(model.gravity)
+        fpar = arr([f.parent_joint for f in model.frames], np.int32)
+        fR = arr(np.concatenate([f.placement.R.ravel() for f in model.frames]))
+        fp = arr(np.concatenate([f.placement.p for f in model.frames]))
+        assert JT_FREEFLYER == 1 and JT_REVOLUTE == 2
+        d = ModelDesc(nj, model.nq, model.nv, iptr(parent), iptr(jtype), dptr(axis), dptr(pR), dptr(pp),
+                      dptr(mass), dptr(lever), dptr(inertia), dptr(grav), len(model.frames), iptr(fpar),
+                      dptr(fR), dptr(fp))
+        h = C.c_void_p()
+        check(lib().pl_model_create(C.byref(d), C.byref(h)))
+        self.h = h
+        self.nq, self.nv = model.nq, model.nv
+
+    def integrate(self, x, dx):
+        x = np.ascontiguousarray(np.asarray(x, dtype=np.float64).ravel())
+        dx = np.ascontiguousarray(np.asarray(dx, dtype=np.float64).ravel())
+        out = np.zeros(self.nq + self.nv)
+        check(lib().pl_state_integrate(self.h, dptr(x), dptr(dx), dptr(out)))
+        return out
+
+    def difference(self, x0, x1):
+        x0 = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).ravel())
+        x1 = np.ascontiguousarray(np.asarray(x1, dtype=np.float64).ravel())
+        out = np.zeros(2 * self.nv)
+        check(lib().pl_state_difference(self.h, dptr(x0), dptr(x1), dptr(out)))
+        return out
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and _lib is not None:
+                _lib.pl_model_destroy(self.h)
+        except Exception:  # noqa: BLE001
+            pass

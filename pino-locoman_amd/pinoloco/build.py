@@ -1,0 +1,68 @@
+"""Build the HIP extension (libpinoloco.so) in-tree for gfx950.
+
+The shared library is the product: every hot-path kernel plus the C-ABI of
+``include/pinoloco.h``.  It is built next to this file so it travels with the
+repository snapshot to the GPU box (``pino-locoman_amd/pinoloco/libpinoloco.so``).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.normpath(os.path.join(HERE, "..", "csrc"))
+LIB = os.path.join(HERE, "libpinoloco.so")
+SOURCES = ["api.hip", "k_eval.hip", "k_qp.hip"]
+ARCH = os.environ.get("PL_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc():
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if cand and (os.path.isabs(cand) and os.path.exists(cand) or not os.path.isabs(cand)):
+            return cand
+    return "hipcc"
+
+
+def _flags():
+    return ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-fPIC", "-Wno-unused-result",
+            "-I", CSRC, "-I", os.path.join(CSRC, "..", "..", "include")]
+
+
+def _newest_input():
+    paths = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [
+        os.path.join(CSRC, "..", "..", "include", "pinoloco.h"), os.path.abspath(__file__)]
+    return max(os.path.getmtime(p) for p in paths if os.path.exists(p))
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest_input():
+        return LIB
+    hipcc = _hipcc()
+    objdir = os.path.join(HERE, "_build")
+    os.makedirs(objdir, exist_ok=True)
+
+    def compile_one(src):
+        obj = os.path.join(objdir, src.replace(".hip", ".o"))
+        cmd = [hipcc] + _flags() + ["-c", os.path.join(CSRC, src), "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    tmp = LIB + ".tmp"
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+    os.replace(tmp, LIB)
+    if verbose:
+        print(f"[pinoloco] built {LIB}", file=sys.stderr)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

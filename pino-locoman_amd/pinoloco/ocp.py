@@ -1,0 +1,537 @@
+"""make_ocp / OCP surface of the reference, backed by the HIP solve path.
+
+Mirrors ``optimization/ocp_factory.py:8-27`` and the methods of
+``optimization/ocp.py`` / ``ocp_whole_body_{rnea,acc,aba}.py`` that the drivers
+use (``run_mpc.py:72-143``, ``run_ocp.py:48-99``): parameter setters, gait update,
+warm start, ``init_solver``, ``solve(retract_all)``, ``retract_stacked_sol``,
+``DX_prev`` / ``U_prev`` / ``q_sol`` ... / ``solve_time``.  Solver ``"osqp"`` runs
+the OSQP-SQP path on the GPU through libpinoloco (one problem = batch of 1);
+:class:`BatchedOCP` exposes the same path for a batch of independent problems.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+
+import numpy as np
+
+from . import _lib
+from .gait import horizon_dts
+
+DYN_CODES = {"whole_body_rnea": 0, "whole_body_acc": 1, "whole_body_aba": 2}
+GAIT_CODES = {"trot": 0, "walk": 1, "stand": 2}
+
+# ocp.py:267-273 plus the OSQP 0.6 library defaults it leaves untouched.
+OSQP_SETTINGS = dict(max_iter=100, alpha=1.4, rho=2e-2, warm_start=True, adaptive_rho=False,
+                     sigma=1e-6, eps_abs=1e-3, eps_rel=1e-3, eps_prim_inf=1e-4, eps_dual_inf=1e-4,
+                     scaling=10, check_termination=25)
+
+# ocp_args.py:2-19
+OCP_ARGS = {
+    "centroidal_vel": {"include_base": True},
+    "centroidal_acc": {"include_base": True},
+    "whole_body_acc": {"include_base": True},
+    "whole_body_aba": {},
+    "whole_body_rnea": {"tau_nodes": 3, "include_acc": True},
+}
+
+STATUS_NAMES = {1: "solved", 2: "solved inaccurate", -2: "maximum iterations reached", -3: "primal infeasible",
+                3: "primal infeasible inaccurate", -4: "dual infeasible", 4: "dual infeasible inaccurate",
+                -7: "problem non convex", -10: "unsolved"}
+
+
+class Layout:
+    """Variable / parameter bookkeeping (setup_variables / setup_parameters)."""
+
+    def __init__(self, robot, dynamics, nodes, tau_nodes=3):
+        self.dynamics = dynamics
+        self.N = nodes
+        self.nq, self.nv, self.nj, self.nf = robot.nq, robot.nv, robot.nj, robot.nf
+        self.nx = self.nq + self.nv
+        self.ndx = 2 * self.nv
+        nv, nj, nf = self.nv, self.nj, self.nf
+        if dynamics == "whole_body_rnea":
+            self.tau_nodes = tau_nodes
+            self.na = nv
+            self.nu = [nv + nf + nj] * tau_nodes + [nv + nf] * (nodes - tau_nodes)
+            self.f_idx, self.tau_idx = nv, nv + nf
+        elif dynamics == "whole_body_acc":
+            self.tau_nodes = 0
+            self.na = nv
+            self.nu = [nv + nf] * nodes
+            self.f_idx, self.tau_idx = nv, nv + nf
+        elif dynamics == "whole_body_aba":
+            self.tau_nodes = 0
+            self.na = 0
+            self.nu = [nj + nf] * nodes
+            self.f_idx, self.tau_idx = nj, None
+        else:
+            raise ValueError(f"Unknown dynamics type: {dynamics}")
+        self.x_off = [0]
+        for i in range(nodes):
+            self.x_off.append(self.x_off[-1] + self.ndx + self.nu[i])
+        self.n = self.x_off[-1] + self.ndx
+        items = [("x_init", self.nx), ("dt_min", 1), ("dt_max", 1), ("contact_schedule", 4 * nodes),
+                 ("swing_schedule", 4 * nodes), ("n_contacts", 1), ("swing_period", 1), ("swing_height", 1),
+                 ("swing_vel_limits", 2), ("Q_diag", self.ndx), ("R_diag", self.nu[0]), ("base_vel_des", 6),
+                 ("ext_force_des", 3), ("arm_vel_des", 3)]
+        if dynamics == "whole_body_rnea":
+            items += [("tau_prev", nj), ("W_diag", nj)]
+        self.poff = {}
+        off = 0
+        for k, s in items:
+            self.poff[k] = (off, s)
+            off += s
+        self.np = off
+
+    def pack(self, values: dict) -> np.ndarray:
+        p = np.zeros(self.np)
+        for k, (o, s) in self.poff.items():
+            v = values.get(k)
+            if v is None:
+                continue
+            v = np.asarray(v, dtype=np.float64)
+            if k in ("contact_schedule", "swing_schedule"):
+                v = v.reshape(4, self.N).T  # column-major 4xN (CasADi parameter vectorisation)
+            p[o:o + s] = v.ravel()
+        return p
+
+    def split(self, x):
+        DX, U = [], []
+        for i in range(self.N):
+            o = self.x_off[i]
+            DX.append(x[o:o + self.ndx])
+            U.append(x[o + self.ndx:o + self.ndx + self.nu[i]])
+        DX.append(x[self.x_off[self.N]:self.x_off[self.N] + self.ndx])
+        return DX, U
+
+
+def default_weights(robot, dynamics, layout):
+    """set_weights (ocp_whole_body_rnea.py:28-63, ocp_whole_body_acc.py:26-54, ocp_whole_body_aba.py:22-50)."""
+    nj, nf = robot.nj, robot.nf
+    Qb = [0, 0, 1000, 10000, 10000, 0]
+    Qj = list(np.tile([1000, 500, 500], 4))
+    if robot.arm_ee_frame is not None:
+        Qj += [100] * 6
+    Qv = [2000, 2000, 1000, 1000, 1000, 2000] + [1] * nj
+    Q = np.array(Qb + Qj + Qv, float)
+    if dynamics == "whole_body_rnea":
+        R = np.array([1e-3] * layout.na + [1e-3] * nf + [1e-4] * nj, float)
+    elif dynamics == "whole_body_acc":
+        R = np.array([1e-3] * robot.nv + [1e-3] * nf, float)
+    else:
+        R = np.array([1e-3] * nj + [1e-3] * nf, float)
+    W = np.zeros(nj)
+    return Q, R, W
+
+
+class BatchedOCP:
+    """A batch of independent OCPs of one (robot, dynamics, N) on one GPU."""
+
+    def __init__(self, robot, dynamics, nodes, batch=1, device=0, tau_nodes=3, include_acc=True,
+                 include_base=True, gait_type="trot", gait_period=0.8, osqp_settings=None, mu=0.7):
+        if dynamics not in DYN_CODES:
+            raise ValueError(f"Unknown dynamics type: {dynamics}")
+        L = _lib.lib()
+        self.robot = robot
+        self.dynamics = dynamics
+        self.batch = batch
+        self.layout = Layout(robot, dynamics, nodes, tau_nodes)
+        self.model_h = ModelCache.get(robot.model)
+        s = dict(OSQP_SETTINGS)
+        if osqp_settings:
+            s.update(osqp_settings)
+        self.settings = s
+        model = robot.model
+        feet = robot.foot_frames if robot.foot_frames is not None else [model.get_frame_id(f) for f in
+                                                                         ("FR_foot", "FL_foot", "RR_foot", "RL_foot")]
+        base = model.get_frame_id("base_link")
+        self._keep = []
+
+        def arr(x):
+            a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+            self._keep.append(a)
+            return _lib.dptr(a)
+
+        d = _lib.OcpDesc()
+        d.dynamics = DYN_CODES[dynamics]
+        d.nodes = nodes
+        d.tau_nodes = tau_nodes if dynamics == "whole_body_rnea" else 0
+        d.include_acc = int(include_acc)
+        d.include_base = int(include_base)
+        d.n_feet = 4
+        for k in range(4):
+            d.foot_frames[k] = int(feet[k])
+        d.ext_force_frame = -1 if robot.ext_force_frame is None else int(robot.ext_force_frame)
+        d.arm_ee_frame = -1 if robot.arm_ee_frame is None else int(robot.arm_ee_frame)
+        d.base_frame = base if base < len(model.frames) else -1
+        d.mu = mu
+        d.q0 = arr(robot.q0)
+        d.joint_pos_min = arr(robot.joint_pos_min)
+        d.joint_pos_max = arr(robot.joint_pos_max)
+        d.joint_vel_max = arr(robot.joint_vel_max)
+        d.joint_torque_max = arr(robot.joint_torque_max)
+        for k in ("rho", "sigma", "alpha", "eps_abs", "eps_rel", "eps_prim_inf", "eps_dual_inf"):
+            setattr(d, k, float(s[k]))
+        d.max_iter, d.scaling, d.check_termination = int(s["max_iter"]), int(s["scaling"]), int(
+            s["check_termination"])
+        d.warm_start = int(bool(s["warm_start"]))
+        d.gait_type = GAIT_CODES[gait_type]
+        d.gait_period = float(gait_period)
+        h = C.c_void_p()
+        _lib.check(L.pl_ocp_create(self.model_h.h, C.byref(d), batch, device, C.byref(h)))
+        self.h = h
+        self.device = device
+        n, m, np_, nnz = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        _lib.check(L.pl_ocp_dims(h, C.byref(n), C.byref(m), C.byref(np_), C.byref(nnz)))
+        self.n, self.m, self.np, self.nnz = n.value, m.value, np_.value, nnz.value
+        assert self.n == self.layout.n and self.np == self.layout.np, (self.n, self.layout.n, self.np, self.layout.np)
+
+    # ---------------------------------------------------------------- queries
+    def pattern(self):
+        rows = np.zeros(self.nnz, dtype=np.int32)
+        cols = np.zeros(self.nnz, dtype=np.int32)
+        _lib.check(_lib.lib().pl_ocp_pattern(self.h, _lib.iptr(rows), _lib.iptr(cols)))
+        return rows, cols
+
+    def node_table(self):
+        out = np.zeros(12 * (self.layout.N + 1), dtype=np.int32)
+        _lib.check(_lib.lib().pl_debug_nodes(self.h, _lib.iptr(out)))
+        return out.reshape(-1, 12)
+
+    # ---------------------------------------------------------------- data
+    def set_params(self, P):
+        P = np.ascontiguousarray(np.broadcast_to(np.asarray(P, dtype=np.float64), (self.batch, self.np)))
+        _lib.check(_lib.lib().pl_ocp_set_params(self.h, _lib.dptr(P)))
+
+    def get_params(self):
+        P = np.zeros((self.batch, self.np))
+        _lib.check(_lib.lib().pl_ocp_get_params(self.h, _lib.dptr(P)))
+        return P
+
+    def set_x(self, X):
+        X = np.ascontiguousarray(np.broadcast_to(np.asarray(X, dtype=np.float64), (self.batch, self.n)))
+        _lib.check(_lib.lib().pl_ocp_set_x(self.h, _lib.dptr(X)))
+
+    def get_x(self):
+        X = np.zeros((self.batch, self.n))
+        _lib.check(_lib.lib().pl_ocp_get_x(self.h, _lib.dptr(X)))
+        return X
+
+    def get_step(self):
+        X = np.zeros((self.batch, self.n))
+        _lib.check(_lib.lib().pl_ocp_get_step(self.h, _lib.dptr(X)))
+        return X
+
+    def init_solver(self):
+        _lib.check(_lib.lib().pl_ocp_init_solver(self.h))
+
+    def solve(self, timed=False):
+        stats = (_lib.Stats * self.batch)()
+        phase = np.zeros(4)
+        _lib.check(_lib.lib().pl_ocp_solve(self.h, stats, _lib.dptr(phase) if timed else None))
+        out = {k: np.array([getattr(s, k) for s in stats]) for k, _ in _lib.Stats._fields_ if k != "pad"}
+        if timed:
+            out["phase_ms"] = phase
+        return out
+
+    def eval_sqp_data(self):
+        B = self.batch
+        grad, J = np.zeros((B, self.n)), np.zeros((B, self.nnz))
+        g, lbg, ubg = np.zeros((B, self.m)), np.zeros((B, self.m)), np.zeros((B, self.m))
+        _lib.check(_lib.lib().pl_eval_sqp_data(self.h, _lib.dptr(grad), _lib.dptr(J), _lib.dptr(g), _lib.dptr(lbg),
+                                               _lib.dptr(ubg)))
+        return grad, J, g, lbg, ubg
+
+    def eval_f(self):
+        f = np.zeros(self.batch)
+        _lib.check(_lib.lib().pl_eval_f(self.h, _lib.dptr(f)))
+        return f
+
+    def debug(self, name, length):
+        out = np.zeros(length)
+        _lib.check(_lib.lib().pl_debug_get(self.h, name.encode(), _lib.dptr(out), length))
+        return out
+
+    # ---------------------------------------------------------------- MPC
+    def mpc_setup(self, x_state, t0):
+        xs = np.ascontiguousarray(np.asarray(x_state, dtype=np.float64).reshape(self.batch, -1))
+        t = np.ascontiguousarray(np.asarray(t0, dtype=np.float64).reshape(self.batch))
+        _lib.check(_lib.lib().pl_mpc_setup(self.h, _lib.dptr(xs), _lib.dptr(t)))
+
+    def mpc_step(self, k):
+        _lib.check(_lib.lib().pl_mpc_step(self.h, int(k)))
+
+    def mpc_state(self):
+        xs = np.zeros((self.batch, self.layout.nx))
+        _lib.check(_lib.lib().pl_mpc_get_state(self.h, _lib.dptr(xs)))
+        return xs
+
+    def mpc_export(self, device_ptr):
+        _lib.check(_lib.lib().pl_mpc_export(self.h, C.c_void_p(device_ptr)))
+
+    def sync(self):
+        _lib.check(_lib.lib().pl_ocp_sync(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.lib().pl_ocp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class ModelCache:
+    _cache = {}
+
+    @classmethod
+    def get(cls, model):
+        key = id(model)
+        if key not in cls._cache:
+            cls._cache[key] = (model, _lib.ModelHandle(model))
+        return cls._cache[key][1]
+
+
+class _StateMap:
+    def __init__(self, fn):
+        self._fn = fn
+
+    def __call__(self, *args):
+        return self._fn(*args)
+
+
+class Dynamics:
+    """Plugin surface of dynamics/dynamics.py: factory methods returning callables.
+
+    ``state_integrate()`` / ``state_difference()`` (dynamics_whole_body_torque.py:11-40)
+    run the library's own Lie-group code on the host (pl_state_integrate)."""
+
+    def __init__(self, robot):
+        self.model = robot.model
+        self.nq, self.nv = robot.nq, robot.nv
+        self.nj = self.nq - 7
+        self._h = ModelCache.get(robot.model)
+
+    def state_integrate(self):
+        return _StateMap(lambda x, dx: self._h.integrate(x, dx))
+
+    def state_difference(self):
+        return _StateMap(lambda x0, x1: self._h.difference(x0, x1))
+
+
+class OCP:
+    """Single-problem OCP with the reference's method surface (ocp.py:11-480)."""
+
+    def __init__(self, robot, solver, nodes, dynamics, tau_nodes=3, include_acc=True, include_base=True):
+        if solver != "osqp":
+            raise ValueError(f"Solver {solver} not supported on the MI355X path (ocp.py:321-322); "
+                             "the Fatrop interior-point path is a later row of the build plan")
+        self.robot = robot
+        self.model = robot.model
+        self.gait_sequence = robot.gait_sequence
+        self.foot_frames = robot.foot_frames
+        self.ext_force_frame = robot.ext_force_frame
+        self.arm_ee_frame = robot.arm_ee_frame
+        self.n_feet = len(self.foot_frames)
+        self.nq, self.nv, self.nf, self.nj = robot.nq, robot.nv, robot.nf, robot.nj
+        self.solver = solver
+        self.nodes = nodes
+        self.mass = robot.mass
+        self.dynamics = dynamics
+        self.dyn = Dynamics(robot)
+        self.layout = Layout(robot, dynamics, nodes, tau_nodes)
+        L = self.layout
+        self.nx, self.ndx_opt, self.nu_opt = L.nx, L.ndx, L.nu
+        self.f_idx, self.tau_idx = L.f_idx, L.tau_idx
+        self.tau_nodes = L.tau_nodes
+        self.na_opt = L.na
+        self.include_acc, self.include_base = include_acc, include_base
+        self.x_nom = np.concatenate((robot.q0, [0] * self.nv))
+        self.q_sol, self.v_sol, self.a_sol, self.forces_sol, self.tau_sol = [], [], [], [], []
+        self.DX_prev = None
+        self.U_prev = None
+        self.lam_g = None
+        self.solve_time = None
+        self.stats = None
+        self._backend = BatchedOCP(robot, dynamics, nodes, batch=1, tau_nodes=tau_nodes, include_acc=include_acc,
+                                   include_base=include_base,
+                                   gait_type=self.gait_sequence.gait_type if self.gait_sequence else "trot",
+                                   gait_period=self.gait_sequence.gait_period if self.gait_sequence else 0.8)
+        self.p = {"tau_prev": np.zeros(self.nj), "W_diag": np.zeros(self.nj), "ext_force_des": np.zeros(3),
+                  "arm_vel_des": np.zeros(3), "x_init": self.x_nom.copy()}
+        if self.gait_sequence is not None:
+            self.p["n_contacts"] = self.gait_sequence.n_contacts
+        # initial guess: DX = 0, U = u_des (ocp.py:159-163, 193)
+        self._x_initial = np.zeros(L.n)
+        for i in range(nodes):
+            o = L.x_off[i] + L.ndx
+            self._x_initial[o:o + L.nu[i]] = self._u_des()[:L.nu[i]]
+
+    # ------------------------------------------------------------------ params
+    def _f_des(self):
+        fg = 9.81 * self.mass
+        nc = float(np.asarray(self.p["n_contacts"]).ravel()[0])
+        f = [0, 0, 0.8 * fg / nc] * 2 + [0, 0, 1.2 * fg / nc] * 2
+        if self.ext_force_frame is not None:
+            f += [0, 0, 0]
+        return np.array(f, float)
+
+    def _u_des(self):
+        f = self._f_des()
+        if self.dynamics == "whole_body_rnea":
+            return np.concatenate([np.zeros(self.na_opt), f, np.zeros(self.nj)])
+        if self.dynamics == "whole_body_acc":
+            return np.concatenate([np.zeros(self.nv), f])
+        return np.concatenate([np.zeros(self.nj), f])
+
+    def set_weights(self):
+        Q, R, W = default_weights(self.robot, self.dynamics, self.layout)
+        self.p["Q_diag"], self.p["R_diag"], self.p["W_diag"] = Q, R, W
+
+    def set_time_params(self, dt_min, dt_max):
+        self.p["dt_min"], self.p["dt_max"] = dt_min, dt_max
+
+    def set_swing_params(self, swing_height, swing_vel_limits):
+        self.p["swing_height"], self.p["swing_vel_limits"] = swing_height, np.asarray(swing_vel_limits, float)
+
+    def set_tracking_targets(self, base_vel_des, ext_force_des=None, arm_vel_des=None):
+        self.p["base_vel_des"] = np.asarray(base_vel_des, float)
+        if self.ext_force_frame is not None:
+            self.p["ext_force_des"] = np.asarray(ext_force_des, float)
+        if self.arm_ee_frame is not None:
+            self.p["arm_vel_des"] = np.asarray(arm_vel_des, float)
+
+    def update_initial_state(self, x_init):
+        self.p["x_init"] = np.asarray(x_init, float).ravel()
+
+    def update_previous_torques(self, tau_prev):
+        self.p["tau_prev"] = np.asarray(tau_prev, float)
+
+    @property
+    def dts(self):
+        return horizon_dts(self.p["dt_min"], self.p["dt_max"], self.nodes)
+
+    def update_gait_sequence(self, t_current):
+        contact, swing = self.gait_sequence.get_gait_schedule(t_current, self.dts, self.nodes)
+        self.p["contact_schedule"], self.p["swing_schedule"] = contact, swing
+        self.p["n_contacts"] = self.gait_sequence.n_contacts
+        self.p["swing_period"] = self.gait_sequence.swing_period
+
+    def param_vector(self):
+        return self.layout.pack(self.p)
+
+    # ------------------------------------------------------------------ warm start
+    def warm_start(self):
+        """ocp_whole_body_rnea.py:207-235 (and the acc / aba variants)."""
+        L = self.layout
+        x = self._x_initial
+        if self.DX_prev is not None:
+            for i in range(self.nodes + 1):
+                x[L.x_off[i]:L.x_off[i] + L.ndx] = self.DX_prev[i]
+        if self.U_prev is not None:
+            contact = self.p["contact_schedule"]
+            for i in range(self.nodes):
+                f_des = self._f_des()
+                for j in range(self.n_feet):
+                    if contact[j, i] == 0:
+                        f_des[3 * j:3 * j + 3] = 0
+                u_prev = self.U_prev[i]
+                if self.dynamics == "whole_body_aba":
+                    u = np.concatenate([u_prev[:self.nj], f_des])
+                else:
+                    u = np.concatenate([u_prev[:self.na_opt], f_des])
+                    if self.dynamics == "whole_body_rnea" and i < self.tau_nodes:
+                        u = np.concatenate([u, u_prev[self.tau_idx:]])
+                o = L.x_off[i] + L.ndx
+                x[o:o + L.nu[i]] = u
+
+    # ------------------------------------------------------------------ solver
+    def init_solver(self):
+        """ocp.py:265-313: constant Hessian diagonal from the current parameters."""
+        self._backend.set_params(self.param_vector())
+        self._backend.init_solver()
+
+    def solve(self, retract_all=True):
+        """ocp.py:375-422 (OSQP branch): one SQP iteration on the GPU."""
+        self._backend.set_params(self.param_vector())
+        self._backend.set_x(self._x_initial)
+        start = time.time()
+        st = self._backend.solve()
+        self.solve_time = time.time() - start
+        self.stats = {k: v[0] for k, v in st.items()}
+        x = self._backend.get_x()[0]
+        self.retract_stacked_sol(x, retract_all)
+        return x
+
+    def retract_stacked_sol(self, sol_x, retract_all=True):
+        """ocp_whole_body_rnea.py:293-324."""
+        L = self.layout
+        x_init = self.p["x_init"]
+        integ = self.dyn.state_integrate()
+        DX, U = L.split(np.asarray(sol_x, float))
+        self.DX_prev = [np.array(d) for d in DX]
+        self.U_prev = [np.array(u) for u in U]
+        for i in range(self.nodes):
+            if i == 0 or retract_all:
+                xs = integ(x_init, DX[i])
+                self.q_sol.append(xs[:self.nq])
+                self.v_sol.append(xs[self.nq:])
+                u = U[i]
+                if self.dynamics == "whole_body_aba":
+                    self.tau_sol.append(u[:self.nj])
+                    self.forces_sol.append(u[self.f_idx:])
+                else:
+                    self.a_sol.append(u[:self.na_opt])
+                    self.forces_sol.append(u[self.f_idx:self.tau_idx] if self.tau_idx else u[self.f_idx:])
+                    if self.dynamics == "whole_body_rnea":
+                        self.tau_sol.append(u[self.tau_idx:])
+        if retract_all:
+            xs = integ(x_init, DX[-1])
+            self.q_sol.append(xs[:self.nq])
+            self.v_sol.append(xs[self.nq:])
+
+    def get_tau_sol(self, i):
+        return self.U_prev[i][self.tau_idx:]
+
+
+class OCPWholeBodyRNEA(OCP):
+    def __init__(self, robot, solver, nodes, tau_nodes, include_acc=True):
+        super().__init__(robot, solver, nodes, "whole_body_rnea", tau_nodes=tau_nodes, include_acc=include_acc)
+
+
+class OCPWholeBodyAcc(OCP):
+    def __init__(self, robot, solver, nodes, include_base=False):
+        super().__init__(robot, solver, nodes, "whole_body_acc", include_base=include_base)
+
+
+class OCPWholeBodyABA(OCP):
+    def __init__(self, robot, solver, nodes):
+        super().__init__(robot, solver, nodes, "whole_body_aba")
+
+
+class _CentroidalOnCPU:
+    def __init__(self, *args, **kwargs):
+        raise NotImplementedError("centroidal_vel / centroidal_acc are not on the MI355X path in this release "
+                                  "(SURVEY.md section 8f, row 3); the CPU oracle restates centroidal_vel for parity")
+
+
+def make_ocp(dynamics, default_args, **kwargs):
+    """ocp_factory.py:8-27."""
+    ocp_classes = {
+        "centroidal_vel": _CentroidalOnCPU,
+        "centroidal_acc": _CentroidalOnCPU,
+        "whole_body_acc": OCPWholeBodyAcc,
+        "whole_body_aba": OCPWholeBodyABA,
+        "whole_body_rnea": OCPWholeBodyRNEA,
+    }
+    if dynamics not in ocp_classes:
+        raise ValueError(f"Unknown dynamics type: {dynamics}")
+    args = default_args.copy()
+    args.update(kwargs)
+    ocp = ocp_classes[dynamics](**args)
+    ocp.set_weights()
+    return ocp
