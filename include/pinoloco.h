@@ -160,9 +160,19 @@ int pl_ocp_sync(pl_ocp* o);
 int pl_state_integrate(const pl_model* m, const double* x, const double* dx, double* out);
 int pl_state_difference(const pl_model* m, const double* x0, const double* x1, double* dx);
 
+/* Timing of the dominant kernel (ADMM sweeps) with HIP events on the handle's
+ * stream: pl_ocp_profile(o, 1) clears and starts, pl_ocp_profile_read returns
+ * [total_ms, launches, problem_iterations]. pl_ocp_sizes: [n, m, nnz,
+ * factor doubles per problem, largest node block, N]. */
+int pl_ocp_profile(pl_ocp* o, int enable);
+int pl_ocp_profile_read(pl_ocp* o, double* out);
+int pl_ocp_sizes(const pl_ocp* o, long long* out);
+
 /* Test / parity access to internal per-problem arrays and the node table. */
 int pl_debug_get(pl_ocp* o, const char* name, double* out, long long count);
 int pl_debug_nodes(const pl_ocp* o, int* out);
+int pl_debug_consts(const pl_ocp* o, void* model_out, void* oc_out, int* sizes);
+int pl_debug_admm(pl_ocp* o, int niter, int reset);
 
 #ifdef __cplusplus
 }

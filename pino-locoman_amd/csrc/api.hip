@@ -365,7 +365,7 @@ int dalloc(pl_ocp* o, T** p, size_t count) {
     pl_set_error("hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
     return -2;
   }
-  hipMemset(q, 0, count * sizeof(T));
+  (void)hipMemset(q, 0, count * sizeof(T));
   o->allocs.push_back(q);
   *p = (T*)q;
   return 0;
@@ -582,13 +582,15 @@ extern "C" int pl_ocp_pattern(const pl_ocp* o, int* rows, int* cols) {
   return 0;
 }
 
+static void prof_collect(PlOcpHandle* h);
+
 #define REQUIRE_DEVICE(o)                                              \
   do {                                                                 \
     if (!(o) || !(o)->on_device) {                                     \
       pl_set_error("handle has no device (created with device = -1)"); \
       return -1;                                                       \
     }                                                                  \
-    hipSetDevice((o)->h.device);                                       \
+    (void)hipSetDevice((o)->h.device);                                 \
   } while (0)
 
 extern "C" int pl_ocp_set_params(pl_ocp* o, const double* P) {
@@ -753,6 +755,7 @@ extern "C" int pl_mpc_setup(pl_ocp* o, const double* x_state, const double* t0) 
 
 extern "C" int pl_mpc_step(pl_ocp* o, int k) {
   REQUIRE_DEVICE(o);
+  if (o->h.profile && o->h.prof_n > 48) prof_collect(&o->h);
   launch_mpc_prepare(&o->h, k);
   enqueue_solve(o, false);
   launch_mpc_finish(&o->h);
@@ -784,9 +787,60 @@ extern "C" int pl_mpc_export(pl_ocp* o, void* device_dst) {
   return 0;
 }
 
+static void prof_collect(PlOcpHandle* h) {
+  if (!h->profile || h->prof_n == 0) return;
+  hipStreamSynchronize(h->stream);
+  for (int k = 0; k < h->prof_n; ++k) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, h->prof_ev[k][0], h->prof_ev[k][1]);
+    h->prof_admm_ms += ms;
+    h->prof_admm_launches++;
+  }
+  h->prof_n = 0;
+}
+
 extern "C" int pl_ocp_sync(pl_ocp* o) {
   REQUIRE_DEVICE(o);
   PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
+  prof_collect(&o->h);
+  return 0;
+}
+
+// Per-launch timing of the dominant kernel (k_admm) with HIP events recorded on
+// the handle's stream around every launch.  enable=1 starts (and clears),
+// enable=0 stops.  out: [total_ms, launches, problem_iterations].
+extern "C" int pl_ocp_profile(pl_ocp* o, int enable) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  prof_collect(h);
+  if (enable && !h->profile) {
+    for (int k = 0; k < 64; ++k) {
+      hipEventCreate(&h->prof_ev[k][0]);
+      hipEventCreate(&h->prof_ev[k][1]);
+    }
+  }
+  h->profile = enable;
+  h->prof_n = 0;
+  h->prof_admm_ms = 0.0;
+  h->prof_admm_launches = 0;
+  h->prof_admm_iters = 0;
+  return 0;
+}
+
+extern "C" int pl_ocp_profile_read(pl_ocp* o, double* out) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  prof_collect(h);
+  out[0] = h->prof_admm_ms;
+  out[1] = (double)h->prof_admm_launches;
+  out[2] = (double)h->prof_admm_iters;
+  return 0;
+}
+
+// Sizes the roofline accounting needs: [n, m, nnz, S_stride (doubles), nw_max, N].
+extern "C" int pl_ocp_sizes(const pl_ocp* o, long long* out) {
+  if (!o) { pl_set_error("null handle"); return -1; }
+  out[0] = o->h.n; out[1] = o->h.m; out[2] = o->h.nnz; out[3] = o->h.S_stride; out[4] = o->h.nw_max; out[5] = o->h.N;
   return 0;
 }
 
@@ -853,5 +907,24 @@ extern "C" int pl_debug_consts(const pl_ocp* o, void* model_out, void* oc_out, i
   if (sizes) { sizes[0] = (int)sizeof(PlModel); sizes[1] = (int)sizeof(PlOcpConst); }
   if (model_out) memcpy(model_out, &o->h.model, sizeof(PlModel));
   if (oc_out) memcpy(oc_out, &o->h.oc, sizeof(PlOcpConst));
+  return 0;
+}
+
+// Tests: evaluate + scale + factor, then exactly `niter` ADMM iterations from the
+// current iterates (no termination checks, no line search).
+extern "C" int pl_debug_admm(pl_ocp* o, int niter, int reset) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  launch_eval_values(h, h->d.x);
+  launch_eval_jac(h);
+  launch_objective(h);
+  launch_qp_setup(h);
+  launch_factor(h);
+  launch_reset_info(h);
+  if (reset) launch_reset_iterates(h);
+  launch_admm_init(h);
+  if (niter > 0) launch_admm(h, niter, 0, 0);
+  PL_CHECK_HIP(hipGetLastError());
+  PL_CHECK_HIP(hipStreamSynchronize(h->stream));
   return 0;
 }

@@ -389,6 +389,27 @@ __global__ __launch_bounds__(256) void k_factor(PlDev d, int N, int n, int m, in
         }
     }
     __syncthreads();
+    // ---- symmetrise: GJ without pivoting leaves S_i slightly non-symmetric
+    // (~eps * cond).  The sweeps read the lower triangle while the Schur
+    // complement of node i+1 uses the dense S_i, so both must see the same
+    // matrix or the block factorisation is inconsistent (the terminal node
+    // amplifies the mismatch by ~1e6).  (S + S^T) / 2 is also the more accurate.
+#pragma unroll
+    for (int rr = 0; rr < FB; ++rr)
+#pragma unroll
+      for (int cc = 0; cc < FB; ++cc) {
+        const int gi = FB * ty + rr, gj = FB * tx + cc;
+        if (gi < nw && gj < nw) big[gi * nw + gj] = Kr[rr][cc];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < FB; ++rr)
+#pragma unroll
+      for (int cc = 0; cc < FB; ++cc) {
+        const int gi = FB * ty + rr, gj = FB * tx + cc;
+        if (gi < nw && gj < nw) Kr[rr][cc] = 0.5 * (Kr[rr][cc] + big[gj * nw + gi]);
+      }
+    __syncthreads();
     // ---- store S_i: tiled global layout + dense copy in LDS (stride nw)
     {
       const int nunit = nd.nunit;
@@ -434,6 +455,11 @@ __global__ __launch_bounds__(256) void k_factor(PlDev d, int N, int n, int m, in
 }
 
 void launch_factor(PlOcpHandle* h) {
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)k_factor, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    attr = true;
+  }
   const size_t lds = sizeof(double) * ((size_t)h->nw_max * h->nw_max + (size_t)h->ndx * h->ndx + 4 * 112 + FCH);
   hipLaunchKernelGGL(k_factor, dim3(h->B), dim3(256), lds, h->stream, h->d, h->N, h->n, h->m, h->nnz, h->ndx,
                      h->S_stride, h->nw_max, h->set.sigma);
@@ -556,6 +582,10 @@ __global__ __launch_bounds__(256) void k_admm(PlDev d, int N, int n, int m, int 
   double* dxs = d.dxs + (size_t)b * n;
   double* dys = d.dys + (size_t)b * m;
   const PlNode* nodes = d.nodes;
+  // trow is read for every row of a column during the backward gathers: it must
+  // hold zeros except for the entries a phase writes and clears.
+  for (int lr = threadIdx.x; lr < nrow_max; lr += blockDim.x) L.trow[lr] = 0.0;
+  __syncthreads();
 
   for (int it = 0; it < niter; ++it) {
     const bool store_delta = check && (it == niter - 1);
@@ -701,10 +731,22 @@ __global__ __launch_bounds__(256) void k_admm(PlDev d, int N, int n, int m, int 
 
 void launch_admm(PlOcpHandle* h, int niter, int check, int it_base) {
   (void)it_base;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)k_admm, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    attr = true;
+  }
   const int vpad = ((h->nw_max + 7) / 8) * 8;
   const size_t lds = sizeof(double) * (3 * (size_t)vpad + h->nrow_max + 12 * (size_t)h->nunit_max);
+  const bool prof = h->profile && h->prof_n < 64;
+  if (prof) hipEventRecord(h->prof_ev[h->prof_n][0], h->stream);
   hipLaunchKernelGGL(k_admm, dim3(h->B), dim3(256), lds, h->stream, h->d, h->N, h->n, h->m, h->nnz, h->ndx,
                      h->S_stride, h->nw_max, h->nunit_max, h->nrow_max, niter, check, h->set.sigma, h->set.alpha);
+  if (prof) {
+    hipEventRecord(h->prof_ev[h->prof_n][1], h->stream);
+    h->prof_n++;
+    h->prof_admm_iters += (long long)h->B * niter;
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -120,6 +120,13 @@ struct PlOcpHandle {
   PlDev d;
   // host copies of the structure
   int* h_nodes_raw;
+  // optional per-kernel timing of the ADMM launches (HIP events on the handle's stream)
+  int profile;
+  hipEvent_t prof_ev[64][2];
+  int prof_n;
+  double prof_admm_ms;
+  long long prof_admm_launches;
+  long long prof_admm_iters;   // problem-iterations (B * niter) covered by the timed launches
 };
 
 // ---- kernel launchers (defined in the k_*.hip translation units)

@@ -67,8 +67,13 @@ EXPORTS = {
     "pl_ocp_sync": (C.c_int, [C.c_void_p]),
     "pl_state_integrate": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
     "pl_state_difference": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
+    "pl_ocp_profile": (C.c_int, [C.c_void_p, C.c_int]),
+    "pl_ocp_profile_read": (C.c_int, [C.c_void_p, _dp]),
+    "pl_ocp_sizes": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong)]),
+    "pl_debug_consts": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, _ip]),
     "pl_debug_get": (C.c_int, [C.c_void_p, C.c_char_p, _dp, C.c_longlong]),
     "pl_debug_nodes": (C.c_int, [C.c_void_p, _ip]),
+    "pl_debug_admm": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
 }
 
 _lib = None

@@ -26,7 +26,7 @@ def _hipcc():
 
 
 def _flags():
-    return ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-fPIC", "-Wno-unused-result",
+    return ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-fPIC", "-Wno-unused-result", "-Wno-unused-value",
             "-I", CSRC, "-I", os.path.join(CSRC, "..", "..", "include")]
 
 

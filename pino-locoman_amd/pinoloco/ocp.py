@@ -273,6 +273,19 @@ class BatchedOCP:
     def sync(self):
         _lib.check(_lib.lib().pl_ocp_sync(self.h))
 
+    def profile(self, enable):
+        _lib.check(_lib.lib().pl_ocp_profile(self.h, int(enable)))
+
+    def profile_read(self):
+        out = np.zeros(3)
+        _lib.check(_lib.lib().pl_ocp_profile_read(self.h, _lib.dptr(out)))
+        return {"admm_ms": out[0], "launches": int(out[1]), "problem_iters": int(out[2])}
+
+    def sizes(self):
+        out = (C.c_longlong * 6)()
+        _lib.check(_lib.lib().pl_ocp_sizes(self.h, out))
+        return dict(zip(("n", "m", "nnz", "S_stride", "nw_max", "N"), [int(v) for v in out]))
+
     def close(self):
         if getattr(self, "h", None):
             _lib.lib().pl_ocp_destroy(self.h)
