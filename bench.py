@@ -28,53 +28,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "pino-locoman_amd"))
 
 from pinoloco import robots  # noqa: E402
-from pinoloco.ocp import BatchedOCP, Layout, default_weights  # noqa: E402
+from pinoloco.ocp import BatchedOCP  # noqa: E402
+from pinoloco import dist as pdist  # noqa: E402
+from pinoloco.synthetic import build_batch, shard  # noqa: E402
 
 METRIC = "MPC solves/sec (B2G whole_body_rnea N=50) at batch; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
-
-
-def random_problem(R, lay, gidx):
-    """Per-problem randomisation, seed = 1234 + global index."""
-    rng = np.random.default_rng(1234 + gidx)
-    q = R.q0.copy()
-    q[:3] += rng.normal(0.0, 0.01, 3)
-    axis = rng.normal(size=3)
-    axis /= np.linalg.norm(axis)
-    ang = rng.uniform(0.0, 0.05)
-    q[3:7] = np.concatenate([axis * np.sin(ang / 2), [np.cos(ang / 2)]])
-    q[7:] = np.clip(q[7:] + rng.normal(0.0, 0.05, R.nj), R.joint_pos_min, R.joint_pos_max)
-    v = rng.normal(0.0, 0.1, R.nv)
-    t0 = rng.uniform(0.0, 0.8)
-    vx = rng.uniform(0.0, 0.3)
-    return np.concatenate([q, v]), t0, vx
-
-
-def build_batch(R, dynamics, N, B, first):
-    lay = Layout(R, dynamics, N)
-    Q, Rw, W = default_weights(R, dynamics, lay)
-    P = np.zeros((B, lay.np))
-    X = np.zeros((B, lay.n))
-    XS = np.zeros((B, lay.nx))
-    T0 = np.zeros(B)
-    fg = 9.81 * R.mass
-    fdes = np.array([0, 0, 0.8 * fg / 2] * 2 + [0, 0, 1.2 * fg / 2] * 2 + ([0, 0, 0] if R.ext_force_frame else []))
-    udes = np.concatenate([np.zeros(lay.na), fdes, np.zeros(R.nj)])
-    x0 = np.zeros(lay.n)
-    for i in range(N):
-        o = lay.x_off[i] + lay.ndx
-        x0[o:o + lay.nu[i]] = udes[:lay.nu[i]]
-    for b in range(B):
-        xs, t0, vx = random_problem(R, lay, first + b)
-        vals = dict(x_init=xs, dt_min=0.01, dt_max=0.08, n_contacts=2, swing_period=0.4, swing_height=0.07,
-                    swing_vel_limits=[0.1, -0.2], Q_diag=Q, R_diag=Rw, base_vel_des=[vx, 0, 0, 0, 0, 0],
-                    ext_force_des=[0, 0, 0], arm_vel_des=[0, 0, 0], tau_prev=np.zeros(R.nj), W_diag=W,
-                    contact_schedule=np.ones((4, N)), swing_schedule=np.zeros((4, N)))
-        P[b] = lay.pack(vals)
-        X[b] = x0
-        XS[b] = xs
-        T0[b] = t0
-    return lay, P, X, XS, T0
 
 
 def admm_bytes_per_problem_iter(sz):
@@ -85,39 +44,35 @@ def admm_bytes_per_problem_iter(sz):
 
 
 def cpu_baseline(R, dynamics, N, n_problems=2, n_steps=2):
-    """Oracle (numpy restatement of the reference path) on a bounded sample, 1 core."""
+    """Oracle (numpy restatement of the reference path) on a bounded sample, 1 core:
+    the same closed loop as the device (gait at t0 + k dt_min, warm start, one SQP
+    iteration, x <- integrate(x, DX[1]))."""
     sys.path.insert(0, HERE)
     from oracle.ocp import OracleOCP  # noqa: E402  (checker / baseline only)
+    from pinoloco.synthetic import problem_values
     lay, P, X, XS, T0 = build_batch(R, dynamics, N, n_problems, 0)
-    from pinoloco.gait import horizon_dts
-    o = OracleOCP(R, dynamics, N)
-    dts = horizon_dts(0.01, 0.08, N)
     elapsed, solves = 0.0, 0
     for b in range(n_problems):
         xs = XS[b].copy()
         x = X[b].copy()
-        oo = OracleOCP(R, dynamics, N)
+        o = OracleOCP(R, dynamics, N)
         for k in range(n_steps):
-            p = P[b].copy()
-            c, s = R.gait_sequence.get_gait_schedule(T0[b] + k * 0.01, dts, N)
-            vals = o.unpack(p)
-            p = oo.pack_params(x_init=xs, dt_min=0.01, dt_max=0.08, contact=c, swing=s, n_contacts=2,
-                               swing_period=0.4, swing_height=0.07, swing_vel_limits=[0.1, -0.2],
-                               Q_diag=vals["Q_diag"], R_diag=vals["R_diag"], base_vel_des=vals["base_vel_des"],
-                               ext_force_des=[0, 0, 0], arm_vel_des=[0, 0, 0], tau_prev=np.zeros(R.nj),
-                               W_diag=vals.get("W_diag", np.zeros(R.nj)))
+            vals, _, _ = problem_values(R, dynamics, N, b, lay, k)
+            vals["x_init"] = xs
+            p = lay.pack(vals)
             if k == 0:
-                oo.init_solver(x, p)  # OSQP setup: excluded like pl_ocp_init_solver
-            else:
-                x = oo.warm_start(x, p)
+                o.init_solver(x, p)  # OSQP setup: excluded like pl_ocp_init_solver
             t = time.perf_counter()
-            x, _, _ = oo.sqp_step(x, p)
-            DX, _ = oo.split(x)
-            xs = oo.integrate_state(xs, DX[1])
+            if k > 0:
+                x = o.warm_start(x, p)
+            x, _, _ = o.sqp_step(x, p)
+            DX, _ = o.split(x)
+            xs = o.integrate_state(xs, DX[1])
             elapsed += time.perf_counter() - t
             solves += 1
     return {"value": solves / elapsed, "unit": "solves/s", "cores": 1, "kind": "port",
-            "sample": f"{n_problems} problems x {n_steps} MPC steps, numpy oracle (oracle/), single thread"}
+            "sample": f"{n_problems} problems x {n_steps} MPC steps of the same workload, numpy oracle (oracle/), "
+                      f"single thread"}
 
 
 def main():
@@ -132,21 +87,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist_mod
-        torch.cuda.set_device(local_rank)
-        dist_mod.init_process_group("nccl")
-        dist = dist_mod
+    world, rank, local_rank = pdist.env_ranks()
+    dist = pdist.init("nccl")
 
     R = robots.ROBOTS[args.robot]()
     R.set_gait_sequence("trot", 0.8)
     B = args.batch
-    lay, P, X, XS, T0 = build_batch(R, args.dynamics, args.nodes, B, rank * B)
+    first, _ = shard(B * world, world, rank)
+    lay, P, X, XS, T0 = build_batch(R, args.dynamics, args.nodes, B, first)
     bo = BatchedOCP(R, args.dynamics, args.nodes, batch=B, device=local_rank, gait_type="trot", gait_period=0.8)
     bo.set_params(P)
     bo.set_x(X)
@@ -172,18 +120,17 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = bo.profile_read()
     bo.profile(0)
+    elapsed = pdist.max_over_ranks(elapsed, dist)
     if dist is not None:
+        # per-problem controller output [u_0, x_state] of the whole job, gathered over
+        # RCCL after the timed region (no collective on the data path)
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        # final gather of per-problem controls + states over RCCL (outside the timed region)
-        row = lay.nu[0] + lay.nx
-        mine = torch.empty((B, row), dtype=torch.float64, device=f"cuda:{local_rank}")
+        mine = torch.empty((B, lay.nu[0] + lay.nx), dtype=torch.float64, device=f"cuda:{local_rank}")
         bo.mpc_export(mine.data_ptr())
-        allp = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(allp, mine)
+        bo.sync()
+        allp = pdist.gather_rows(mine, dist)
         torch.cuda.synchronize()
+        assert allp.shape[0] == B * world
 
     sz = bo.sizes()
     bytes_it = admm_bytes_per_problem_iter(sz)

@@ -1,0 +1,89 @@
+"""The product's device math (csrc/rows.h, rbd.h, targets.h) compiled for the host.
+
+The same templated node-row function the GPU kernels instantiate
+(k_eval_values / k_eval_jac) is built for the CPU by tests/native/rows_host.cpp
+and compared against the numpy oracle: values and bounds of every row of every
+node, the forward-mode dual Jacobian column by column against the oracle's
+complex-step Jacobian, and dx_des.  Tolerance: 1e-12 relative to max |J|.
+"""
+import ctypes as C
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, make_robot
+from oracle.ocp import OracleOCP
+
+_dp = C.POINTER(C.c_double)
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc) and shutil.which(hipcc) is None:
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("rows") / "librows_host.so"
+    cmd = [hipcc, "-std=c++17", "-O2", "-fPIC", "-shared", "-x", "hip", "--offload-arch=gfx950",
+           "-Wno-unused-result", "-I", os.path.join(ROOT, "pino-locoman_amd", "csrc"),
+           os.path.join(ROOT, "tests", "native", "rows_host.cpp"), "-o", str(out)]
+    subprocess.run(cmd, check=True, capture_output=True)
+    return C.CDLL(str(out))
+
+
+def _consts(bo):
+    from pinoloco import _lib
+    L = _lib.lib()
+    sizes = (C.c_int * 2)()
+    _lib.check(L.pl_debug_consts(bo.h, None, None, sizes))
+    mb, ob = C.create_string_buffer(sizes[0]), C.create_string_buffer(sizes[1])
+    _lib.check(L.pl_debug_consts(bo.h, mb, ob, None))
+    return mb, ob
+
+
+@pytest.mark.parametrize("rname,dyn,N,nodes_checked", [
+    ("go2", "whole_body_rnea", 20, None),
+    ("b2", "whole_body_aba", 40, [0, 1, 2, 3, 20, 39]),
+    ("b2g", "whole_body_acc", 50, [0, 1, 25, 49]),
+    ("b2g", "whole_body_rnea", 50, [0, 2, 3, 26, 49]),
+])
+def test_node_rows_and_dual_jacobian(harness, rname, dyn, N, nodes_checked):
+    from pinoloco.ocp import BatchedOCP
+    from pinoloco.synthetic import build_batch
+    R = make_robot(rname)
+    bo = BatchedOCP(R, dyn, N, batch=1, device=-1)
+    mb, ob = _consts(bo)
+    o = OracleOCP(R, dyn, N)
+    lay, P, X, _, _ = build_batch(R, dyn, N, 1, 17)
+    rng = np.random.default_rng(4)
+    p = P[0].copy()
+    x = X[0] + rng.normal(0, 0.05, o.n)
+    g_ref, l_ref, u_ref = o.eval_g(x, p)
+    Jref = o.eval_J(x, p).tocsc()
+    scale = np.abs(Jref.data).max()
+    nt = bo.node_table()
+    dxd = np.zeros(lay.ndx)
+    harness.th_dx_des(mb, ob, p.ctypes.data_as(_dp), dxd.ctypes.data_as(_dp))
+    Pd = o.unpack(p)
+    assert np.abs(dxd - o.dx_des(Pd)).max() < 1e-13
+    for i in (nodes_checked if nodes_checked is not None else range(N)):
+        nw, ro, nrow = nt[i, 0], nt[i, 3], nt[i, 4]
+        xo, xn = lay.x_off[i], lay.x_off[i + 1]
+        dx = np.ascontiguousarray(x[xo:xo + lay.ndx])
+        u = np.ascontiguousarray(x[xo + lay.ndx:xn])
+        dxn = np.ascontiguousarray(x[xn:xn + lay.ndx])
+        g, lb, ub, tan = (np.zeros(nrow) for _ in range(4))
+        args = [p.ctypes.data_as(_dp), dx.ctypes.data_as(_dp), u.ctypes.data_as(_dp), dxn.ctypes.data_as(_dp)]
+        r = harness.th_node_rows(mb, ob, i, *args, -1, g.ctypes.data_as(_dp), lb.ctypes.data_as(_dp),
+                                 ub.ctypes.data_as(_dp), None)
+        assert r == nrow
+        assert np.abs(g - g_ref[ro:ro + nrow]).max() < 1e-12 * max(1.0, np.abs(g_ref).max())
+        assert np.array_equal(lb, l_ref[ro:ro + nrow]) and np.array_equal(ub, u_ref[ro:ro + nrow])
+        cols = list(range(xo, xo + nw)) + list(range(xn, xn + lay.ndx))
+        for lc, gc in enumerate(cols):
+            harness.th_node_rows(mb, ob, i, *args, lc, None, None, None, tan.ctypes.data_as(_dp))
+            ref = Jref[ro:ro + nrow, gc].toarray().ravel()
+            assert np.abs(tan - ref).max() <= 1e-12 * scale, (i, lc)
+    bo.close()
