@@ -162,8 +162,9 @@ int pl_state_difference(const pl_model* m, const double* x0, const double* x1, d
 
 /* Timing of the dominant kernel (ADMM sweeps) with HIP events on the handle's
  * stream: pl_ocp_profile(o, 1) clears and starts, pl_ocp_profile_read returns
- * [total_ms, launches, problem_iterations]. pl_ocp_sizes: [n, m, nnz,
- * factor doubles per problem, largest node block, N]. */
+ * [total_ms, launches, problem_iterations]. pl_ocp_sizes (out[10]): [n, m, nnz,
+ * factor doubles per problem, largest node block, N, ADMM gather program length,
+ * its LDS-resident part, ADMM LDS bytes per workgroup, A values per thread]. */
 int pl_ocp_profile(pl_ocp* o, int enable);
 int pl_ocp_profile_read(pl_ocp* o, double* out);
 int pl_ocp_sizes(const pl_ocp* o, long long* out);

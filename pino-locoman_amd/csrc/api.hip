@@ -39,6 +39,8 @@ struct pl_ocp {
   bool on_device;
   std::vector<PlNode> nodes;
   std::vector<int> colptr, rowidx, entcol, rowptr, rowent, cplrow, rownode, colnode;
+  std::vector<PlAdmmNode> anodes;
+  std::vector<uint16_t> aprog;
   std::vector<double> h_params;  // host copy of the parameters (B x np)
   std::vector<void*> allocs;
   hipEvent_t ev[5];
@@ -356,6 +358,122 @@ int build_layout(pl_ocp* o) {
   return 0;
 }
 
+// Gather programs of the ADMM sweeps (PlAdmmNode, state.h), one per distinct
+// local structure.
+int build_admm_prog(pl_ocp* o) {
+  PlOcpHandle& h = o->h;
+  const int N = h.oc.N, ndx = h.oc.ndx;
+  o->anodes.assign(N + 1, PlAdmmNode());
+  o->aprog.clear();
+  std::vector<std::vector<uint16_t>> progs;
+  std::vector<int> prog_off, prog_count;
+  h.ncpl_max = 0;
+  h.nent_max = 0;
+  for (int i = 0; i <= N; ++i) {
+    const PlNode& nd = o->nodes[i];
+    PlAdmmNode& a = o->anodes[i];
+    memset(&a, 0, sizeof(a));
+    a.nw = nd.nw; a.nrow = nd.nrow; a.ncol = nd.ncol; a.ncpl = nd.ncpl; a.nent = nd.nent;
+    a.nunit = nd.nunit; a.ntile = nd.ntile; a.x_off = nd.x_off; a.row_off = nd.row_off;
+    a.ent_off = nd.ent_off; a.s_off = nd.s_off;
+    if (nd.nent > 65535 || nd.ncol > 65535) { pl_set_error("node too large for u16 programs"); return -1; }
+    std::vector<uint16_t> P;
+    auto mark = [&](int& field) { field = (int)P.size(); };
+    const int* cp = o->colptr.data() + nd.colptr_off;
+    const int* rp = o->rowptr.data() + nd.rowptr_off;
+    const int* re = o->rowent.data() + nd.csr_off;
+    const int* rid = o->rowidx.data() + nd.ent_off;
+    const int* ecol = o->entcol.data() + nd.ent_off;
+    const int* cpl = o->cplrow.data() + nd.cpl_off;
+    std::vector<int> cpl_index(nd.nrow, -1);
+    for (int s = 0; s < nd.ncpl; ++s) cpl_index[cpl[s]] = s;
+    mark(a.rowptr);
+    for (int r = 0; r <= nd.nrow; ++r) P.push_back((uint16_t)(nd.nrow ? rp[r] : 0));
+    mark(a.rowe);
+    for (int q = 0; nd.nrow && q < rp[nd.nrow]; ++q) P.push_back((uint16_t)re[q]);
+    mark(a.rowc);
+    for (int q = 0; nd.nrow && q < rp[nd.nrow]; ++q) P.push_back((uint16_t)ecol[re[q]]);
+    mark(a.colptr);
+    for (int c = 0; c <= nd.ncol; ++c) P.push_back((uint16_t)(nd.ncol ? cp[c] : 0));
+    mark(a.colr);
+    for (int e = 0; e < nd.nent; ++e) P.push_back((uint16_t)rid[e]);
+    mark(a.cplr);
+    for (int s = 0; s < nd.ncpl; ++s) P.push_back((uint16_t)cpl[s]);
+    // coupling rows split into their w part and their dx_{i+1} part
+    std::vector<uint16_t> cwp{0}, cwe, cwc, cxp{0}, cxe, cxc;
+    for (int s = 0; s < nd.ncpl; ++s) {
+      const int r = cpl[s];
+      for (int q = rp[r]; q < rp[r + 1]; ++q) {
+        const int e = re[q], c = ecol[e];
+        if (c < nd.nw) { cwe.push_back((uint16_t)e); cwc.push_back((uint16_t)c); }
+        else { cxe.push_back((uint16_t)e); cxc.push_back((uint16_t)(c - nd.nw)); }
+      }
+      cwp.push_back((uint16_t)cwe.size());
+      cxp.push_back((uint16_t)cxe.size());
+    }
+    mark(a.cwptr); P.insert(P.end(), cwp.begin(), cwp.end());
+    mark(a.cwe); P.insert(P.end(), cwe.begin(), cwe.end());
+    mark(a.cwc); P.insert(P.end(), cwc.begin(), cwc.end());
+    mark(a.cxptr); P.insert(P.end(), cxp.begin(), cxp.end());
+    mark(a.cxe); P.insert(P.end(), cxe.begin(), cxe.end());
+    mark(a.cxc); P.insert(P.end(), cxc.begin(), cxc.end());
+    // per column: entries in coupling rows, as (entry, coupling index)
+    std::vector<uint16_t> ccp{0}, cce, ccs, xcp{0}, xce, xcs;
+    for (int c = 0; c < nd.nw && nd.ncol; ++c) {
+      for (int e = cp[c]; e < cp[c + 1]; ++e)
+        if (cpl_index[rid[e]] >= 0) { cce.push_back((uint16_t)e); ccs.push_back((uint16_t)cpl_index[rid[e]]); }
+      ccp.push_back((uint16_t)cce.size());
+    }
+    for (int c = 0; c < ndx && nd.ncol; ++c) {
+      for (int e = cp[nd.nw + c]; e < cp[nd.nw + c + 1]; ++e) {
+        if (cpl_index[rid[e]] < 0) { pl_set_error("dx_{i+1} entry outside a coupling row"); return -1; }
+        xce.push_back((uint16_t)e);
+        xcs.push_back((uint16_t)cpl_index[rid[e]]);
+      }
+      xcp.push_back((uint16_t)xce.size());
+    }
+    mark(a.ccptr); P.insert(P.end(), ccp.begin(), ccp.end());
+    mark(a.cce); P.insert(P.end(), cce.begin(), cce.end());
+    mark(a.ccs); P.insert(P.end(), ccs.begin(), ccs.end());
+    mark(a.xcptr); P.insert(P.end(), xcp.begin(), xcp.end());
+    mark(a.xce); P.insert(P.end(), xce.begin(), xce.end());
+    mark(a.xcs); P.insert(P.end(), xcs.begin(), xcs.end());
+    while (P.size() % 8) P.push_back(0);
+    int found = -1;
+    for (size_t k = 0; k < progs.size(); ++k)
+      if (progs[k] == P) { found = (int)k; break; }
+    if (found < 0) {
+      found = (int)progs.size();
+      progs.push_back(P);
+      prog_off.push_back((int)o->aprog.size());
+      o->aprog.insert(o->aprog.end(), P.begin(), P.end());
+    }
+    a.prog = prog_off[found];
+    a.prog_len = (int)progs[found].size();
+    if ((int)prog_count.size() <= found) prog_count.resize(found + 1, 0);
+    prog_count[found]++;
+    h.ncpl_max = std::max(h.ncpl_max, nd.ncpl);
+    h.nent_max = std::max(h.nent_max, nd.nent);
+  }
+  // the most frequent node program is kept in LDS by the ADMM kernel
+  int dom = 0;
+  for (size_t k = 0; k < prog_count.size(); ++k)
+    if (prog_count[k] > prog_count[dom]) dom = (int)k;
+  h.admm_dom_prog = prog_off[dom];
+  h.admm_dom_len = 0;  // LDS program buffer: the longest program
+  for (const auto& pr : progs) h.admm_dom_len = std::max(h.admm_dom_len, (int)pr.size());
+  int dom_nent = 0;
+  for (int i = 0; i <= N; ++i)
+    if (o->anodes[i].prog == h.admm_dom_prog) dom_nent = std::max(dom_nent, o->anodes[i].nent);
+  h.admm_asr = std::max(4, (dom_nent + 255) / 256);
+  if (h.admm_asr > 8) h.admm_asr = 8;
+  if (h.nrow_max > 256 || h.nw_max > 256) {
+    pl_set_error("ADMM kernel needs <= 256 rows and columns per node (rows %d)", h.nrow_max);
+    return -1;
+  }
+  return 0;
+}
+
 template <class T>
 int dalloc(pl_ocp* o, T** p, size_t count) {
   void* q = nullptr;
@@ -452,7 +570,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
     O.P.tau_prev = O.P.W_diag = -1;
   }
   O.P.np = off;
-  if (build_layout(o)) { delete o; return -1; }
+  if (build_layout(o) || build_admm_prog(o)) { delete o; return -1; }
   O.n = h.n;
   O.m = h.m;
   h.B = batch;
@@ -500,6 +618,8 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= upload(o, &D.cplrow, o->cplrow);
   rc |= upload(o, &D.rownode, o->rownode);
   rc |= upload(o, &D.colnode, o->colnode);
+  rc |= upload(o, &D.anodes, o->anodes);
+  rc |= upload(o, &D.aprog, o->aprog);
   const size_t n = h.n, m = h.m, nnz = h.nnz;
   rc |= dalloc(o, &D.p, B * h.np);
   rc |= dalloc(o, &D.x, B * n);
@@ -515,6 +635,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= dalloc(o, &D.ls, B * m);
   rc |= dalloc(o, &D.us, B * m);
   rc |= dalloc(o, &D.rho, B * m);
+  rc |= dalloc(o, &D.rhoc, B * (size_t)(h.N + 1) * std::max(h.ncpl_max, 1));
   rc |= dalloc(o, &D.D, B * n);
   rc |= dalloc(o, &D.E, B * m);
   rc |= dalloc(o, &D.cs, B);
@@ -837,10 +958,14 @@ extern "C" int pl_ocp_profile_read(pl_ocp* o, double* out) {
   return 0;
 }
 
-// Sizes the roofline accounting needs: [n, m, nnz, S_stride (doubles), nw_max, N].
+int admm_lds_bytes(const PlOcpHandle* h);
+
+// Sizes: [n, m, nnz, S_stride (doubles), nw_max, N, ADMM program length (u16),
+// LDS-resident program length, ADMM LDS bytes per workgroup, A values per thread].
 extern "C" int pl_ocp_sizes(const pl_ocp* o, long long* out) {
   if (!o) { pl_set_error("null handle"); return -1; }
   out[0] = o->h.n; out[1] = o->h.m; out[2] = o->h.nnz; out[3] = o->h.S_stride; out[4] = o->h.nw_max; out[5] = o->h.N;
+  out[6] = (long long)o->aprog.size(); out[7] = o->h.admm_dom_len; out[8] = admm_lds_bytes(&o->h); out[9] = o->h.admm_asr;
   return 0;
 }
 

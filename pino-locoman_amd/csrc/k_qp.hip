@@ -19,6 +19,8 @@
 // 8x4 sub-block rows 0..7, cols 4h..4h+3 of tile t; element pair k (0..15) of
 // unit u lives at s_off + (k * nunit + u) * 2 -> every 16-byte load instruction of
 // a wave is one contiguous 1 KiB segment.
+#include <algorithm>
+
 #include "state.h"
 
 #define PL_OSQP_INFTY 1e30
@@ -116,7 +118,7 @@ __device__ void for_row_entries(const PlDev& d, int r, F fn) {
 // ---------------------------------------------------------------------------
 // OSQP data update + Ruiz equilibration (osqp_update_lin_cost / _bounds / _A and
 // scale_data, OSQP 0.6 src/scaling.c), one workgroup per problem.
-__global__ __launch_bounds__(256) void k_qp_setup(PlDev d, int N, int n, int m, int nnz, PlSettings st) {
+__global__ __launch_bounds__(256) void k_qp_setup(PlDev d, int N, int n, int m, int nnz, int ncpl_max, PlSettings st) {
   const int b = blockIdx.x;
   __shared__ double red[256];
   __shared__ double s_c;
@@ -201,10 +203,19 @@ __global__ __launch_bounds__(256) void k_qp_setup(PlDev d, int N, int n, int m, 
     else rr = st.rho;
     rho[r] = rr;
   }
+  __syncthreads();
+  // rho of each node's coupling rows, contiguous for the ADMM prefetch
+  double* rhoc = d.rhoc + (size_t)b * (N + 1) * ncpl_max;
+  for (int i = 0; i < N; ++i) {
+    const PlNode& nd = d.nodes[i];
+    for (int s = threadIdx.x; s < nd.ncpl; s += blockDim.x)
+      rhoc[i * ncpl_max + s] = rho[nd.row_off + d.cplrow[nd.cpl_off + s]];
+  }
 }
 
 void launch_qp_setup(PlOcpHandle* h) {
-  hipLaunchKernelGGL(k_qp_setup, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz, h->set);
+  hipLaunchKernelGGL(k_qp_setup, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz,
+                     std::max(h->ncpl_max, 1), h->set);
 }
 
 // ---------------------------------------------------------------------------
@@ -465,71 +476,6 @@ void launch_factor(PlOcpHandle* h) {
                      h->S_stride, h->nw_max, h->set.sigma);
 }
 
-// ---------------------------------------------------------------------------
-// ADMM (OSQP 0.6 osqp_solve loop).  One workgroup per problem runs `niter`
-// iterations; the last one stores delta_x / delta_y for the termination check.
-namespace {
-
-struct AdmmLds {
-  double* v;      // mat-vec input (padded to 8 * ntile)
-  double* y;      // mat-vec output / w_i
-  double* xn;     // x~ of node i+1 (dx part)
-  double* trow;   // per local row temporaries (coupling t_r, s_r)
-  double* dpart;  // [nunit][8]
-  double* tpart;  // [nunit][4]
-};
-
-// y[0..nw) = S v for the node's tiled block; v must hold zeros past nw.
-__device__ void sym_matvec(const double* __restrict__ Sn, int nunit, int ntile, int nw, const double* v,
-                           double* y, double* dpart, double* tpart) {
-  const int u = threadIdx.x;
-  if (u < nunit) {
-    double2 T[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) T[k] = reinterpret_cast<const double2*>(Sn)[k * nunit + u];
-    const int t = u >> 1, h = u & 1;
-    int I = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-    while (I * (I + 1) / 2 > t) --I;
-    while ((I + 1) * (I + 2) / 2 <= t) ++I;
-    const int J = t - I * (I + 1) / 2;
-    double vj[4], vi[8];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) vj[c] = v[8 * J + 4 * h + c];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) vi[r] = v[8 * I + r];
-    double tp[4] = {0.0, 0.0, 0.0, 0.0};
-    // element (r, c) is pair (r*4+c)/2, slot (r*4+c)&1
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const double e0 = T[2 * r].x, e1 = T[2 * r].y, e2 = T[2 * r + 1].x, e3 = T[2 * r + 1].y;
-      dpart[u * 8 + r] = e0 * vj[0] + e1 * vj[1] + e2 * vj[2] + e3 * vj[3];
-      tp[0] += e0 * vi[r];
-      tp[1] += e1 * vi[r];
-      tp[2] += e2 * vi[r];
-      tp[3] += e3 * vi[r];
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) tpart[u * 4 + c] = (I != J) ? tp[c] : 0.0;
-  }
-  __syncthreads();
-  for (int o = threadIdx.x; o < nw; o += blockDim.x) {
-    const int I = o >> 3, r = o & 7;
-    double acc = 0.0;
-    for (int J = 0; J <= I; ++J) {
-      const int t = I * (I + 1) / 2 + J;
-      acc += dpart[(2 * t) * 8 + r] + dpart[(2 * t + 1) * 8 + r];
-    }
-    for (int Ip = I + 1; Ip < ntile; ++Ip) {
-      const int t = Ip * (Ip + 1) / 2 + I;
-      acc += tpart[(2 * t + (r >> 2)) * 4 + (r & 3)];
-    }
-    y[o] = acc;
-  }
-  __syncthreads();
-}
-
-}  // namespace
-
 // rhs = sigma x - q + A^T (rho z - y)   (before the first iteration of a solve)
 __global__ __launch_bounds__(256) void k_admm_init(PlDev d, int N, int n, int m, int nnz, double sigma) {
   const int b = blockIdx.x;
@@ -551,202 +497,6 @@ __global__ __launch_bounds__(256) void k_admm_init(PlDev d, int N, int n, int m,
 void launch_admm_init(PlOcpHandle* h) {
   hipLaunchKernelGGL(k_admm_init, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz,
                      h->set.sigma);
-}
-
-__global__ __launch_bounds__(256) void k_admm(PlDev d, int N, int n, int m, int nnz, int ndx, int S_stride,
-                                              int nw_max, int nunit_max, int nrow_max, int niter, int check,
-                                              double sigma, double alpha) {
-  const int b = blockIdx.x;
-  PlProbInfo* info = d.info + b;
-  if (info->done) return;
-  extern __shared__ double lds[];
-  const int vpad = ((nw_max + 7) / 8) * 8;
-  AdmmLds L;
-  L.v = lds;
-  L.y = L.v + vpad;
-  L.xn = L.y + vpad;
-  L.trow = L.xn + vpad;
-  L.dpart = L.trow + nrow_max;
-  L.tpart = L.dpart + 8 * nunit_max;
-  const double* As = d.As + (size_t)b * nnz;
-  const double* rho = d.rho + (size_t)b * m;
-  const double* ls = d.ls + (size_t)b * m;
-  const double* us = d.us + (size_t)b * m;
-  const double* qs = d.qs + (size_t)b * n;
-  const double* Sg = d.S + (size_t)b * S_stride;
-  double* za = d.za + (size_t)b * m;
-  double* ya = d.ya + (size_t)b * m;
-  double* xa = d.xa + (size_t)b * n;
-  double* rhs = d.rhs + (size_t)b * n;
-  double* bt = d.bt + (size_t)b * n;
-  double* dxs = d.dxs + (size_t)b * n;
-  double* dys = d.dys + (size_t)b * m;
-  const PlNode* nodes = d.nodes;
-  // trow is read for every row of a column during the backward gathers: it must
-  // hold zeros except for the entries a phase writes and clears.
-  for (int lr = threadIdx.x; lr < nrow_max; lr += blockDim.x) L.trow[lr] = 0.0;
-  __syncthreads();
-
-  for (int it = 0; it < niter; ++it) {
-    const bool store_delta = check && (it == niter - 1);
-    // ================= forward sweep
-    for (int i = 0; i <= N; ++i) {
-      const PlNode nd = nodes[i];
-      const int nw = nd.nw;
-      // coupling t_r = rho_r * a_r(w_{i-1}) . w_{i-1} for coupling rows of node i-1
-      if (i > 0) {
-        const PlNode pv = nodes[i - 1];
-        const int* rp = d.rowptr + pv.rowptr_off;
-        const int* re = d.rowent + pv.csr_off;
-        for (int s = threadIdx.x; s < pv.ncpl; s += blockDim.x) {
-          const int lr = d.cplrow[pv.cpl_off + s];
-          double acc = 0.0;
-          for (int q = rp[lr]; q < rp[lr + 1]; ++q) {
-            const int e = re[q];
-            const int lc = d.entcol[pv.ent_off + e];
-            if (lc < pv.nw) acc += As[pv.ent_off + e] * L.y[lc];
-          }
-          L.trow[lr] = rho[pv.row_off + lr] * acc;
-        }
-        __syncthreads();
-      }
-      // bt_i = rhs_i - K_{i,i-1} w_{i-1}
-      for (int c = threadIdx.x; c < ((nw + 7) & ~7); c += blockDim.x) {
-        double v = 0.0;
-        if (c < nw) {
-          v = rhs[nd.x_off + c];
-          if (i > 0 && c < ndx) {
-            const PlNode pv = nodes[i - 1];
-            const int* cp = d.colptr + pv.colptr_off;
-            const int col = pv.nw + c;
-            double acc = 0.0;
-            for (int e = cp[col]; e < cp[col + 1]; ++e) acc += As[pv.ent_off + e] * L.trow[d.rowidx[pv.ent_off + e]];
-            v -= acc;
-          }
-          bt[nd.x_off + c] = v;
-        }
-        L.v[c] = v;
-      }
-      __syncthreads();
-      sym_matvec(Sg + nd.s_off, nd.nunit, nd.ntile, nw, L.v, L.y, L.dpart, L.tpart);
-      // zero the coupling temporaries of node i-1 rows that were written
-      if (i > 0) {
-        const PlNode pv = nodes[i - 1];
-        for (int s = threadIdx.x; s < pv.ncpl; s += blockDim.x) L.trow[d.cplrow[pv.cpl_off + s]] = 0.0;
-      }
-      __syncthreads();
-    }
-    // ================= backward sweep
-    for (int i = N; i >= 0; --i) {
-      const PlNode nd = nodes[i];
-      const int nw = nd.nw;
-      // coupling t_r = rho_r * a_r(dx_{i+1}) . x~_{i+1}
-      if (i < N) {
-        const int* rp = d.rowptr + nd.rowptr_off;
-        const int* re = d.rowent + nd.csr_off;
-        for (int s = threadIdx.x; s < nd.ncpl; s += blockDim.x) {
-          const int lr = d.cplrow[nd.cpl_off + s];
-          double acc = 0.0;
-          for (int q = rp[lr]; q < rp[lr + 1]; ++q) {
-            const int e = re[q];
-            const int lc = d.entcol[nd.ent_off + e];
-            if (lc >= nw) acc += As[nd.ent_off + e] * L.xn[lc - nw];
-          }
-          L.trow[lr] = rho[nd.row_off + lr] * acc;
-        }
-        __syncthreads();
-      }
-      // v = bt_i - K_{i+1,i}^T x~_{i+1}
-      for (int c = threadIdx.x; c < ((nw + 7) & ~7); c += blockDim.x) {
-        double v = 0.0;
-        if (c < nw) {
-          v = bt[nd.x_off + c];
-          if (i < N) {
-            const int* cp = d.colptr + nd.colptr_off;
-            double acc = 0.0;
-            for (int e = cp[c]; e < cp[c + 1]; ++e) acc += As[nd.ent_off + e] * L.trow[d.rowidx[nd.ent_off + e]];
-            v -= acc;
-          }
-        }
-        L.v[c] = v;
-      }
-      __syncthreads();
-      if (i < N) {
-        for (int s = threadIdx.x; s < nd.ncpl; s += blockDim.x) L.trow[d.cplrow[nd.cpl_off + s]] = 0.0;
-      }
-      sym_matvec(Sg + nd.s_off, nd.nunit, nd.ntile, nw, L.v, L.y, L.dpart, L.tpart);
-      // L.y = x~_i.  Rows of node i: z~ = A x~, relaxed z / y updates (update_z, update_y)
-      for (int lr = threadIdx.x; lr < nd.nrow; lr += blockDim.x) {
-        const int r = nd.row_off + lr;
-        const int* rp = d.rowptr + nd.rowptr_off;
-        const int* re = d.rowent + nd.csr_off;
-        double zt = 0.0;
-        for (int q = rp[lr]; q < rp[lr + 1]; ++q) {
-          const int e = re[q];
-          const int lc = d.entcol[nd.ent_off + e];
-          zt += As[nd.ent_off + e] * (lc < nw ? L.y[lc] : L.xn[lc - nw]);
-        }
-        const double zp = za[r], yv = ya[r], rr = rho[r];
-        const double zrel = alpha * zt + (1.0 - alpha) * zp;
-        double zn = zrel + (1.0 / rr) * yv;
-        zn = fmin(fmax(zn, ls[r]), us[r]);
-        const double dy = rr * (zrel - zn);
-        const double yn = yv + dy;
-        za[r] = zn;
-        ya[r] = yn;
-        if (store_delta) dys[r] = dy;
-        L.trow[lr] = rr * zn - yn;  // s_r for the next rhs
-      }
-      __syncthreads();
-      // x update and next-iteration rhs contributions of the rows of node i
-      for (int c = threadIdx.x; c < nw; c += blockDim.x) {
-        const int j = nd.x_off + c;
-        const double xp = xa[j];
-        const double xn = alpha * L.y[c] + (1.0 - alpha) * xp;
-        xa[j] = xn;
-        if (store_delta) dxs[j] = xn - xp;
-        double acc = sigma * xn - qs[j];
-        if (i < N) {
-          const int* cp = d.colptr + nd.colptr_off;
-          for (int e = cp[c]; e < cp[c + 1]; ++e) acc += As[nd.ent_off + e] * L.trow[d.rowidx[nd.ent_off + e]];
-        }
-        rhs[j] = acc;
-      }
-      if (i < N) {
-        const int* cp = d.colptr + nd.colptr_off;
-        for (int c = threadIdx.x; c < ndx; c += blockDim.x) {
-          double acc = 0.0;
-          for (int e = cp[nw + c]; e < cp[nw + c + 1]; ++e) acc += As[nd.ent_off + e] * L.trow[d.rowidx[nd.ent_off + e]];
-          rhs[nodes[i + 1].x_off + c] += acc;
-        }
-      }
-      __syncthreads();
-      for (int c = threadIdx.x; c < ndx; c += blockDim.x) L.xn[c] = L.y[c];
-      for (int lr = threadIdx.x; lr < nd.nrow; lr += blockDim.x) L.trow[lr] = 0.0;
-      __syncthreads();
-    }
-  }
-  if (threadIdx.x == 0) info->iter += niter;
-}
-
-void launch_admm(PlOcpHandle* h, int niter, int check, int it_base) {
-  (void)it_base;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)k_admm, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
-    attr = true;
-  }
-  const int vpad = ((h->nw_max + 7) / 8) * 8;
-  const size_t lds = sizeof(double) * (3 * (size_t)vpad + h->nrow_max + 12 * (size_t)h->nunit_max);
-  const bool prof = h->profile && h->prof_n < 64;
-  if (prof) hipEventRecord(h->prof_ev[h->prof_n][0], h->stream);
-  hipLaunchKernelGGL(k_admm, dim3(h->B), dim3(256), lds, h->stream, h->d, h->N, h->n, h->m, h->nnz, h->ndx,
-                     h->S_stride, h->nw_max, h->nunit_max, h->nrow_max, niter, check, h->set.sigma, h->set.alpha);
-  if (prof) {
-    hipEventRecord(h->prof_ev[h->prof_n][1], h->stream);
-    h->prof_n++;
-    h->prof_admm_iters += (long long)h->B * niter;
-  }
 }
 
 // ---------------------------------------------------------------------------

@@ -32,6 +32,26 @@ struct PlNode {
   int pad[2];
 };
 
+// Gather program of one node for the ADMM sweeps (k_admm.hip).  All lists are
+// u16 offsets relative to `prog`, and nodes with identical local structure share
+// one program (3-4 programs per OCP), so the whole table is L1/L2 resident.
+//   row lists  (CSR over the node's rows):       rowptr[nrow+1], rowe[], rowc[]
+//   col lists  (CSC, entries in storage order):  colptr[ncol+1], colr[]
+//   coupling rows (rows with a dx_{i+1} entry):  cplr[ncpl]
+//     w-part of each coupling row:               cwptr[ncpl+1], cwe[], cwc[]
+//     dx_{i+1}-part of each coupling row:        cxptr[ncpl+1], cxe[], cxc[] (col - nw)
+//   per column c < nw, entries in coupling rows: ccptr[nw+1], cce[], ccs[] (coupling index)
+//   per dx_{i+1} column c < ndx:                 xcptr[ndx+1], xce[], xcs[]
+struct PlAdmmNode {
+  int nw, nrow, ncol, ncpl, nent, nunit, ntile;
+  int x_off, row_off, ent_off, s_off;
+  int prog;
+  int rowptr, rowe, rowc, colptr, colr, cplr;
+  int cwptr, cwe, cwc, cxptr, cxe, cxc, ccptr, cce, ccs, xcptr, xce, xcs;
+  int prog_len;    // u16 words of the node's program
+  int pad;
+};
+
 struct PlSettings {
   double rho, sigma, alpha, eps_abs, eps_rel, eps_prim_inf, eps_dual_inf;
   int max_iter, scaling, check_termination, warm_start;
@@ -66,6 +86,8 @@ struct PlDev {
   int* cplrow;       // coupling rows (local row ids)
   int* rownode;      // global row -> node
   int* colnode;      // global column -> node
+  PlAdmmNode* anodes;    // N + 1 ADMM gather programs
+  uint16_t* aprog;
   // per problem [B][*]
   double* p;         // params
   double* x;         // SQP iterate (decision vector)
@@ -81,6 +103,7 @@ struct PlDev {
   double* ls;
   double* us;
   double* rho;
+  double* rhoc;      // rho of the coupling rows, [N+1][ncpl_max] per problem (ADMM prefetch)
   double* D;
   double* E;
   double* cs;        // cost scaling c (1 per problem)
@@ -111,6 +134,9 @@ struct PlOcpHandle {
   int B;
   int N, n, m, np, nnz, nx, ndx, nw_max, ncol_max, nrow_max, S_stride;
   int nunit_max;
+  int ncpl_max, nent_max;
+  int admm_dom_prog, admm_dom_len;  // most frequent ADMM gather program (kept in LDS)
+  int admm_asr;                     // A values per thread staged through registers
   PlSettings set;
   PlModel model;
   PlOcpConst oc;
