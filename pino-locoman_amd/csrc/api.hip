@@ -6,6 +6,7 @@
 // iteration exactly as OCP.solve() sequences sqp_data -> osqp.update ->
 // osqp.solve -> line search (ocp.py:375-414).
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -369,6 +370,7 @@ int build_admm_prog(pl_ocp* o) {
   std::vector<int> prog_off, prog_count;
   h.ncpl_max = 0;
   h.nent_max = 0;
+  h.chunk_max = 1;
   for (int i = 0; i <= N; ++i) {
     const PlNode& nd = o->nodes[i];
     PlAdmmNode& a = o->anodes[i];
@@ -379,6 +381,14 @@ int build_admm_prog(pl_ocp* o) {
     if (nd.nent > 65535 || nd.ncol > 65535) { pl_set_error("node too large for u16 programs"); return -1; }
     std::vector<uint16_t> P;
     auto mark = [&](int& field) { field = (int)P.size(); };
+    auto mark2 = [&](int& field) {  // pair lists start on a 32-bit boundary
+      if (P.size() & 1) P.push_back(0);
+      field = (int)P.size();
+    };
+    auto pair = [&](int e, int c) {
+      P.push_back((uint16_t)e);
+      P.push_back((uint16_t)c);
+    };
     const int* cp = o->colptr.data() + nd.colptr_off;
     const int* rp = o->rowptr.data() + nd.rowptr_off;
     const int* re = o->rowent.data() + nd.csr_off;
@@ -389,10 +399,8 @@ int build_admm_prog(pl_ocp* o) {
     for (int s = 0; s < nd.ncpl; ++s) cpl_index[cpl[s]] = s;
     mark(a.rowptr);
     for (int r = 0; r <= nd.nrow; ++r) P.push_back((uint16_t)(nd.nrow ? rp[r] : 0));
-    mark(a.rowe);
-    for (int q = 0; nd.nrow && q < rp[nd.nrow]; ++q) P.push_back((uint16_t)re[q]);
-    mark(a.rowc);
-    for (int q = 0; nd.nrow && q < rp[nd.nrow]; ++q) P.push_back((uint16_t)ecol[re[q]]);
+    mark2(a.rowp);
+    for (int q = 0; nd.nrow && q < rp[nd.nrow]; ++q) pair(re[q], ecol[re[q]]);
     mark(a.colptr);
     for (int c = 0; c <= nd.ncol; ++c) P.push_back((uint16_t)(nd.ncol ? cp[c] : 0));
     mark(a.colr);
@@ -400,44 +408,75 @@ int build_admm_prog(pl_ocp* o) {
     mark(a.cplr);
     for (int s = 0; s < nd.ncpl; ++s) P.push_back((uint16_t)cpl[s]);
     // coupling rows split into their w part and their dx_{i+1} part
-    std::vector<uint16_t> cwp{0}, cwe, cwc, cxp{0}, cxe, cxc;
+    std::vector<int> cwp{0}, cxp{0};
+    std::vector<std::pair<int, int>> cw, cx;
     for (int s = 0; s < nd.ncpl; ++s) {
       const int r = cpl[s];
       for (int q = rp[r]; q < rp[r + 1]; ++q) {
         const int e = re[q], c = ecol[e];
-        if (c < nd.nw) { cwe.push_back((uint16_t)e); cwc.push_back((uint16_t)c); }
-        else { cxe.push_back((uint16_t)e); cxc.push_back((uint16_t)(c - nd.nw)); }
+        if (c < nd.nw) cw.push_back({e, c});
+        else cx.push_back({e, c - nd.nw});
       }
-      cwp.push_back((uint16_t)cwe.size());
-      cxp.push_back((uint16_t)cxe.size());
+      cwp.push_back((int)cw.size());
+      cxp.push_back((int)cx.size());
     }
-    mark(a.cwptr); P.insert(P.end(), cwp.begin(), cwp.end());
-    mark(a.cwe); P.insert(P.end(), cwe.begin(), cwe.end());
-    mark(a.cwc); P.insert(P.end(), cwc.begin(), cwc.end());
-    mark(a.cxptr); P.insert(P.end(), cxp.begin(), cxp.end());
-    mark(a.cxe); P.insert(P.end(), cxe.begin(), cxe.end());
-    mark(a.cxc); P.insert(P.end(), cxc.begin(), cxc.end());
+    mark(a.cwptr);
+    for (int x : cwp) P.push_back((uint16_t)x);
+    mark2(a.cwp);
+    for (auto& pr : cw) pair(pr.first, pr.second);
+    mark(a.cxptr);
+    for (int x : cxp) P.push_back((uint16_t)x);
+    mark2(a.cxp);
+    for (auto& pr : cx) pair(pr.first, pr.second);
     // per column: entries in coupling rows, as (entry, coupling index)
-    std::vector<uint16_t> ccp{0}, cce, ccs, xcp{0}, xce, xcs;
+    std::vector<int> ccp{0}, xcp{0};
+    std::vector<std::pair<int, int>> cc, xc;
     for (int c = 0; c < nd.nw && nd.ncol; ++c) {
       for (int e = cp[c]; e < cp[c + 1]; ++e)
-        if (cpl_index[rid[e]] >= 0) { cce.push_back((uint16_t)e); ccs.push_back((uint16_t)cpl_index[rid[e]]); }
-      ccp.push_back((uint16_t)cce.size());
+        if (cpl_index[rid[e]] >= 0) cc.push_back({e, cpl_index[rid[e]]});
+      ccp.push_back((int)cc.size());
     }
     for (int c = 0; c < ndx && nd.ncol; ++c) {
       for (int e = cp[nd.nw + c]; e < cp[nd.nw + c + 1]; ++e) {
         if (cpl_index[rid[e]] < 0) { pl_set_error("dx_{i+1} entry outside a coupling row"); return -1; }
-        xce.push_back((uint16_t)e);
-        xcs.push_back((uint16_t)cpl_index[rid[e]]);
+        xc.push_back({e, cpl_index[rid[e]]});
       }
-      xcp.push_back((uint16_t)xce.size());
+      xcp.push_back((int)xc.size());
     }
-    mark(a.ccptr); P.insert(P.end(), ccp.begin(), ccp.end());
-    mark(a.cce); P.insert(P.end(), cce.begin(), cce.end());
-    mark(a.ccs); P.insert(P.end(), ccs.begin(), ccs.end());
-    mark(a.xcptr); P.insert(P.end(), xcp.begin(), xcp.end());
-    mark(a.xce); P.insert(P.end(), xce.begin(), xce.end());
-    mark(a.xcs); P.insert(P.end(), xcs.begin(), xcs.end());
+    mark(a.ccptr);
+    for (int x : ccp) P.push_back((uint16_t)x);
+    mark2(a.ccp);
+    for (auto& pr : cc) pair(pr.first, pr.second);
+    mark(a.xcptr);
+    for (int x : xcp) P.push_back((uint16_t)x);
+    mark2(a.xcp);
+    for (auto& pr : xc) pair(pr.first, pr.second);
+    // balanced chunks of <= PL_CHUNK entries for the row and column gathers
+    {
+      std::vector<std::pair<int, int>> ch;
+      std::vector<int> ptr{0};
+      for (int r = 0; r < nd.nrow; ++r) {
+        for (int q = rp[r]; q < rp[r + 1]; q += PL_CHUNK) ch.push_back({q, std::min(q + PL_CHUNK, rp[r + 1])});
+        ptr.push_back((int)ch.size());
+      }
+      a.rchn = (int)ch.size();
+      mark2(a.rch);
+      for (auto& c : ch) pair(c.first, c.second);
+      mark(a.rchptr);
+      for (int x : ptr) P.push_back((uint16_t)x);
+      ch.clear();
+      ptr.assign(1, 0);
+      for (int c = 0; c < nd.ncol; ++c) {
+        for (int e = cp[c]; e < cp[c + 1]; e += PL_CHUNK) ch.push_back({e, std::min(e + PL_CHUNK, cp[c + 1])});
+        ptr.push_back((int)ch.size());
+      }
+      a.cchn = (int)ch.size();
+      mark2(a.cch);
+      for (auto& c : ch) pair(c.first, c.second);
+      mark(a.cchptr);
+      for (int x : ptr) P.push_back((uint16_t)x);
+      h.chunk_max = std::max(h.chunk_max, std::max(a.rchn, a.cchn));
+    }
     while (P.size() % 8) P.push_back(0);
     int found = -1;
     for (size_t k = 0; k < progs.size(); ++k)
@@ -477,7 +516,7 @@ int build_admm_prog(pl_ocp* o) {
 template <class T>
 int dalloc(pl_ocp* o, T** p, size_t count) {
   void* q = nullptr;
-  if (count == 0) count = 1;
+  count += 256;  // slack: kernels issue clamped, unconditional loads up to one row past the end
   hipError_t e = hipMalloc(&q, count * sizeof(T));
   if (e != hipSuccess) {
     pl_set_error("hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
@@ -657,6 +696,8 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= dalloc(o, &D.info, B);
   rc |= dalloc(o, &D.t0, B);
   rc |= dalloc(o, &D.xstate, B * (size_t)h.nx);
+  D.dbg = nullptr;
+  if (getenv("PL_ADMM_TIMING") && atoi(getenv("PL_ADMM_TIMING")) > 0) rc |= dalloc(o, &D.dbg, B * 16);
   if (rc) { pl_ocp_destroy(o); return -2; }
   if (hipMemcpy(D.model, &h.model, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(D.oc, &h.oc, sizeof(PlOcpConst), hipMemcpyHostToDevice) != hipSuccess) {
@@ -978,7 +1019,7 @@ extern "C" int pl_debug_get(pl_ocp* o, const char* name, double* out, long long 
       {"As", h->d.As, B * h->nnz}, {"Araw", h->d.Araw, B * h->nnz}, {"qs", h->d.qs, B * h->n},
       {"ls", h->d.ls, B * h->m},   {"us", h->d.us, B * h->m},       {"rho", h->d.rho, B * h->m},
       {"D", h->d.D, B * h->n},     {"E", h->d.E, B * h->m},         {"cs", h->d.cs, B},
-      {"Ps", h->d.Ps, B * h->n},   {"P", h->d.P, B * h->n},         {"xa", h->d.xa, B * h->n},
+      {"admm_t", h->d.dbg, h->d.dbg ? B * 16 : 0}, {"Ps", h->d.Ps, B * h->n},   {"P", h->d.P, B * h->n},         {"xa", h->d.xa, B * h->n},
       {"za", h->d.za, B * h->m},   {"ya", h->d.ya, B * h->m},       {"S", h->d.S, B * (size_t)h->S_stride},
       {"rhs", h->d.rhs, B * h->n}, {"step", h->d.step, B * h->n},   {"grad", h->d.grad, B * h->n},
       {"g", h->d.g, B * h->m},     {"xstate", h->d.xstate, B * h->nx}};

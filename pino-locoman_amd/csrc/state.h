@@ -33,23 +33,27 @@ struct PlNode {
 };
 
 // Gather program of one node for the ADMM sweeps (k_admm.hip).  All lists are
-// u16 offsets relative to `prog`, and nodes with identical local structure share
-// one program (3-4 programs per OCP), so the whole table is L1/L2 resident.
-//   row lists  (CSR over the node's rows):       rowptr[nrow+1], rowe[], rowc[]
-//   col lists  (CSC, entries in storage order):  colptr[ncol+1], colr[]
+// u16 offsets relative to `prog`; nodes with identical local structure share
+// one program (3-4 programs per OCP).  Pair lists hold (entry, index) as two
+// consecutive u16 (one 32-bit read; their offsets are even):
+//   rows (CSR over the node's rows):             rowptr[nrow+1], rowp[] = (entry, local col)
+//   cols (CSC, entries in storage order):        colptr[ncol+1], colr[] = local row
 //   coupling rows (rows with a dx_{i+1} entry):  cplr[ncpl]
-//     w-part of each coupling row:               cwptr[ncpl+1], cwe[], cwc[]
-//     dx_{i+1}-part of each coupling row:        cxptr[ncpl+1], cxe[], cxc[] (col - nw)
-//   per column c < nw, entries in coupling rows: ccptr[nw+1], cce[], ccs[] (coupling index)
-//   per dx_{i+1} column c < ndx:                 xcptr[ndx+1], xce[], xcs[]
+//     w part of each coupling row:               cwptr[ncpl+1], cwp[] = (entry, col)
+//     dx_{i+1} part of each coupling row:        cxptr[ncpl+1], cxp[] = (entry, col - nw)
+//   per column c < nw, entries in coupling rows: ccptr[nw+1],   ccp[] = (entry, coupling index)
+//   per dx_{i+1} column c < ndx:                 xcptr[ndx+1],  xcp[] = (entry, coupling index)
+//   row chunks (<= PL_CHUNK entries of one row): rchn chunks rch[] = (q0, q1) into rowp,
+//                                                rchptr[nrow+1] = first chunk of each row
+//   column chunks (<= PL_CHUNK entries):         cchn chunks cch[] = (e0, e1), cchptr[ncol+1]
+#define PL_CHUNK 6
 struct PlAdmmNode {
   int nw, nrow, ncol, ncpl, nent, nunit, ntile;
   int x_off, row_off, ent_off, s_off;
-  int prog;
-  int rowptr, rowe, rowc, colptr, colr, cplr;
-  int cwptr, cwe, cwc, cxptr, cxe, cxc, ccptr, cce, ccs, xcptr, xce, xcs;
-  int prog_len;    // u16 words of the node's program
-  int pad;
+  int prog, prog_len;
+  int rowptr, rowp, colptr, colr, cplr, cwptr, cwp, cxptr, cxp, ccptr, ccp, xcptr, xcp;
+  int rchn, rch, rchptr, cchn, cch, cchptr;
+  int pad[1];
 };
 
 struct PlSettings {
@@ -126,6 +130,7 @@ struct PlDev {
   // MPC (device loop)
   double* t0;        // per-problem gait time offset
   double* xstate;    // per-problem current state x_init (nx)
+  double* dbg;       // optional kernel timing [B][16] (PL_ADMM_TIMING=1 at handle creation)
 };
 
 struct PlOcpHandle {
@@ -135,6 +140,7 @@ struct PlOcpHandle {
   int N, n, m, np, nnz, nx, ndx, nw_max, ncol_max, nrow_max, S_stride;
   int nunit_max;
   int ncpl_max, nent_max;
+  int chunk_max;                    // max(rchn, cchn) over nodes (ADMM partial-sum buffer)
   int admm_dom_prog, admm_dom_len;  // most frequent ADMM gather program (kept in LDS)
   int admm_asr;                     // A values per thread staged through registers
   PlSettings set;

@@ -1,0 +1,40 @@
+"""Phase timing of the ADMM sweep kernel (s_memtime, thread 0 of each workgroup).
+
+Run on the GPU box:  python tools/gpu_admm_timing.py [B]
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+os.environ["PL_ADMM_TIMING"] = "1"
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "pino-locoman_amd"))
+from pinoloco import robots  # noqa: E402
+from pinoloco.ocp import BatchedOCP  # noqa: E402
+from pinoloco.synthetic import build_batch  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+N = 50
+R = robots.ROBOTS["b2g"]()
+R.set_gait_sequence("trot", 0.8)
+lay, P, X, XS, T0 = build_batch(R, "whole_body_rnea", N, B, 0)
+bo = BatchedOCP(R, "whole_body_rnea", N, batch=B, device=0)
+bo.set_params(P)
+bo.set_x(X)
+bo.init_solver()
+t = time.time()
+st = bo.solve(timed=True)
+print("solve s", time.time() - t, "phase_ms", st["phase_ms"], "iters", np.bincount(st["admm_iters"]).nonzero())
+T = bo.debug("admm_t", B * 16).reshape(B, 16)
+it = st["admm_iters"].astype(float)
+steps = it * (N + 1)  # per direction
+names = ["f:bar0", "f:stageA", "f:gather+bar", "f:mv+bar", "f:issue", "f:reduce", "-", "-",
+         "b:bar0", "b:stageA", "b:gather+bar", "b:mv+bar", "b:issue", "b:reduce+bar", "b:rows+bar", "b:cols"]
+per = T / steps[:, None]
+for k, nm in enumerate(names):
+    if nm != "-":
+        print(f"{nm:14s} mean cycles/step {per[:, k].mean():9.1f}  p10 {np.percentile(per[:, k], 10):9.1f}  "
+              f"p90 {np.percentile(per[:, k], 90):9.1f}")
+print("total cycles/step fwd", per[:, :6].sum(1).mean(), "bwd", per[:, 8:].sum(1).mean())
