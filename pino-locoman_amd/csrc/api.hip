@@ -371,6 +371,7 @@ int build_admm_prog(pl_ocp* o) {
   h.ncpl_max = 0;
   h.nent_max = 0;
   h.chunk_max = 1;
+  h.flen_max = 2;
   for (int i = 0; i <= N; ++i) {
     const PlNode& nd = o->nodes[i];
     PlAdmmNode& a = o->anodes[i];
@@ -397,16 +398,19 @@ int build_admm_prog(pl_ocp* o) {
     const int* cpl = o->cplrow.data() + nd.cpl_off;
     std::vector<int> cpl_index(nd.nrow, -1);
     for (int s = 0; s < nd.ncpl; ++s) cpl_index[cpl[s]] = s;
+    // prefix used by the factor kernel: rowptr, cplr, rowp (flen u16 words)
     mark(a.rowptr);
     for (int r = 0; r <= nd.nrow; ++r) P.push_back((uint16_t)(nd.nrow ? rp[r] : 0));
+    mark(a.cplr);
+    for (int s = 0; s < nd.ncpl; ++s) P.push_back((uint16_t)cpl[s]);
     mark2(a.rowp);
     for (int q = 0; nd.nrow && q < rp[nd.nrow]; ++q) pair(re[q], ecol[re[q]]);
+    if (P.size() & 1) P.push_back(0);
+    a.flen = (int)P.size();
     mark(a.colptr);
     for (int c = 0; c <= nd.ncol; ++c) P.push_back((uint16_t)(nd.ncol ? cp[c] : 0));
     mark(a.colr);
     for (int e = 0; e < nd.nent; ++e) P.push_back((uint16_t)rid[e]);
-    mark(a.cplr);
-    for (int s = 0; s < nd.ncpl; ++s) P.push_back((uint16_t)cpl[s]);
     // coupling rows split into their w part and their dx_{i+1} part
     std::vector<int> cwp{0}, cxp{0};
     std::vector<std::pair<int, int>> cw, cx;
@@ -477,6 +481,7 @@ int build_admm_prog(pl_ocp* o) {
       for (int x : ptr) P.push_back((uint16_t)x);
       h.chunk_max = std::max(h.chunk_max, std::max(a.rchn, a.cchn));
     }
+    h.flen_max = std::max(h.flen_max, a.flen);
     while (P.size() % 8) P.push_back(0);
     int found = -1;
     for (size_t k = 0; k < progs.size(); ++k)
@@ -506,6 +511,10 @@ int build_admm_prog(pl_ocp* o) {
     if (o->anodes[i].prog == h.admm_dom_prog) dom_nent = std::max(dom_nent, o->anodes[i].nent);
   h.admm_asr = std::max(4, (dom_nent + 255) / 256);
   if (h.admm_asr > 8) h.admm_asr = 8;
+  if (ndx > 48) {
+    pl_set_error("state dimension 2 nv = %d > 48 is not supported by the factor kernel", ndx);
+    return -1;
+  }
   if (h.nrow_max > 256 || h.nw_max > 256) {
     pl_set_error("ADMM kernel needs <= 256 rows and columns per node (rows %d)", h.nrow_max);
     return -1;
@@ -689,15 +698,12 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= dalloc(o, &D.aty, B * n);
   rc |= dalloc(o, &D.step, B * n);
   rc |= dalloc(o, &D.S, B * (size_t)h.S_stride);
-  rc |= dalloc(o, &D.Kc, B * (size_t)h.ndx * h.nw_max);
-  rc |= dalloc(o, &D.Uc, B * (size_t)h.ndx * h.nw_max);
-  rc |= dalloc(o, &D.Cs, B * (size_t)h.ndx * h.ndx);
   rc |= dalloc(o, &D.work, B * 8);
   rc |= dalloc(o, &D.info, B);
   rc |= dalloc(o, &D.t0, B);
   rc |= dalloc(o, &D.xstate, B * (size_t)h.nx);
   D.dbg = nullptr;
-  if (getenv("PL_ADMM_TIMING") && atoi(getenv("PL_ADMM_TIMING")) > 0) rc |= dalloc(o, &D.dbg, B * 16);
+  if (getenv("PL_ADMM_TIMING") && atoi(getenv("PL_ADMM_TIMING")) > 0) rc |= dalloc(o, &D.dbg, B * 32);
   if (rc) { pl_ocp_destroy(o); return -2; }
   if (hipMemcpy(D.model, &h.model, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(D.oc, &h.oc, sizeof(PlOcpConst), hipMemcpyHostToDevice) != hipSuccess) {
@@ -1019,7 +1025,7 @@ extern "C" int pl_debug_get(pl_ocp* o, const char* name, double* out, long long 
       {"As", h->d.As, B * h->nnz}, {"Araw", h->d.Araw, B * h->nnz}, {"qs", h->d.qs, B * h->n},
       {"ls", h->d.ls, B * h->m},   {"us", h->d.us, B * h->m},       {"rho", h->d.rho, B * h->m},
       {"D", h->d.D, B * h->n},     {"E", h->d.E, B * h->m},         {"cs", h->d.cs, B},
-      {"admm_t", h->d.dbg, h->d.dbg ? B * 16 : 0}, {"Ps", h->d.Ps, B * h->n},   {"P", h->d.P, B * h->n},         {"xa", h->d.xa, B * h->n},
+      {"admm_t", h->d.dbg, h->d.dbg ? B * 32 : 0}, {"Ps", h->d.Ps, B * h->n},   {"P", h->d.P, B * h->n},         {"xa", h->d.xa, B * h->n},
       {"za", h->d.za, B * h->m},   {"ya", h->d.ya, B * h->m},       {"S", h->d.S, B * (size_t)h->S_stride},
       {"rhs", h->d.rhs, B * h->n}, {"step", h->d.step, B * h->n},   {"grad", h->d.grad, B * h->n},
       {"g", h->d.g, B * h->m},     {"xstate", h->d.xstate, B * h->nx}};

@@ -218,264 +218,6 @@ void launch_qp_setup(PlOcpHandle* h) {
                      std::max(h->ncpl_max, 1), h->set);
 }
 
-// ---------------------------------------------------------------------------
-// Block factorisation: for i = 0..N
-//   Kt_ii = diag(P + sigma) + sum_{rows of node i} rho a a^T |_{w_i}
-//         + sum_{coupling rows of node i-1} rho a a^T |_{dx_i} - C_i
-//   S_i = Kt_ii^-1 (Gauss-Jordan, register-blocked 7x7 per thread)
-//   Kc  = K_{i+1,i} (coupling rows of node i),  U = Kc S_i,  C_{i+1} = U Kc^T.
-// One workgroup (256 threads = 16 x 16 blocks of 7x7) per problem.
-#define FB 7
-#define FG 16
-#define FCH 16  // rows per assembly chunk
-
-namespace {
-
-// Fill the dense chunk buf[s][c - c0] (c in [c0, c0 + W)) with the scaled A
-// entries of rows rows[s] of node i; rw[s] = rho of the row.
-__device__ void fill_chunk(const PlDev& d, const double* As, const double* rho, int i, const int* rows, int nr,
-                           int c0, int W, double* buf, double* rw) {
-  const PlNode& nd = d.nodes[i];
-  for (int t = threadIdx.x; t < FCH * W; t += blockDim.x) buf[t] = 0.0;
-  __syncthreads();
-  const int* rp = d.rowptr + nd.rowptr_off;
-  const int* re = d.rowent + nd.csr_off;
-  for (int s = threadIdx.x / 16; s < nr; s += blockDim.x / 16) {
-    const int lr = rows[s];
-    for (int q = rp[lr] + (threadIdx.x & 15); q < rp[lr + 1]; q += 16) {
-      const int e = re[q];
-      const int lc = d.entcol[nd.ent_off + e];
-      if (lc >= c0 && lc < c0 + W) buf[s * W + (lc - c0)] = As[nd.ent_off + e];
-    }
-    if ((threadIdx.x & 15) == 0) rw[s] = rho[nd.row_off + lr];
-  }
-  __syncthreads();
-}
-
-}  // namespace
-
-__global__ __launch_bounds__(256) void k_factor(PlDev d, int N, int n, int m, int nnz, int ndx, int S_stride,
-                                                int nw_max, double sigma) {
-  const int b = blockIdx.x;
-  extern __shared__ double lds[];
-  double* big = lds;                          // nw_max^2 (S) or FCH * ncol chunk
-  double* C = big + nw_max * nw_max;          // ndx^2
-  double* rk = C + ndx * ndx;                 // 2 x 112
-  double* ck = rk + 2 * 112;                  // 2 x 112
-  double* rw = ck + 2 * 112;                  // FCH
-  __shared__ int rows_s[FCH];
-  const int ty = threadIdx.x / FG, tx = threadIdx.x % FG;
-  const double* As = d.As + (size_t)b * nnz;
-  const double* rho = d.rho + (size_t)b * m;
-  const double* Ps = d.Ps + (size_t)b * n;
-  double* Sg = d.S + (size_t)b * S_stride;
-  double* Kc = d.Kc + (size_t)b * ndx * nw_max;
-  double* Uc = d.Uc + (size_t)b * ndx * nw_max;
-
-  for (int i = 0; i <= N; ++i) {
-    const PlNode nd = d.nodes[i];
-    const int nw = nd.nw;
-    // ---- coupling block Kc = K_{i+1,i}[a][c] = sum_{coupling rows} rho a_{nw+a} a_c
-    if (i < N) {
-      const int W = nd.ncol;
-      for (int el = threadIdx.x; el < ndx * nw; el += blockDim.x) Kc[el] = 0.0;
-      for (int r0 = 0; r0 < nd.ncpl; r0 += FCH) {
-        const int nr = min(FCH, nd.ncpl - r0);
-        __syncthreads();
-        if (threadIdx.x < nr) rows_s[threadIdx.x] = d.cplrow[nd.cpl_off + r0 + threadIdx.x];
-        __syncthreads();
-        fill_chunk(d, As, rho, i, rows_s, nr, 0, W, big, rw);
-        for (int el = threadIdx.x; el < ndx * nw; el += blockDim.x) {
-          const int aa = el / nw, cc = el - aa * nw;
-          double acc = Kc[el];
-          for (int s = 0; s < nr; ++s) acc += rw[s] * big[s * W + nw + aa] * big[s * W + cc];
-          Kc[el] = acc;
-        }
-        __syncthreads();
-      }
-    }
-    double Kr[FB][FB];
-    // ---- diagonal, padding, Schur complement from node i-1
-#pragma unroll
-    for (int rr = 0; rr < FB; ++rr)
-#pragma unroll
-      for (int cc = 0; cc < FB; ++cc) {
-        const int gi = FB * ty + rr, gj = FB * tx + cc;
-        double v = 0.0;
-        if (gi == gj) v = (gi < nw) ? Ps[nd.x_off + gi] + sigma : 1.0;
-        if (i > 0 && gi < ndx && gj < ndx) v -= C[gi * ndx + gj];
-        Kr[rr][cc] = v;
-      }
-    __syncthreads();  // C consumed
-    // ---- rows of node i on the w_i columns
-    if (i < N) {
-      const int W = nd.ncol;
-      for (int r0 = 0; r0 < nd.nrow; r0 += FCH) {
-        const int nr = min(FCH, nd.nrow - r0);
-        if (threadIdx.x < nr) rows_s[threadIdx.x] = r0 + threadIdx.x;
-        __syncthreads();
-        fill_chunk(d, As, rho, i, rows_s, nr, 0, W, big, rw);
-        for (int s = 0; s < nr; ++s) {
-          const double* a = big + s * W;
-          const double w = rw[s];
-          double ar[FB], ac[FB];
-#pragma unroll
-          for (int k = 0; k < FB; ++k) {
-            const int gi = FB * ty + k, gj = FB * tx + k;
-            ar[k] = gi < nw ? w * a[gi] : 0.0;
-            ac[k] = gj < nw ? a[gj] : 0.0;
-          }
-#pragma unroll
-          for (int rr = 0; rr < FB; ++rr)
-#pragma unroll
-            for (int cc = 0; cc < FB; ++cc) Kr[rr][cc] += ar[rr] * ac[cc];
-        }
-        __syncthreads();
-      }
-    }
-    // ---- coupling rows of node i-1 on dx_i
-    if (i > 0) {
-      const PlNode pv = d.nodes[i - 1];
-      for (int r0 = 0; r0 < pv.ncpl; r0 += FCH) {
-        const int nr = min(FCH, pv.ncpl - r0);
-        if (threadIdx.x < nr) rows_s[threadIdx.x] = d.cplrow[pv.cpl_off + r0 + threadIdx.x];
-        __syncthreads();
-        fill_chunk(d, As, rho, i - 1, rows_s, nr, pv.nw, ndx, big, rw);
-        for (int s = 0; s < nr; ++s) {
-          const double* a = big + s * ndx;
-          const double w = rw[s];
-          double ar[FB], ac[FB];
-#pragma unroll
-          for (int k = 0; k < FB; ++k) {
-            const int gi = FB * ty + k, gj = FB * tx + k;
-            ar[k] = gi < ndx ? w * a[gi] : 0.0;
-            ac[k] = gj < ndx ? a[gj] : 0.0;
-          }
-#pragma unroll
-          for (int rr = 0; rr < FB; ++rr)
-#pragma unroll
-            for (int cc = 0; cc < FB; ++cc) Kr[rr][cc] += ar[rr] * ac[cc];
-        }
-        __syncthreads();
-      }
-    }
-    // ---- in-place Gauss-Jordan inversion (SPD, no pivoting)
-    for (int k = 0; k < nw; ++k) {
-      double* rkb = rk + (k & 1) * 112;
-      double* ckb = ck + (k & 1) * 112;
-      const int kb = k / FB, kr = k - kb * FB;
-      if (ty == kb) {
-#pragma unroll
-        for (int rr = 0; rr < FB; ++rr)
-          if (rr == kr)
-#pragma unroll
-            for (int cc = 0; cc < FB; ++cc) rkb[FB * tx + cc] = Kr[rr][cc];
-      }
-      if (tx == kb) {
-#pragma unroll
-        for (int cc = 0; cc < FB; ++cc)
-          if (cc == kr)
-#pragma unroll
-            for (int rr = 0; rr < FB; ++rr) ckb[FB * ty + rr] = Kr[rr][cc];
-      }
-      __syncthreads();
-      const double pinv = 1.0 / rkb[k];
-      double cv[FB], rv[FB];
-#pragma unroll
-      for (int q = 0; q < FB; ++q) {
-        cv[q] = ckb[FB * ty + q];
-        rv[q] = rkb[FB * tx + q];
-      }
-#pragma unroll
-      for (int rr = 0; rr < FB; ++rr)
-#pragma unroll
-        for (int cc = 0; cc < FB; ++cc) {
-          const int gi = FB * ty + rr, gj = FB * tx + cc;
-          double v = Kr[rr][cc];
-          if (gi == k && gj == k) v = pinv;
-          else if (gi == k) v = rv[cc] * pinv;
-          else if (gj == k) v = -cv[rr] * pinv;
-          else v = v - cv[rr] * (rv[cc] * pinv);
-          Kr[rr][cc] = v;
-        }
-    }
-    __syncthreads();
-    // ---- symmetrise: GJ without pivoting leaves S_i slightly non-symmetric
-    // (~eps * cond).  The sweeps read the lower triangle while the Schur
-    // complement of node i+1 uses the dense S_i, so both must see the same
-    // matrix or the block factorisation is inconsistent (the terminal node
-    // amplifies the mismatch by ~1e6).  (S + S^T) / 2 is also the more accurate.
-#pragma unroll
-    for (int rr = 0; rr < FB; ++rr)
-#pragma unroll
-      for (int cc = 0; cc < FB; ++cc) {
-        const int gi = FB * ty + rr, gj = FB * tx + cc;
-        if (gi < nw && gj < nw) big[gi * nw + gj] = Kr[rr][cc];
-      }
-    __syncthreads();
-#pragma unroll
-    for (int rr = 0; rr < FB; ++rr)
-#pragma unroll
-      for (int cc = 0; cc < FB; ++cc) {
-        const int gi = FB * ty + rr, gj = FB * tx + cc;
-        if (gi < nw && gj < nw) Kr[rr][cc] = 0.5 * (Kr[rr][cc] + big[gj * nw + gi]);
-      }
-    __syncthreads();
-    // ---- store S_i: tiled global layout + dense copy in LDS (stride nw)
-    {
-      const int nunit = nd.nunit;
-      double* Sn = Sg + nd.s_off;
-#pragma unroll
-      for (int rr = 0; rr < FB; ++rr)
-#pragma unroll
-        for (int cc = 0; cc < FB; ++cc) {
-          const int gi = FB * ty + rr, gj = FB * tx + cc;
-          const int I = gi >> 3, J = gj >> 3;
-          if (I < nd.ntile && J <= I) {
-            const double v = (gi < nw && gj < nw) ? Kr[rr][cc] : 0.0;
-            const int t = I * (I + 1) / 2 + J;
-            const int h = (gj & 7) >> 2;
-            const int u = 2 * t + h;
-            const int pos = (gi & 7) * 4 + (gj & 3);
-            Sn[((pos >> 1) * nunit + u) * 2 + (pos & 1)] = v;
-          }
-          if (gi < nw && gj < nw) big[gi * nw + gj] = Kr[rr][cc];
-        }
-    }
-    __syncthreads();
-    if (i == N) break;
-    // ---- U = Kc S (ndx x nw), then C = U Kc^T (ndx x ndx)
-    for (int el = threadIdx.x; el < ndx * nw; el += blockDim.x) {
-      const int aa = el / nw, cc = el - aa * nw;
-      const double* kr = Kc + aa * nw;
-      double acc = 0.0;
-      for (int k = 0; k < nw; ++k) acc += kr[k] * big[k * nw + cc];
-      Uc[el] = acc;
-    }
-    __syncthreads();
-    for (int el = threadIdx.x; el < ndx * ndx; el += blockDim.x) {
-      const int aa = el / ndx, bb = el - aa * ndx;
-      const double* ur = Uc + aa * nw;
-      const double* kr = Kc + bb * nw;
-      double acc = 0.0;
-      for (int k = 0; k < nw; ++k) acc += ur[k] * kr[k];
-      C[el] = acc;
-    }
-    __syncthreads();
-  }
-}
-
-void launch_factor(PlOcpHandle* h) {
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)k_factor, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
-    attr = true;
-  }
-  const size_t lds = sizeof(double) * ((size_t)h->nw_max * h->nw_max + (size_t)h->ndx * h->ndx + 4 * 112 + FCH);
-  hipLaunchKernelGGL(k_factor, dim3(h->B), dim3(256), lds, h->stream, h->d, h->N, h->n, h->m, h->nnz, h->ndx,
-                     h->S_stride, h->nw_max, h->set.sigma);
-}
-
 // rhs = sigma x - q + A^T (rho z - y)   (before the first iteration of a solve)
 __global__ __launch_bounds__(256) void k_admm_init(PlDev d, int N, int n, int m, int nnz, double sigma) {
   const int b = blockIdx.x;

@@ -53,7 +53,7 @@ struct PlAdmmNode {
   int prog, prog_len;
   int rowptr, rowp, colptr, colr, cplr, cwptr, cwp, cxptr, cxp, ccptr, ccp, xcptr, xcp;
   int rchn, rch, rchptr, cchn, cch, cchptr;
-  int pad[1];
+  int flen;        // u16 words of the prefix [rowptr, cplr, rowp] the factor kernel stages
 };
 
 struct PlSettings {
@@ -122,9 +122,6 @@ struct PlDev {
   double* aty;       // A^T y scratch (check iterations)
   double* step;      // unscaled QP step dx
   double* S;         // factor blocks (tiled)
-  double* Kc;        // coupling scratch (ndx x nw_max) per problem
-  double* Uc;        // U = Kc S scratch
-  double* Cs;        // Schur complement carried to the next node (ndx x ndx)
   double* work;      // generic reductions scratch
   PlProbInfo* info;
   // MPC (device loop)
@@ -141,6 +138,7 @@ struct PlOcpHandle {
   int nunit_max;
   int ncpl_max, nent_max;
   int chunk_max;                    // max(rchn, cchn) over nodes (ADMM partial-sum buffer)
+  int flen_max;                     // longest factor program prefix (u16)
   int admm_dom_prog, admm_dom_len;  // most frequent ADMM gather program (kept in LDS)
   int admm_asr;                     // A values per thread staged through registers
   PlSettings set;

@@ -27,7 +27,8 @@ bo.init_solver()
 t = time.time()
 st = bo.solve(timed=True)
 print("solve s", time.time() - t, "phase_ms", st["phase_ms"], "iters", np.bincount(st["admm_iters"]).nonzero())
-T = bo.debug("admm_t", B * 16).reshape(B, 16)
+ALL = bo.debug("admm_t", B * 32)
+T = ALL[:B * 16].reshape(B, 16)
 it = st["admm_iters"].astype(float)
 steps = it * (N + 1)  # per direction
 names = ["f:bar0", "f:stageA", "f:gather+bar", "f:mv+bar", "f:issue", "f:reduce", "-", "-",
@@ -38,3 +39,8 @@ for k, nm in enumerate(names):
         print(f"{nm:14s} mean cycles/step {per[:, k].mean():9.1f}  p10 {np.percentile(per[:, k], 10):9.1f}  "
               f"p90 {np.percentile(per[:, k], 90):9.1f}")
 print("total cycles/step fwd", per[:, :6].sum(1).mean(), "bwd", per[:, 8:].sum(1).mean())
+F = ALL[B * 16:].reshape(B, 16)[:, :9] / (N + 1)
+fn = ["stage", "Kc+D", "init", "assemble", "GJ", "symm", "store", "U", "C"]
+for k, nm in enumerate(fn):
+    print(f"factor {nm:10s} mean cycles/node {F[:, k].mean():10.1f}")
+print("factor total cycles/node", F.sum(1).mean())
