@@ -117,73 +117,120 @@ __device__ void for_row_entries(const PlDev& d, int r, F fn) {
 
 // ---------------------------------------------------------------------------
 // OSQP data update + Ruiz equilibration (osqp_update_lin_cost / _bounds / _A and
-// scale_data, OSQP 0.6 src/scaling.c), one workgroup per problem.
-__global__ __launch_bounds__(256) void k_qp_setup(PlDev d, int N, int n, int m, int nnz, int ncpl_max, PlSettings st) {
+// scale_data, OSQP 0.6 src/scaling.c).  D, E and the cost scale c are kept
+// cumulatively against the raw data, so each pass needs
+//   Dt_j = max(c D_j^2 |P_jj|, D_j max_r |A_rj| E_r),   Et_r = E_r max_j |A_rj| D_j.
+// The norms of a pass run over a (problem x node) grid: the workgroup of node i
+// owns its columns w_i (entries of node i plus node i-1's entries on dx_i) and
+// its rows; the update of D, E and c is one workgroup per problem.
+__global__ __launch_bounds__(256) void k_ruiz_init(PlDev d, int n, int m) {
+  const int b = blockIdx.x;
+  double* D = d.D + (size_t)b * n;
+  double* E = d.E + (size_t)b * m;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) D[j] = 1.0;
+  for (int r = threadIdx.x; r < m; r += blockDim.x) E[r] = 1.0;
+  if (threadIdx.x == 0) d.cs[b] = 1.0;
+}
+
+__global__ __launch_bounds__(256) void k_ruiz_norms(PlDev d, int N, int n, int m, int nnz) {
+  const int b = blockIdx.x / (N + 1), i = blockIdx.x - b * (N + 1);
+  const PlNode nd = d.nodes[i];
+  const double* A = d.Araw + (size_t)b * nnz;
+  const double* P = d.P + (size_t)b * n;
+  const double* D = d.D + (size_t)b * n;
+  const double* E = d.E + (size_t)b * m;
+  double* Dt = d.dxs + (size_t)b * n;  // scratch
+  double* Et = d.dys + (size_t)b * m;  // scratch
+  const double c = d.cs[b];
+  for (int lc = threadIdx.x; lc < nd.nw; lc += blockDim.x) {
+    double mx = 0.0;
+    if (i < N) {
+      const int* cp = d.colptr + nd.colptr_off;
+      for (int e = cp[lc]; e < cp[lc + 1]; ++e)
+        mx = fmax(mx, fabs(A[nd.ent_off + e]) * E[nd.row_off + d.rowidx[nd.ent_off + e]]);
+    }
+    if (i > 0 && lc < d.oc->ndx) {
+      const PlNode pv = d.nodes[i - 1];
+      const int* cp = d.colptr + pv.colptr_off;
+      for (int e = cp[pv.nw + lc]; e < cp[pv.nw + lc + 1]; ++e)
+        mx = fmax(mx, fabs(A[pv.ent_off + e]) * E[pv.row_off + d.rowidx[pv.ent_off + e]]);
+    }
+    const int j = nd.x_off + lc;
+    const double dj = D[j];
+    Dt[j] = fmax(c * dj * dj * fabs(P[j]), dj * mx);
+  }
+  if (i < N) {
+    const PlNode nn = d.nodes[i + 1];
+    const int* rp = d.rowptr + nd.rowptr_off;
+    const int* re = d.rowent + nd.csr_off;
+    for (int lr = threadIdx.x; lr < nd.nrow; lr += blockDim.x) {
+      double mx = 0.0;
+      for (int q = rp[lr]; q < rp[lr + 1]; ++q) {
+        const int e = re[q];
+        const int lc = d.entcol[nd.ent_off + e];
+        const int j = lc < nd.nw ? nd.x_off + lc : nn.x_off + (lc - nd.nw);
+        mx = fmax(mx, fabs(A[nd.ent_off + e]) * D[j]);
+      }
+      const int r = nd.row_off + lr;
+      Et[r] = E[r] * mx;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ruiz_update(PlDev d, int n, int m) {
   const int b = blockIdx.x;
   __shared__ double red[256];
-  __shared__ double s_c;
-  const double* A = d.Araw + (size_t)b * nnz;
   const double* P = d.P + (size_t)b * n;
   const double* q = d.grad + (size_t)b * n;
   double* D = d.D + (size_t)b * n;
   double* E = d.E + (size_t)b * m;
-  double* Dt = d.dxs + (size_t)b * n;  // scratch
-  double* Et = d.dys + (size_t)b * m;  // scratch
-  for (int j = threadIdx.x; j < n; j += blockDim.x) D[j] = 1.0;
-  for (int r = threadIdx.x; r < m; r += blockDim.x) E[r] = 1.0;
-  if (threadIdx.x == 0) s_c = 1.0;
-  __syncthreads();
-  for (int pass = 0; pass < st.scaling; ++pass) {
-    const double c = s_c;
-    // inf-norms of the columns of [P; A] and of the rows of A (scaled data)
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-      double mx = 0.0;
-      for_col_entries(d, N, j, [&](int e, int r) { mx = fmax(mx, fabs(A[e]) * E[r]); });
-      double dj = D[j];
-      Dt[j] = fmax(c * dj * dj * fabs(P[j]), dj * mx);
-    }
-    for (int r = threadIdx.x; r < m; r += blockDim.x) {
-      double mx = 0.0;
-      for_row_entries(d, r, [&](int e, int j) { mx = fmax(mx, fabs(A[e]) * D[j]); });
-      Et[r] = E[r] * mx;
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j < n; j += blockDim.x) D[j] *= 1.0 / sqrt(limit_scaling(Dt[j]));
-    for (int r = threadIdx.x; r < m; r += blockDim.x) E[r] *= 1.0 / sqrt(limit_scaling(Et[r]));
-    __syncthreads();
-    // cost normalisation: c_temp = max(mean |P_jj|, ||q||_inf) on the scaled data
-    double sum = 0.0, qmax = 0.0;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-      double dj = D[j];
-      sum += c * dj * dj * fabs(P[j]);
-      qmax = fmax(qmax, fabs(c * dj * q[j]));
-    }
-    sum = block_sum(sum, red);
-    qmax = block_max(qmax, red);
-    if (threadIdx.x == 0) {
-      double ct = fmax(sum / (double)n, limit_scaling(qmax));
-      ct = limit_scaling(ct);
-      s_c = c * (1.0 / ct);
-    }
-    __syncthreads();
+  const double* Dt = d.dxs + (size_t)b * n;
+  const double* Et = d.dys + (size_t)b * m;
+  const double c = d.cs[b];
+  double sum = 0.0, qmax = 0.0;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const double dj = D[j] * (1.0 / sqrt(limit_scaling(Dt[j])));
+    D[j] = dj;
+    sum += c * dj * dj * fabs(P[j]);
+    qmax = fmax(qmax, fabs(c * dj * q[j]));
   }
-  const double c = s_c;
-  if (threadIdx.x == 0) d.cs[b] = c;
-  // scaled problem data
-  double* As = d.As + (size_t)b * nnz;
-  for (int i = 0; i < N; ++i) {
-    const PlNode nd = d.nodes[i];
-    for (int e = threadIdx.x; e < nd.nent; e += blockDim.x) {
-      const int r = nd.row_off + d.rowidx[nd.ent_off + e];
-      const int j = gcol(d.nodes, i, d.entcol[nd.ent_off + e]);
-      As[nd.ent_off + e] = E[r] * A[nd.ent_off + e] * D[j];
-    }
+  for (int r = threadIdx.x; r < m; r += blockDim.x) E[r] *= 1.0 / sqrt(limit_scaling(Et[r]));
+  // cost normalisation: c_temp = max(mean |P_jj|, ||q||_inf) on the scaled data
+  sum = block_sum(sum, red);
+  qmax = block_max(qmax, red);
+  if (threadIdx.x == 0) {
+    double ct = fmax(sum / (double)n, limit_scaling(qmax));
+    ct = limit_scaling(ct);
+    d.cs[b] = c * (1.0 / ct);
   }
+}
+
+// Scaled problem data of node i: As, qs, Ps (columns), ls, us, rho (rows), and
+// rho of the coupling rows for the ADMM prefetch.
+__global__ __launch_bounds__(256) void k_qp_finish(PlDev d, int N, int n, int m, int nnz, int ncpl_max, PlSettings st) {
+  const int b = blockIdx.x / (N + 1), i = blockIdx.x - b * (N + 1);
+  const PlNode nd = d.nodes[i];
+  const double* A = d.Araw + (size_t)b * nnz;
+  const double* P = d.P + (size_t)b * n;
+  const double* q = d.grad + (size_t)b * n;
+  const double* D = d.D + (size_t)b * n;
+  const double* E = d.E + (size_t)b * m;
+  const double c = d.cs[b];
   double* qs = d.qs + (size_t)b * n;
   double* Ps = d.Ps + (size_t)b * n;
-  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+  for (int lc = threadIdx.x; lc < nd.nw; lc += blockDim.x) {
+    const int j = nd.x_off + lc;
     qs[j] = c * D[j] * q[j];
     Ps[j] = c * D[j] * D[j] * P[j];
+  }
+  if (i == N) return;
+  const PlNode nn = d.nodes[i + 1];
+  double* As = d.As + (size_t)b * nnz;
+  for (int e = threadIdx.x; e < nd.nent; e += blockDim.x) {
+    const int r = nd.row_off + d.rowidx[nd.ent_off + e];
+    const int lc = d.entcol[nd.ent_off + e];
+    const int j = lc < nd.nw ? nd.x_off + lc : nn.x_off + (lc - nd.nw);
+    As[nd.ent_off + e] = E[r] * A[nd.ent_off + e] * D[j];
   }
   const double* g = d.g + (size_t)b * m;
   const double* lbg = d.lbg + (size_t)b * m;
@@ -191,7 +238,9 @@ __global__ __launch_bounds__(256) void k_qp_setup(PlDev d, int N, int n, int m, 
   double* ls = d.ls + (size_t)b * m;
   double* us = d.us + (size_t)b * m;
   double* rho = d.rho + (size_t)b * m;
-  for (int r = threadIdx.x; r < m; r += blockDim.x) {
+  __shared__ double rho_s[256];
+  for (int lr = threadIdx.x; lr < nd.nrow; lr += blockDim.x) {
+    const int r = nd.row_off + lr;
     double l = fmax(lbg[r] - g[r], -PL_OSQP_INFTY);
     double u = fmin(ubg[r] - g[r], PL_OSQP_INFTY);
     double lsr = E[r] * l, usr = E[r] * u;
@@ -202,19 +251,25 @@ __global__ __launch_bounds__(256) void k_qp_setup(PlDev d, int N, int n, int m, 
     else if (usr - lsr < PL_RHO_TOL) rr = PL_RHO_EQ_OVER_INEQ * st.rho;
     else rr = st.rho;
     rho[r] = rr;
+    if (lr < 256) rho_s[lr] = rr;
   }
   __syncthreads();
-  // rho of each node's coupling rows, contiguous for the ADMM prefetch
-  double* rhoc = d.rhoc + (size_t)b * (N + 1) * ncpl_max;
-  for (int i = 0; i < N; ++i) {
-    const PlNode& nd = d.nodes[i];
-    for (int s = threadIdx.x; s < nd.ncpl; s += blockDim.x)
-      rhoc[i * ncpl_max + s] = rho[nd.row_off + d.cplrow[nd.cpl_off + s]];
+  // rho of the node's coupling rows, contiguous for the ADMM prefetch
+  double* rhoc = d.rhoc + (size_t)b * (N + 1) * ncpl_max + (size_t)i * ncpl_max;
+  for (int s = threadIdx.x; s < nd.ncpl; s += blockDim.x) {
+    const int lr = d.cplrow[nd.cpl_off + s];
+    rhoc[s] = lr < 256 ? rho_s[lr] : rho[nd.row_off + lr];
   }
 }
 
 void launch_qp_setup(PlOcpHandle* h) {
-  hipLaunchKernelGGL(k_qp_setup, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz,
+  const dim3 nodes_grid(h->B * (h->N + 1));
+  hipLaunchKernelGGL(k_ruiz_init, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, h->m);
+  for (int pass = 0; pass < h->set.scaling; ++pass) {
+    hipLaunchKernelGGL(k_ruiz_norms, nodes_grid, dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz);
+    hipLaunchKernelGGL(k_ruiz_update, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, h->m);
+  }
+  hipLaunchKernelGGL(k_qp_finish, nodes_grid, dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz,
                      std::max(h->ncpl_max, 1), h->set);
 }
 
