@@ -36,11 +36,14 @@ METRIC = "MPC solves/sec (B2G whole_body_rnea N=50) at batch; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 
 
-def admm_bytes_per_problem_iter(sz):
+def admm_bytes_per_problem_iter(sz, node_table):
     """Algorithmic HBM bytes of one ADMM iteration of one problem (roofline):
-    both sweeps read the factor once (2 * S), A is read once, and the vectors
+    the two sweeps read every factor block S_i once each, except S_0 and S_N which the
+    fused turnaround steps read once per iteration; A is read once, and the vectors
     x, rhs, bt, q (7n) and z, y, l, u, rho (7m) are read / written once."""
-    return 8.0 * (2 * sz["S_stride"] + sz["nnz"] + 7 * sz["n"] + 7 * sz["m"])
+    blk = node_table[:, 9].astype(float) * 64 * 16  # doubles per factor block (K slots x 64 lanes x 16)
+    s_once = blk[0] + blk[-1]
+    return 8.0 * (2 * sz["S_stride"] - s_once + sz["nnz"] + 7 * sz["n"] + 7 * sz["m"])
 
 
 def cpu_baseline(R, dynamics, N, n_problems=2, n_steps=2):
@@ -133,7 +136,7 @@ def main():
         assert allp.shape[0] == B * world
 
     sz = bo.sizes()
-    bytes_it = admm_bytes_per_problem_iter(sz)
+    bytes_it = admm_bytes_per_problem_iter(sz, bo.node_table())
     per_launch_bytes = bytes_it * prof["problem_iters"] / max(1, prof["launches"])
     avg_launch_s = prof["admm_ms"] / max(1, prof["launches"]) / 1e3
     achieved = per_launch_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0

@@ -41,7 +41,7 @@ struct pl_ocp {
   std::vector<PlNode> nodes;
   std::vector<int> colptr, rowidx, entcol, rowptr, rowent, cplrow, rownode, colnode;
   std::vector<PlAdmmNode> anodes;
-  std::vector<uint16_t> aprog;
+  std::vector<uint16_t> aprog, fprog;
   std::vector<double> h_params;  // host copy of the parameters (B x np)
   std::vector<void*> allocs;
   hipEvent_t ev[5];
@@ -282,6 +282,7 @@ int build_layout(pl_ocp* o) {
   h.ncol_max = 0;
   h.nrow_max = 0;
   h.nunit_max = 0;
+  h.ntile_max = 0;
   for (int i = 0; i <= N; ++i) {
     PlNode& nd = o->nodes[i];
     memset(&nd, 0, sizeof(nd));
@@ -329,10 +330,11 @@ int build_layout(pl_ocp* o) {
       o->rowptr.push_back(s);
       nd.ncpl = (int)o->cplrow.size() - nd.cpl_off;
     }
-    nd.ntile = (nd.nw + 7) / 8;
-    nd.nunit = nd.ntile * (nd.ntile + 1);
+    // factor block: lower triangle in 4x4 tiles, K tile slots per lane of a wave
+    nd.ntile = (nd.nw + 3) / 4;
+    nd.nunit = (nd.ntile * (nd.ntile + 1) / 2 + 63) / 64;
     nd.s_off = s_off;
-    s_off += nd.nunit * 32;
+    s_off += nd.nunit * 64 * 16;
     x_off += nd.nw;
     row_off += nd.nrow;
     ent_off += nd.nent;
@@ -340,6 +342,7 @@ int build_layout(pl_ocp* o) {
     h.ncol_max = std::max(h.ncol_max, nd.ncol);
     h.nrow_max = std::max(h.nrow_max, nd.nrow);
     h.nunit_max = std::max(h.nunit_max, nd.nunit);
+    h.ntile_max = std::max(h.ntile_max, nd.ntile);
   }
   h.n = x_off;
   h.m = row_off;
@@ -359,27 +362,46 @@ int build_layout(pl_ocp* o) {
   return 0;
 }
 
-// Gather programs of the ADMM sweeps (PlAdmmNode, state.h), one per distinct
-// local structure.
+// Node programs of the factor and ADMM kernels (PlAdmmNode, state.h), one per
+// distinct local structure.
 int build_admm_prog(pl_ocp* o) {
   PlOcpHandle& h = o->h;
   const int N = h.oc.N, ndx = h.oc.ndx;
   o->anodes.assign(N + 1, PlAdmmNode());
   o->aprog.clear();
-  std::vector<std::vector<uint16_t>> progs;
-  std::vector<int> prog_off, prog_count;
+  o->fprog.clear();
+  std::vector<std::vector<uint16_t>> aprogs, fprogs;
+  std::vector<int> aoff, foff;
   h.ncpl_max = 0;
   h.nent_max = 0;
   h.chunk_max = 1;
   h.flen_max = 2;
+  h.admm_fwd_asb = 0;
+  auto intern = [](std::vector<std::vector<uint16_t>>& progs, std::vector<int>& off, std::vector<uint16_t>& all,
+                   std::vector<uint16_t>& P) {
+    while (P.size() % 4) P.push_back(0);  // 8-byte aligned programs
+    for (size_t k = 0; k < progs.size(); ++k)
+      if (progs[k] == P) return off[k];
+    progs.push_back(P);
+    off.push_back((int)all.size());
+    all.insert(all.end(), P.begin(), P.end());
+    return off.back();
+  };
   for (int i = 0; i <= N; ++i) {
     const PlNode& nd = o->nodes[i];
     PlAdmmNode& a = o->anodes[i];
     memset(&a, 0, sizeof(a));
     a.nw = nd.nw; a.nrow = nd.nrow; a.ncol = nd.ncol; a.ncpl = nd.ncpl; a.nent = nd.nent;
-    a.nunit = nd.nunit; a.ntile = nd.ntile; a.x_off = nd.x_off; a.row_off = nd.row_off;
-    a.ent_off = nd.ent_off; a.s_off = nd.s_off;
+    a.nunit = nd.nunit; a.ntile = nd.ntile; a.ntl = nd.ntile * (nd.ntile + 1) / 2;
+    a.kmagic = (unsigned)((0x100000000ull + nd.nunit - 1) / nd.nunit);
+    a.x_off = nd.x_off; a.row_off = nd.row_off; a.ent_off = nd.ent_off; a.s_off = nd.s_off;
     if (nd.nent > 65535 || nd.ncol > 65535) { pl_set_error("node too large for u16 programs"); return -1; }
+    const int* cp = o->colptr.data() + nd.colptr_off;
+    const int* rp = o->rowptr.data() + nd.rowptr_off;
+    const int* re = o->rowent.data() + nd.csr_off;
+    const int* rid = o->rowidx.data() + nd.ent_off;
+    const int* ecol = o->entcol.data() + nd.ent_off;
+    const int* cpl = o->cplrow.data() + nd.cpl_off;
     std::vector<uint16_t> P;
     auto mark = [&](int& field) { field = (int)P.size(); };
     auto mark2 = [&](int& field) {  // pair lists start on a 32-bit boundary
@@ -390,27 +412,33 @@ int build_admm_prog(pl_ocp* o) {
       P.push_back((uint16_t)e);
       P.push_back((uint16_t)c);
     };
-    const int* cp = o->colptr.data() + nd.colptr_off;
-    const int* rp = o->rowptr.data() + nd.rowptr_off;
-    const int* re = o->rowent.data() + nd.csr_off;
-    const int* rid = o->rowidx.data() + nd.ent_off;
-    const int* ecol = o->entcol.data() + nd.ent_off;
-    const int* cpl = o->cplrow.data() + nd.cpl_off;
+    // ---- factor program: rowptr, cplr, rowp
+    mark(a.f_rowptr);
+    for (int r = 0; r <= nd.nrow; ++r) P.push_back((uint16_t)(nd.nrow ? rp[r] : 0));
+    mark(a.f_cplr);
+    for (int s = 0; s < nd.ncpl; ++s) P.push_back((uint16_t)cpl[s]);
+    mark2(a.f_rowp);
+    for (int q = 0; nd.nrow && q < rp[nd.nrow]; ++q) pair(re[q], ecol[re[q]]);
+    a.fprog = intern(fprogs, foff, o->fprog, P);
+    a.flen = (int)P.size();
+    h.flen_max = std::max(h.flen_max, a.flen);
+    // ---- ADMM program
+    P.clear();
     std::vector<int> cpl_index(nd.nrow, -1);
     for (int s = 0; s < nd.ncpl; ++s) cpl_index[cpl[s]] = s;
-    // prefix used by the factor kernel: rowptr, cplr, rowp (flen u16 words)
-    mark(a.rowptr);
-    for (int r = 0; r <= nd.nrow; ++r) P.push_back((uint16_t)(nd.nrow ? rp[r] : 0));
-    mark(a.cplr);
-    for (int s = 0; s < nd.ncpl; ++s) P.push_back((uint16_t)cpl[s]);
-    mark2(a.rowp);
-    for (int q = 0; nd.nrow && q < rp[nd.nrow]; ++q) pair(re[q], ecol[re[q]]);
-    if (P.size() & 1) P.push_back(0);
-    a.flen = (int)P.size();
-    mark(a.colptr);
-    for (int c = 0; c <= nd.ncol; ++c) P.push_back((uint16_t)(nd.ncol ? cp[c] : 0));
-    mark(a.colr);
-    for (int e = 0; e < nd.nent; ++e) P.push_back((uint16_t)rid[e]);
+    // rows: entry (u16) and local column (u8) of every CSR slot; cols: local row (u8)
+    // of every entry.  u8 lists are packed two per u16 word.
+    if (nd.ncol > 255 || nd.nrow > 255) { pl_set_error("node with > 255 local rows / columns"); return -1; }
+    auto bytes = [&](int& field, int count, auto get) {
+      field = (int)P.size();
+      for (int k = 0; k < count; k += 2)
+        P.push_back((uint16_t)(get(k) | ((k + 1 < count ? get(k + 1) : 0) << 8)));
+    };
+    const int nq = nd.nrow ? rp[nd.nrow] : 0;
+    mark(a.rowe);
+    for (int q = 0; q < nq; ++q) P.push_back((uint16_t)re[q]);
+    bytes(a.rowc, nq, [&](int q) { return ecol[re[q]]; });
+    bytes(a.colr, nd.nent, [&](int e) { return rid[e]; });
     // coupling rows split into their w part and their dx_{i+1} part
     std::vector<int> cwp{0}, cxp{0};
     std::vector<std::pair<int, int>> cw, cx;
@@ -423,6 +451,7 @@ int build_admm_prog(pl_ocp* o) {
       }
       cwp.push_back((int)cw.size());
       cxp.push_back((int)cx.size());
+      if (cwp[s + 1] - cwp[s] > PL_ADMM_CWM) h.admm_fwd_asb = 1;
     }
     mark(a.cwptr);
     for (int x : cwp) P.push_back((uint16_t)x);
@@ -446,6 +475,7 @@ int build_admm_prog(pl_ocp* o) {
         xc.push_back({e, cpl_index[rid[e]]});
       }
       xcp.push_back((int)xc.size());
+      if (xcp[c + 1] - xcp[c] > PL_ADMM_XCM) h.admm_fwd_asb = 1;
     }
     mark(a.ccptr);
     for (int x : ccp) P.push_back((uint16_t)x);
@@ -481,42 +511,41 @@ int build_admm_prog(pl_ocp* o) {
       for (int x : ptr) P.push_back((uint16_t)x);
       h.chunk_max = std::max(h.chunk_max, std::max(a.rchn, a.cchn));
     }
-    h.flen_max = std::max(h.flen_max, a.flen);
-    while (P.size() % 8) P.push_back(0);
-    int found = -1;
-    for (size_t k = 0; k < progs.size(); ++k)
-      if (progs[k] == P) { found = (int)k; break; }
-    if (found < 0) {
-      found = (int)progs.size();
-      progs.push_back(P);
-      prog_off.push_back((int)o->aprog.size());
-      o->aprog.insert(o->aprog.end(), P.begin(), P.end());
-    }
-    a.prog = prog_off[found];
-    a.prog_len = (int)progs[found].size();
-    if ((int)prog_count.size() <= found) prog_count.resize(found + 1, 0);
-    prog_count[found]++;
+    a.prog = intern(aprogs, aoff, o->aprog, P);
+    a.prog_len = (int)P.size();
     h.ncpl_max = std::max(h.ncpl_max, nd.ncpl);
     h.nent_max = std::max(h.nent_max, nd.nent);
   }
-  // the most frequent node program is kept in LDS by the ADMM kernel
-  int dom = 0;
-  for (size_t k = 0; k < prog_count.size(); ++k)
-    if (prog_count[k] > prog_count[dom]) dom = (int)k;
-  h.admm_dom_prog = prog_off[dom];
-  h.admm_dom_len = 0;  // LDS program buffer: the longest program
-  for (const auto& pr : progs) h.admm_dom_len = std::max(h.admm_dom_len, (int)pr.size());
-  int dom_nent = 0;
-  for (int i = 0; i <= N; ++i)
-    if (o->anodes[i].prog == h.admm_dom_prog) dom_nent = std::max(dom_nent, o->anodes[i].nent);
-  h.admm_asr = std::max(4, (dom_nent + 255) / 256);
-  if (h.admm_asr > 8) h.admm_asr = 8;
+  h.aprog_len = (int)o->aprog.size();
+  {  // A values staged through registers: enough for the most frequent node program
+    std::vector<int> cnt;
+    std::vector<int> nmax;
+    std::vector<int> keys;
+    for (int i = 0; i <= N; ++i) {
+      const int key = o->anodes[i].prog;
+      size_t k = 0;
+      while (k < keys.size() && keys[k] != key) ++k;
+      if (k == keys.size()) { keys.push_back(key); cnt.push_back(0); nmax.push_back(0); }
+      cnt[k]++;
+      nmax[k] = std::max(nmax[k], o->anodes[i].nent);
+    }
+    size_t dom = 0;
+    for (size_t k = 0; k < keys.size(); ++k)
+      if (cnt[k] > cnt[dom]) dom = k;
+    h.admm_asr = nmax[dom] <= 16 * 64 ? 16 : PL_ADMM_ASR_MAX;
+  }
   if (ndx > 48) {
     pl_set_error("state dimension 2 nv = %d > 48 is not supported by the factor kernel", ndx);
     return -1;
   }
-  if (h.nrow_max > 256 || h.nw_max > 256) {
-    pl_set_error("ADMM kernel needs <= 256 rows and columns per node (rows %d)", h.nrow_max);
+  if (h.nrow_max > 64 * PL_ADMM_MR || h.nw_max > 64 * PL_ADMM_MV || h.ncpl_max > 64) {
+    pl_set_error("ADMM kernel needs <= %d rows, <= %d columns and <= 64 coupling rows per node", 64 * PL_ADMM_MR,
+                 64 * PL_ADMM_MV);
+    return -1;
+  }
+  const PlNode& last = o->nodes[N];
+  if (last.nrow != 0 || last.nw != ndx) {
+    pl_set_error("terminal node must own exactly dx_N and no rows");
     return -1;
   }
   return 0;
@@ -668,6 +697,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= upload(o, &D.colnode, o->colnode);
   rc |= upload(o, &D.anodes, o->anodes);
   rc |= upload(o, &D.aprog, o->aprog);
+  rc |= upload(o, &D.fprog, o->fprog);
   const size_t n = h.n, m = h.m, nnz = h.nnz;
   rc |= dalloc(o, &D.p, B * h.np);
   rc |= dalloc(o, &D.x, B * n);
@@ -1006,13 +1036,14 @@ extern "C" int pl_ocp_profile_read(pl_ocp* o, double* out) {
 }
 
 int admm_lds_bytes(const PlOcpHandle* h);
+int admm_ppw(const PlOcpHandle* h);
 
-// Sizes: [n, m, nnz, S_stride (doubles), nw_max, N, ADMM program length (u16),
-// LDS-resident program length, ADMM LDS bytes per workgroup, A values per thread].
+// Sizes: [n, m, nnz, S_stride (doubles), nw_max, N, ADMM programs (u16, LDS-resident),
+// problems per ADMM workgroup, ADMM LDS bytes per workgroup, A values per lane / 64].
 extern "C" int pl_ocp_sizes(const pl_ocp* o, long long* out) {
   if (!o) { pl_set_error("null handle"); return -1; }
   out[0] = o->h.n; out[1] = o->h.m; out[2] = o->h.nnz; out[3] = o->h.S_stride; out[4] = o->h.nw_max; out[5] = o->h.N;
-  out[6] = (long long)o->aprog.size(); out[7] = o->h.admm_dom_len; out[8] = admm_lds_bytes(&o->h); out[9] = o->h.admm_asr;
+  out[6] = (long long)o->aprog.size(); out[7] = admm_ppw(&o->h); out[8] = admm_lds_bytes(&o->h); out[9] = o->h.admm_asr;
   return 0;
 }
 

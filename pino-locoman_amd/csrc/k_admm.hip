@@ -1,5 +1,5 @@
 // ADMM sweeps (OSQP 0.6 osqp_solve loop body, src/osqp.c: update_xz_tilde,
-// update_x, update_z, update_y), one 256-thread workgroup per problem.
+// update_x, update_z, update_y) -- ONE WAVE PER PROBLEM.
 //
 // Per iteration the reduced KKT system K x~ = rhs is solved with the block
 // factor of k_factor (S_i = explicit inverse of the Schur-complemented block):
@@ -10,22 +10,33 @@
 // the iteration for the rows / columns of node i: z~ = A x~, relaxed z and y
 // updates, x update, and the next iteration's rhs = sigma x - q + A^T (rho z - y).
 //
-// The kernel is a stream over the schedule p = 0 .. 2 (N+1) niter - 1 (forward
-// nodes 0..N, then backward N..0, repeated).  It is HBM-bound on the factor
-// blocks, so it is written as a software pipeline:
-//   * S of step p+1 is loaded into registers right after the mat-vec of step p
-//     (one (tile, half) unit = 16 double2 per thread), so its latency hides
-//     behind the rest of step p and the gather phases of step p+1;
-//   * the small operands of step p+1 (A values of the node the step gathers
-//     from, rhs / bt, x, q, z, y, rho, l, u) are loaded into one of two register
-//     sets just before, so the in-order vmcnt wait for them at the start of step
-//     p+1 never waits for the S stream;
-//   * the A values are staged into LDS at the start of the step, and the gather
-//     program (u16 lists, PlAdmmNode) of the current node type is staged in LDS
-//     when the type changes (a few times per sweep); node-table fields are
-//     uniform scalar loads.  So no structure read waits on vmcnt.
-// All reductions are in a fixed order: results are bit-identical for a problem
-// regardless of the batch it runs in.
+// Schedule of one launch (every step consumes exactly one factor block S_i):
+//     F0 | { FWD 1..N-1, TN, BWD N-1..1, T0 } x niter   (the last T0 is B0)
+// TN fuses forward N and backward N (x~_N = w_N, so S_N is read once); T0 fuses
+// backward 0 with the next iteration's forward 0 (S_0 stays in registers).  Per
+// iteration 2N factor blocks are streamed instead of 2(N+1).
+//
+// MI355X mapping.  The kernel is HBM-bound on the factor stream (4.5 MB per
+// problem-iteration for B2G whole_body_rnea N=50), so the design goal is to keep
+// the whole batch resident with one factor block per problem in flight:
+//   * one 64-lane wave per problem, PPW problems per workgroup: 1024 problems =
+//     256 workgroups x 4 waves = one wave per SIMD on every CU, all resident
+//     (the previous 256-thread-per-problem kernel fit only 2 problems per CU and
+//     ran the batch in two rounds);
+//   * no s_barrier in the sweep: all cross-lane exchange goes through the wave's
+//     private LDS region (in-order LDS, wave-scope fences only);
+//   * S_i is streamed through a register double buffer (PL_ADMM_KM 4x4 tile slots
+//     per lane, 1 KiB-contiguous 16-byte loads): step q issues the loads of step
+//     q+1's block before it touches its own, so every block has a whole step of
+//     latency cover; the small operands of step q+1 follow the same pipeline;
+//   * every distinct node program (u16 gather lists) is LDS-resident for the whole
+//     launch and shared by the PPW waves.
+// The symmetric mat-vec uses the packed lower 4x4 tiles: each tile gives 4 row
+// partials (accumulated per lane over the lane's run of tiles in a tile row, one
+// LDS "segment" per (lane, tile row)) and 4 column partials (one LDS slot per
+// tile); every output sums its segments and the column partials of its tile
+// column in a fixed order, so results are bit-identical for a problem regardless
+// of the batch or workgroup it runs in.
 #include <algorithm>
 #include <type_traits>
 
@@ -33,139 +44,161 @@
 
 namespace {
 
-constexpr int NT = 256;
+constexpr int KM = PL_ADMM_KM, CWM = PL_ADMM_CWM, XCM = PL_ADMM_XCM, MV = PL_ADMM_MV, MR = PL_ADMM_MR;
 
-struct Sreg {
-  double2 t[16];
+enum { KF0 = 0, KFWD = 1, KTN = 2, KBWD = 3, KT0 = 4, KB0 = 5 };
+
+__device__ __forceinline__ int step_kind_v(int q, int N, int niter, int& i, int& it) {
+  if (q == 0) {
+    i = 0;
+    it = 0;
+    return KF0;
+  }
+  const int r = (q - 1) % (2 * N);
+  it = (q - 1) / (2 * N);
+  if (r < N - 1) {
+    i = r + 1;
+    return KFWD;
+  }
+  if (r == N - 1) {
+    i = N;
+    return KTN;
+  }
+  if (r < 2 * N - 1) {
+    i = 2 * N - 1 - r;
+    return KBWD;
+  }
+  i = 0;
+  return it < niter - 1 ? KT0 : KB0;
+}
+
+// the schedule is wave-uniform; readfirstlane keeps it (and every node-table read and
+// base address derived from it) in scalar registers
+__device__ __forceinline__ int step_kind(int q, int N, int niter, int& i, int& it) {
+  const int k = step_kind_v(q, N, niter, i, it);
+  i = __builtin_amdgcn_readfirstlane(i);
+  it = __builtin_amdgcn_readfirstlane(it);
+  return __builtin_amdgcn_readfirstlane(k);
+}
+
+__device__ __forceinline__ bool bwd_kind(int k) { return k >= KBWD; }
+
+__device__ __forceinline__ double sel2(const double2& v, int k) { return k == 0 ? v.x : v.y; }
+__device__ __forceinline__ void set2(double2& v, int k, double x) {
+  if (k == 0) v.x = x;
+  else v.y = x;
+}
+
+// Cross-lane LDS exchange inside one wave: LDS executes a wave's operations in
+// order, so only the compiler has to be kept from reordering across the phase.
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// sum_{k0 <= k < k1} f(k), 8 clamped independent reads per round (branch-free within a
+// round, so the LDS reads of a round issue back to back)
+template <int U = 8, class F>
+__device__ __forceinline__ double range_sum(int k0, int k1, F f) {
+  double acc = 0.0;
+  for (int b = k0; b < k1; b += U) {
+    double t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[u] = f(min(b + u, k1 - 1));
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += (b + u < k1) ? t[u] : 0.0;
+  }
+  return acc;
+}
+
+// Global accesses as scalar base + unsigned 32-bit byte offset (the saddr + voffset
+// form: no per-lane 64-bit address arithmetic).  Indices are < 2^32 / sizeof(T).
+template <class T>
+__device__ __forceinline__ T gld(const T* base, int idx) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (unsigned)idx * (unsigned)sizeof(T));
+}
+template <class T>
+__device__ __forceinline__ void gst(T* base, int idx, T v) {
+  *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (unsigned)idx * (unsigned)sizeof(T)) = v;
+}
+
+__device__ __forceinline__ int div_k(int t, int K, unsigned km) { return K == 1 ? t : (int)__umulhi((unsigned)t, km); }
+
+__device__ __forceinline__ void tile_ij(int t, int& I, int& J) {
+  I = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+  while (I * (I + 1) / 2 > t) --I;
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  J = t - I * (I + 1) / 2;
+}
+
+struct Sbuf {
+  double2 s[KM][8];
+};
+// operands of a step needed at its start (double-buffered across steps)
+struct Early {
+  double acw[CWM];  // forward: A of the w part of coupling row `lane` of node i-1
+  double axc[XCM];  // forward: A of the coupling entries of dx_i column `lane`
+  double rhoc;      // rho of coupling row `lane` (node i-1 forward, node i backward)
+  double vv[MV];    // forward: rhs_i, backward: bt_i (columns lane, lane + 64)
+};
+struct LateR {  // backward rows of node i (lane, lane + 64, lane + 128)
+  double z[MR], y[MR], rho[MR], l[MR], u[MR];
+};
+struct LateC {  // backward columns of node i
+  double x[MV], q[MV];
 };
 
-// Operands a step needs before its mat-vec (double-buffered across steps).
-template <int ASR>
-struct Small {
-  double as[ASR];  // A values of the node the step gathers from (entries tid + NT k)
-  double v0;       // forward: rhs_i[c]; backward: bt_i[c]
-  double rhoc;     // rho of coupling row tid of the gather node
-};
-// Operands a backward step needs after its mat-vec (single buffer, loaded at
-// the end of the previous step: waited on only after the S loads ahead of
-// them have retired).
-struct Late {
-  double xa, qs;           // x_i[c], q_i[c]
-  double z, y, rho, l, u;  // row data of node i
-};
-
-__device__ __forceinline__ int sched_node(int p, int N, bool& fwd) {
-  const int k = p % (2 * (N + 1));
-  fwd = k <= N;
-  return fwd ? k : 2 * N + 1 - k;
-}
-
-// Unconditional (clamped) loads: with no branch around them the waitcnt pass
-// keeps exact vmcnt counts, so later waits never drain the whole queue.
-__device__ __forceinline__ void load_S(const double* __restrict__ Sn, int nunit, Sreg& R) {
-  const int u = min((int)threadIdx.x, nunit - 1);
-  const double2* p = reinterpret_cast<const double2*>(Sn);
-#pragma unroll
-  for (int k = 0; k < 16; ++k) R.t[k] = p[(unsigned)(k * nunit + u)];
-}
-
-// Partial products of y = S v for this thread's unit: 8 row sums of the 8x4
-// sub-block against v_J, and (off-diagonal tiles) 4 column sums against v_I.
-__device__ __forceinline__ void matvec_partials(const Sreg& R, int nunit, const double* v, double* dpart,
-                                                double* tpart) {
-  const int u = threadIdx.x;
-  if (u < nunit) {
-    const int t = u >> 1, h = u & 1;
-    int I = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-    while (I * (I + 1) / 2 > t) --I;
-    while ((I + 1) * (I + 2) / 2 <= t) ++I;
-    const int J = t - I * (I + 1) / 2;
-    double vj[4], vi[8];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) vj[c] = v[8 * J + 4 * h + c];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) vi[r] = v[8 * I + r];
-    double tp[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const double e0 = R.t[2 * r].x, e1 = R.t[2 * r].y, e2 = R.t[2 * r + 1].x, e3 = R.t[2 * r + 1].y;
-      dpart[u * 8 + r] = e0 * vj[0] + e1 * vj[1] + e2 * vj[2] + e3 * vj[3];
-      tp[0] += e0 * vi[r];
-      tp[1] += e1 * vi[r];
-      tp[2] += e2 * vi[r];
-      tp[3] += e3 * vi[r];
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) tpart[u * 4 + c] = (I != J) ? tp[c] : 0.0;
-  }
-}
-
-__device__ __forceinline__ double matvec_reduce(int o, int ntile, const double* dpart, const double* tpart) {
-  // fixed trip counts (ntile <= 14) so all LDS reads issue before the adds
-  const int I = o >> 3, r = o & 7;
-  const int t0 = I * (I + 1) / 2;
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-#pragma unroll
-  for (int J = 0; J < 14; ++J)
-    if (J <= I) {
-      a0 += dpart[(2 * (t0 + J)) * 8 + r];
-      a1 += dpart[(2 * (t0 + J) + 1) * 8 + r];
-    }
-#pragma unroll
-  for (int k = 1; k < 14; ++k) {
-    const int Ip = I + k;
-    if (Ip < ntile) a2 += tpart[(2 * (Ip * (Ip + 1) / 2 + I) + (r >> 2)) * 4 + (r & 3)];
-  }
-  return (a0 + a1) + a2;
-}
-
-struct LdsMap {
-  int v, cpl, row, unit, ent;  // capacities (doubles); v >= nw_max + ndx
-  int prog_len;                // LDS gather-program buffer (u16), the longest node program
-  int chunk;                   // chunk partial sums
-  __host__ __device__ size_t total() const {
-    return (4 * (size_t)v + cpl + row + 12 * (size_t)unit + ent + chunk) * sizeof(double) + 2 * (size_t)prog_len;
-  }
+// Per-wave LDS carve-up (offsets in doubles from the wave's region).
+struct AdmmLds {
+  int prog_dbl;  // all ADMM programs (u16), rounded to 16 bytes, in doubles
+  int per_wave;
+  int v, y, xn, r1, tcpl, trow, red, colp, asb, asb_cap;
 };
 
 }  // namespace
 
-template <int ASR, bool TIMING>
-__global__ __launch_bounds__(256, 2) void k_admm(PlDev d, int N, int n, int m, int nnz, int ndx, int S_stride, LdsMap lm,
-                                                 int niter, int check, double sigma, double alpha) {
-  // optional phase timing (s_memtime, thread 0): [fwd: 6 phases][bwd: 8 phases]
-  __shared__ unsigned long long tacc[TIMING ? 17 : 1];
-  if constexpr (TIMING) {
-    if (threadIdx.x < 17) tacc[threadIdx.x] = 0;
+template <int PPW, int ASR, bool TIMING>
+__global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int n, int m, int nnz, int ndx,
+                                                      int S_stride, int cpl_stride, AdmmLds lm, int niter, int check,
+                                                      int fwd_asb, double sigma, double alpha) {
+  extern __shared__ double lds[];
+  {  // every node program, shared by the waves of the workgroup
+    const uint4* src = reinterpret_cast<const uint4*>(d.aprog);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    for (int k = threadIdx.x; k < lm.prog_dbl / 2; k += 64 * PPW) dst[k] = src[k];
   }
-  auto T = [&](int slot) {
-    if constexpr (TIMING) {
-      if (threadIdx.x == 0) {
-        const unsigned long long now = __builtin_amdgcn_s_memtime();
-        if (slot >= 0) tacc[slot] += now - tacc[16];
-        tacc[16] = now;
-      }
-    }
-  };
-  const int b = blockIdx.x;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar bases
+  const int b = blockIdx.x * PPW + wv;
+  if (b >= B) return;
   PlProbInfo* info = d.info + b;
   if (info->done) return;
-  extern __shared__ double lds[];
-  double* v = lds;          // mat-vec input, zero padded to 8 * ntile
-  double* y = v + lm.v;     // mat-vec output; backward: [x~_i | x~_{i+1}(dx)]
-  double* xn = y + lm.v;    // x~_{i+1} (dx part) across backward steps
-  double* tcpl = xn + lm.v;
-  double* trow = tcpl + lm.cpl;
-  double* dpart = trow + lm.row;
-  double* tpart = dpart + 8 * lm.unit;
-  double* asb = tpart + 4 * lm.unit;
-  double* v0fix = asb + lm.ent;  // rhs_0 handed from backward node 0 to forward node 0
-  double* part = v0fix + lm.v;   // chunk partial sums
-  uint16_t* lprog = reinterpret_cast<uint16_t*>(part + lm.chunk);
+  // optional phase timing (s_memtime, per wave) into d.dbg[b][0..15]
+  unsigned long long tacc[TIMING ? 12 : 1] = {}, tlast = 0;
+  auto T = [&](int slot) __attribute__((always_inline)) {
+    if constexpr (TIMING) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (slot >= 0) tacc[slot] += now - tlast;
+      tlast = now;
+    }
+  };
+  const uint16_t* PG = reinterpret_cast<const uint16_t*>(lds);
+  double* W = lds + lm.prog_dbl + wv * lm.per_wave;
+  double* v = W + lm.v;        // mat-vec input (zero padded to 4 T)
+  double* y = W + lm.y;        // mat-vec output; backward: [x~_i | x~_{i+1}(dx)]
+  double* xn = W + lm.xn;      // x~_{i+1} (dx part) across backward steps
+  double* r1 = W + lm.r1;      // rhs_1 (dx part) completed by T0, read by the next forward 1
+  double* tcpl = W + lm.tcpl;  // coupling-row products (before the mat-vec; aliases `red`)
+  double* trow = W + lm.trow;  // rho z - y of the node's rows (after the mat-vec; aliases `red`)
+  double* seg = W + lm.red;    // mat-vec row segments [(lane + I) * 4 + r]
+  double* colp = W + lm.colp;  // mat-vec column partials, off-diagonal tiles in column-major order
+  double* part = W + lm.red;   // chunk sums of the row / column gathers (after the mat-vec)
+  double* asb = W + lm.asb;    // A values of the backward node
 
   const double* __restrict__ As = d.As + (size_t)b * nnz;
   const double* __restrict__ rho = d.rho + (size_t)b * m;
-  const double* __restrict__ rhoc = d.rhoc + (size_t)b * (N + 1) * lm.cpl;
+  const double* __restrict__ rhoc = d.rhoc + (size_t)b * (N + 1) * cpl_stride;
   const double* __restrict__ ls = d.ls + (size_t)b * m;
   const double* __restrict__ us = d.us + (size_t)b * m;
   const double* __restrict__ qs = d.qs + (size_t)b * n;
@@ -177,320 +210,622 @@ __global__ __launch_bounds__(256, 2) void k_admm(PlDev d, int N, int n, int m, i
   double* bt = d.bt + (size_t)b * n;
   double* dxs = d.dxs + (size_t)b * n;
   double* dys = d.dys + (size_t)b * m;
-  // Node table: uniform reads through the constant address space are scalar
-  // loads (lgkmcnt), which cannot drain the S stream.
-  typedef const __attribute__((address_space(4))) PlAdmmNode* CNode;  // constant AS -> s_load
+  // node table: uniform reads through the constant address space are scalar loads
+  typedef const __attribute__((address_space(4))) PlAdmmNode* CNode;
   CNode an = (CNode)d.anodes;
-  const uint16_t* __restrict__ prog = d.aprog;
-  const int tid = threadIdx.x;
-  const int P = niter * 2 * (N + 1);
+  const int Q = 1 + niter * 2 * N;
 
-  int cur_prog = -1;
-  // make node `i`'s gather program the one in LDS (synchronous; only when the
-  // node type changes, a few times per sweep)
-  auto use_prog = [&](int i) {
-    const int pr = an[i].prog, len = an[i].prog_len;
-    if (pr == cur_prog) return;
-    __syncthreads();
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(prog + pr);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(lprog);
-    for (int k = tid; k < (len >> 1); k += NT) dst[k] = src[k];
-    cur_prog = pr;
-    __syncthreads();
-  };
+  // Software pipeline.  Step q issues, in this order: the deferred end-of-step
+  // stores of step q-1, the operands of step q+1 (E, las, LR, LC -- right after
+  // their step-q copies are consumed), then the factor block of step q+1 slot by
+  // slot inside its own mat-vec.  So the only vector-memory wait of a step is at
+  // its start, and it is for data issued a whole step earlier.
+  Sbuf SR;  // factor slots of the current block; refilled with the next block's as they are consumed
+  Early E, En;  // current / next step (the copy at the start of a step is its only vmcnt wait)
+  double las[ASR];
+  LateR LR, LRn;
+  LateC LC, LCn;
+  double rkeep = 0.0;           // rhs of node i (dx part, lane < ndx) completed at node i-1
+  double2 r0v = make_double2(0.0, 0.0);  // rhs_0 of the backward-0 half of T0 (columns lane, lane + 64)
+  bool fix1 = false;
+  // deferred end-of-step stores (x update and rhs of a backward / TN step)
+  double2 pxa = make_double2(0.0, 0.0), pdx = pxa, prh = pxa;
+  double prn = 0.0;
+  int pnode = -1, pkind = KF0;
+  bool psd = false;
 
-  Sreg S;
-  Small<ASR> QA, QB;
-  double rhs_keep = 0.0;  // rhs of the dx part of node i+1 (thread c < ndx), completed at node i
-
-  // Loads of step p's small operands.  No load here depends on another vector
-  // load, so nothing waits before the S stream behind them is issued.
-  auto prefetch_small = [&](int p, Small<ASR>& Q) {
-    if (p >= P) return;
-    bool f;
-    const int i = sched_node(p, N, f);
-    const int ia = f ? i - 1 : i;
-    const int ia_c = ia >= 0 ? ia : 0;
-    const int ne = an[ia_c].nent, eo = an[ia_c].ent_off, nc = an[ia_c].ncpl;
-    const int xo = an[i].x_off, nw = an[i].nw;
-    // clamped, unconditional loads (allocations are padded past the end)
-    const int nemax = max(ne - 1, 0);
+  // ---------------- loads (unconditional and clamped: exact vmcnt accounting)
+  auto load_S = [&](int i, int kbase, Sbuf& R) __attribute__((always_inline)) {
+    const int K = an[i].nunit;
+    const double2* p = reinterpret_cast<const double2*>(Sg + an[i].s_off);
 #pragma unroll
-    for (int k = 0; k < ASR; ++k) Q.as[k] = As[eo + min(tid + NT * k, nemax)];
-    Q.rhoc = rhoc[ia_c * lm.cpl + min(tid, lm.cpl - 1)];
-    const double* vsrc = f ? rhs : bt;
-    Q.v0 = vsrc[xo + min(tid, nw - 1)];
+    for (int k = 0; k < KM; ++k) {
+      const int kk = min(kbase + k, K - 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) R.s[k][j] = gld(p, (kk * 8 + j) * 64 + lane);
+    }
   };
-  Late LT;
-  auto prefetch_late = [&](int p) {
-    if (p >= P) return;
-    bool f;
-    const int i = sched_node(p, N, f);
-    const int xo = an[i].x_off, nw = an[i].nw, nrow = an[i].nrow, ro = an[i].row_off;
-    if (f) return;
-    const int j = xo + min(tid, nw - 1);
-    LT.xa = xa[j];
-    LT.qs = qs[j];
-    const int r = ro + min(tid, max(nrow - 1, 0));
-    LT.z = za[r];
-    LT.y = ya[r];
-    LT.rho = rho[r];
-    LT.l = ls[r];
-    LT.u = us[r];
+  auto prefetch_E = [&](int kind1, int i1, Early& E) __attribute__((always_inline)) {
+    const bool fw = kind1 == KFWD || kind1 == KTN;
+    const bool fr = fw && !fwd_asb;  // coupling A values through registers
+    const int g = fw ? i1 - 1 : i1;
+    const uint16_t* P = PG + an[g].prog;
+    const int ncp = an[g].ncpl, eo = an[g].ent_off;
+    const int s = min(lane, max(ncp - 1, 0));
+    {
+      const int q0 = P[an[g].cwptr + s], cnt = fr ? P[an[g].cwptr + s + 1] - q0 : 0;
+      const uint32_t* cw = reinterpret_cast<const uint32_t*>(P + an[g].cwp);
+#pragma unroll
+      for (int k = 0; k < CWM; ++k) {
+        const int e = cnt > 0 ? (int)(cw[q0 + min(k, cnt - 1)] & 0xffff) : 0;
+        E.acw[k] = gld(As, eo + e);
+      }
+    }
+    {
+      const int c = min(lane, ndx - 1);
+      const int q0 = P[an[g].xcptr + c], cnt = fr ? P[an[g].xcptr + c + 1] - q0 : 0;
+      const uint32_t* xc = reinterpret_cast<const uint32_t*>(P + an[g].xcp);
+#pragma unroll
+      for (int k = 0; k < XCM; ++k) {
+        const int e = cnt > 0 ? (int)(xc[q0 + min(k, cnt - 1)] & 0xffff) : 0;
+        E.axc[k] = gld(As, eo + e);
+      }
+    }
+    E.rhoc = gld(rhoc, g * cpl_stride + s);
+    const double* src = (kind1 == KF0 || fw) ? rhs : bt;
+    const int xo = an[i1].x_off, nw1 = an[i1].nw;
+#pragma unroll
+    for (int mm = 0; mm < MV; ++mm) E.vv[mm] = gld(src, xo + min(lane + 64 * mm, nw1 - 1));
   };
-  auto prefetch_S = [&](int p) {
-    if (p >= P) return;
-    bool f;
-    const int i = sched_node(p, N, f);
-    const int so = an[i].s_off, nu = an[i].nunit;
-    load_S(Sg + so, nu, S);
+  auto prefetch_as = [&](int kind1, int i1) __attribute__((always_inline)) {
+    // backward steps: A of node i1; forward steps with dense coupling rows: A of node i1 - 1
+    const bool fa = fwd_asb && (kind1 == KFWD || kind1 == KTN);
+    const bool bw = bwd_kind(kind1) || fa;
+    const int ia = fa ? i1 - 1 : i1;
+    const int eo = an[ia].ent_off, ne = an[ia].nent;
+#pragma unroll
+    for (int k = 0; k < ASR; ++k) las[k] = gld(As, eo + (bw ? min(lane + 64 * k, ne - 1) : 0));
+  };
+  auto prefetch_LR = [&](int kind1, int i1, LateR& LR) __attribute__((always_inline)) {
+    const bool bw = bwd_kind(kind1);
+    const int ro = an[i1].row_off, nr = an[i1].nrow;
+#pragma unroll
+    for (int mm = 0; mm < MR; ++mm) {
+      const int r = ro + (bw ? min(lane + 64 * mm, max(nr - 1, 0)) : 0);
+      LR.z[mm] = gld(za, r);
+      LR.y[mm] = gld(ya, r);
+      LR.rho[mm] = gld(rho, r);
+      LR.l[mm] = gld(ls, r);
+      LR.u[mm] = gld(us, r);
+    }
+  };
+  auto prefetch_LC = [&](int kind1, int i1, LateC& LC) __attribute__((always_inline)) {
+    const bool need = bwd_kind(kind1) || kind1 == KTN;
+    const int xo = an[i1].x_off, nw1 = an[i1].nw;
+#pragma unroll
+    for (int mm = 0; mm < MV; ++mm) {
+      const int j = xo + (need ? min(lane + 64 * mm, nw1 - 1) : 0);
+      LC.x[mm] = gld(xa, j);
+      LC.q[mm] = gld(qs, j);
+    }
   };
 
-  auto step = [&](auto bufsel, int p) {
-    constexpr bool odd = decltype(bufsel)::value;
-    Small<ASR>& Q = odd ? QB : QA;
-    Small<ASR>& Qn = odd ? QA : QB;
-    bool fwd;
-    const int i = sched_node(p, N, fwd);
-    const int nw = an[i].nw, ntile = an[i].ntile, nunit = an[i].nunit, x_off = an[i].x_off;
-    const int ia = fwd ? i - 1 : i;
-    const int ia_c = ia >= 0 ? ia : 0;
-    const int ne = an[ia_c].nent, eo = an[ia_c].ent_off;
-    // all node fields are read here, in uniform control flow (scalar loads)
-    const int g = ia_c;
-    const int g_ncpl = an[g].ncpl, g_cwptr = an[g].cwptr, g_cwp = an[g].cwp, g_xcptr = an[g].xcptr,
-              g_xcp = an[g].xcp, g_cxptr = an[g].cxptr, g_cxp = an[g].cxp, g_ccptr = an[g].ccptr,
-              g_ccp = an[g].ccp, g_rowptr = an[g].rowptr, g_rowp = an[g].rowp, g_colptr = an[g].colptr,
-              g_colr = an[g].colr, g_nrow = an[g].nrow, g_row_off = an[g].row_off, g_rchn = an[g].rchn,
-              g_rch = an[g].rch, g_rchptr = an[g].rchptr, g_cchn = an[g].cchn, g_cch = an[g].cch,
-              g_cchptr = an[g].cchptr;
-    const int x_next = (!fwd && i < N) ? an[i + 1].x_off : 0;
-    const uint16_t* pg = lprog;
-    T(-1);
-    __syncthreads();  // previous step done with asb / trow / tcpl / v / y
-    T(fwd ? 0 : 8);
-    if (ia >= 0) {
-      use_prog(ia);
-      // A values of node ia into LDS: the first NT * ASR from registers, the
-      // rest (nodes larger than the dominant type) straight from HBM
+  // ---------------- y[0..nw) = S_i v  (R holds slots 0..KM-1 unless reload).  Slot k
+  // of node next's block is loaded into R as soon as the last pass has consumed slot
+  // k (the software pipeline of the factor stream; next = i re-reads the block).
+  auto matvec = [&](Sbuf& R, int i, bool reload, int next) __attribute__((always_inline)) {
+    const int K = an[i].nunit, T = an[i].ntile, ntl = an[i].ntl, nw = an[i].nw;
+    const int Kn = an[next].nunit;
+    const double2* pn = reinterpret_cast<const double2*>(Sg + an[next].s_off);
+    const unsigned km = an[i].kmagic;
+    const double2* v2 = reinterpret_cast<const double2*>(v);
+    int curI = -1;
+    double sa[4] = {0.0, 0.0, 0.0, 0.0};
+    auto pass = [&](int kb, bool last_pass) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const int kk = kb + k;
+        const int t = K * lane + kk;
+        if (kk < K && t < ntl) {
+          int I, J;
+          tile_ij(t, I, J);
+          const double2 a0 = v2[2 * J], a1 = v2[2 * J + 1];
+          double rp[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            rp[r] = R.s[k][2 * r].x * a0.x + R.s[k][2 * r].y * a0.y + R.s[k][2 * r + 1].x * a1.x +
+                    R.s[k][2 * r + 1].y * a1.y;
+          if (I != J) {
+            const double2 c0 = v2[2 * I], c1 = v2[2 * I + 1];
+            const double vi[4] = {c0.x, c0.y, c1.x, c1.y};
+            double cp[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              cp[0] += R.s[k][2 * r].x * vi[r];
+              cp[1] += R.s[k][2 * r].y * vi[r];
+              cp[2] += R.s[k][2 * r + 1].x * vi[r];
+              cp[3] += R.s[k][2 * r + 1].y * vi[r];
+            }
+            // column-major packed off-diagonal index: the partials of one output tile
+            // column are contiguous
+            double2* cpp = reinterpret_cast<double2*>(colp + ((J * (2 * T - J - 1)) / 2 + I - J - 1) * 4);
+            cpp[0] = make_double2(cp[0], cp[1]);
+            cpp[1] = make_double2(cp[2], cp[3]);
+          }
+          if (I != curI) {
+            if (curI >= 0) {
+              double2* sp = reinterpret_cast<double2*>(seg + (lane + curI) * 4);
+              sp[0] = make_double2(sa[0], sa[1]);
+              sp[1] = make_double2(sa[2], sa[3]);
+            }
+            curI = I;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sa[r] = rp[r];
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sa[r] += rp[r];
+          }
+        }
+        if (last_pass) {  // uniform; always true for blocks of <= KM slots per lane
+          const int kq = min(k, Kn - 1);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) R.s[k][j] = gld(pn, (kq * 8 + j) * 64 + lane);
+        }
+      }
+    };
+    if (K <= KM && !reload) {
+      pass(0, true);  // the common case, straight-line: the refill loads never force a wait
+    } else {
+      for (int kb = 0; kb < K; kb += KM) {
+        load_S(i, kb, R);  // blocks with more than KM slots per lane (synchronous)
+        pass(kb, kb + KM >= K);
+      }
+    }
+    if (curI >= 0) {
+      double2* sp = reinterpret_cast<double2*>(seg + (lane + curI) * 4);
+      sp[0] = make_double2(sa[0], sa[1]);
+      sp[1] = make_double2(sa[2], sa[3]);
+    }
+    wsync();
+#pragma unroll
+    for (int mm = 0; mm < MV; ++mm) {
+      const int o = lane + 64 * mm;
+      if (o < nw) {
+        const int I = o >> 2, r = o & 3;
+        const int t0 = I * (I + 1) / 2;
+        const int lf = div_k(t0, K, km), ll = div_k(t0 + I, K, km);
+        const double rs = range_sum(lf, ll + 1, [&](int lp) { return seg[(lp + I) * 4 + r]; });
+        const int cb = (I * (2 * T - I - 1)) / 2;
+        const double cs = range_sum(cb, cb + T - 1 - I, [&](int c) { return colp[c * 4 + r]; });
+        y[o] = rs + cs;
+      }
+    }
+    wsync();
+  };
+
+  // ---------------- deferred stores of the previous step
+  auto flush = [&]() __attribute__((always_inline)) {
+    if (pnode < 0) return;
+    const int ip = pnode, nwp = an[ip].nw, xo = an[ip].x_off;
+    const bool pb = bwd_kind(pkind);
+    const int xnx = pb ? an[ip + 1].x_off : 0;
+#pragma unroll
+    for (int mm = 0; mm < MV; ++mm) {
+      const int c = lane + 64 * mm;
+      if (c < nwp) {
+        gst(xa, xo + c, sel2(pxa, mm));
+        if (psd) gst(dxs, xo + c, sel2(pdx, mm));
+        if (pb) {
+          if (c < ndx) gst(rhs, xnx + c, prn);
+          if (!(c < ndx && ip > 0)) gst(rhs, xo + c, sel2(prh, mm));
+        }
+      }
+    }
+    pnode = -1;
+  };
+
+  // ---------------- one step of the schedule
+  auto step = [&](int q) __attribute__((always_inline)) {
+    int i, it;
+    const int kind = step_kind(q, N, niter, i, it);
+    const bool has_next = q + 1 < Q;
+    int i1 = 0, it1 = 0;
+    const int kind1 = has_next ? step_kind(q + 1, N, niter, i1, it1) : kind;
+    if (!has_next) i1 = i;
+    const bool bw = bwd_kind(kind);
+    const bool store_delta = check && it == niter - 1;
+    const int nw = an[i].nw, x_off = an[i].x_off, T4 = 4 * an[i].ntile;
+    const int eo = an[i].ent_off, ne = an[i].nent;
+    const double* __restrict__ Ai = As + eo;
+    const int cap = lm.asb_cap;
+    const uint16_t* P = PG + an[i].prog;
+    auto stage = [&](int ns, const double* __restrict__ src) __attribute__((always_inline)) {
 #pragma unroll
       for (int k = 0; k < ASR; ++k) {
-        const int idx = tid + NT * k;
-        if (idx < ne) asb[idx] = Q.as[k];
+        const int e = lane + 64 * k;
+        if (e < ns && e < cap) asb[e] = las[k];
       }
-      for (int idx = tid + NT * ASR; idx < ne; idx += NT) asb[idx] = As[eo + idx];
-    }
-    T(fwd ? 1 : 9);
-    // ---------------- gathers before the mat-vec: v = bt_i (fwd) / bt_i - K_{i+1,i}^T x~_{i+1} (bwd)
-    if (fwd) {
-      if (i > 0) {
-        const uint32_t* cw = reinterpret_cast<const uint32_t*>(pg + g_cwp);
-        __syncthreads();
-        if (tid < g_ncpl) {  // t_s = rho_s a_s(w_{i-1}) . w_{i-1}
-          double acc = 0.0;
-          const int q0 = pg[g_cwptr + tid], q1 = pg[g_cwptr + tid + 1];
-#pragma unroll 4
-          for (int q = q0; q < q1; ++q) {
-            const uint32_t w = cw[q];
-            acc += asb[w & 0xffff] * y[w >> 16];
-          }
-          tcpl[tid] = Q.rhoc * acc;
+      for (int e = 64 * ASR + lane; e < min(ns, cap); e += 64) asb[e] = src[e];
+      wsync();
+    };
+    // gathers over A: LDS only when the node's A fits (uniform), else LDS + global
+    // (the overflow path ends with vmcnt(0) so its global loads never leave pending
+    // state behind for the wait-count bookkeeping of the common path)
+    auto with_A = [&](int ns, const double* __restrict__ src, auto body) __attribute__((always_inline)) {
+      if (ns <= cap) {
+        body([&](int e) __attribute__((always_inline)) { return asb[e]; });
+      } else {
+        typedef const __attribute__((address_space(1))) double* GPtr;
+        const GPtr gs = (GPtr)src;
+        body([&](int e) __attribute__((always_inline)) { return e < cap ? asb[e] : gs[e]; });
+        __builtin_amdgcn_s_waitcnt(0xF70);
+      }
+    };
+    T(-1);
+    // ---- start: everything prefetched for this step becomes current (the one wait),
+    // this step's A goes to LDS, then the previous step's deferred stores
+    __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): step q-1's loads (and stores) are done
+    E = En;
+    LR = LRn;
+    LC = LCn;
+    if (bw) stage(ne, Ai);
+    else if (fwd_asb && kind != KF0) stage(an[i - 1].nent, As + an[i - 1].ent_off);
+    T(0);
+    flush();
+    T(1);
+    if (bw) {
+      with_A(ne, Ai, [&](auto A) __attribute__((always_inline)) {
+        // ---- t_s = rho_s a_s(dx_{i+1}) . x~_{i+1}
+        const int ncp = an[i].ncpl;
+        if (lane < ncp) {
+          const uint32_t* cx = reinterpret_cast<const uint32_t*>(P + an[i].cxp);
+          const int q0 = P[an[i].cxptr + lane], q1 = P[an[i].cxptr + lane + 1];
+          const double acc = range_sum<2>(q0, q1, [&](int qq) {
+            const uint32_t w = cx[qq];
+            return A(w & 0xffff) * xn[w >> 16];
+          });
+          tcpl[lane] = E.rhoc * acc;
         }
-        __syncthreads();
-      }
-      if (tid < nw) {  // bt_i = rhs_i - A_{c,dx_i}^T t
-        double vv = i == 0 ? v0fix[tid] : Q.v0;
-        if (i > 0 && tid < ndx) {
-          const uint32_t* xc = reinterpret_cast<const uint32_t*>(pg + g_xcp);
-          double acc = 0.0;
-          const int q0 = pg[g_xcptr + tid], q1 = pg[g_xcptr + tid + 1];
-#pragma unroll 4
-          for (int q = q0; q < q1; ++q) {
-            const uint32_t w = xc[q];
-            acc += asb[w & 0xffff] * tcpl[w >> 16];
-          }
-          vv -= acc;
-        }
-        bt[x_off + tid] = vv;
-        v[tid] = vv;
-      } else if (tid < 8 * ntile) {
-        v[tid] = 0.0;
-      }
-    } else {
-      __syncthreads();
-      if (i < N && tid < g_ncpl) {  // t_s = rho_s a_s(dx_{i+1}) . x~_{i+1}
-        const uint32_t* cx = reinterpret_cast<const uint32_t*>(pg + g_cxp);
-        double acc = 0.0;
-        const int q0 = pg[g_cxptr + tid], q1 = pg[g_cxptr + tid + 1];
-#pragma unroll 4
-        for (int q = q0; q < q1; ++q) {
-          const uint32_t w = cx[q];
-          acc += asb[w & 0xffff] * xn[w >> 16];
-        }
-        tcpl[tid] = Q.rhoc * acc;
-      }
-      __syncthreads();
-      if (tid < nw) {  // bt_i - A_{c,w_i}^T t
-        double vv = Q.v0;
-        if (i < N) {
-          const uint32_t* cc = reinterpret_cast<const uint32_t*>(pg + g_ccp);
-          double acc = 0.0;
-          const int q0 = pg[g_ccptr + tid], q1 = pg[g_ccptr + tid + 1];
-#pragma unroll 4
-          for (int q = q0; q < q1; ++q) {
-            const uint32_t w = cc[q];
-            acc += asb[w & 0xffff] * tcpl[w >> 16];
-          }
-          vv -= acc;
-        }
-        v[tid] = vv;
-      } else if (tid < 8 * ntile) {
-        v[tid] = 0.0;
-      }
-    }
-    __syncthreads();
-    T(fwd ? 2 : 10);
-    // ---------------- mat-vec with S_i, then issue the next step's operands
-    matvec_partials(S, nunit, v, dpart, tpart);
-    __syncthreads();
-    T(fwd ? 3 : 11);
-    prefetch_small(p + 1, Qn);
-    __builtin_amdgcn_sched_barrier(0);
-    prefetch_S(p + 1);
-    T(fwd ? 4 : 12);
-    if (tid < nw) y[tid] = matvec_reduce(tid, ntile, dpart, tpart);  // w_i / x~_i
-    else if (!fwd && tid < nw + ndx && i < N) y[tid] = xn[tid - nw];  // x~_{i+1} (dx) behind x~_i
-    T(fwd ? 5 : -1);
-    if (!fwd) {
-      // ---------------- backward: finish the iteration for the rows / columns of node i
-      __syncthreads();
-      T(13);
-      const bool store_delta = check && (p >= P - (N + 1));
-      // z~ = A x~ over balanced chunks of <= PL_CHUNK entries, one chunk per thread
-      {
-        const uint32_t* rw = reinterpret_cast<const uint32_t*>(pg + g_rowp);
-        const uint32_t* rch = reinterpret_cast<const uint32_t*>(pg + g_rch);
-        for (int t = tid; t < g_rchn; t += NT) {
-          const uint32_t c = rch[t];
-          const int q0 = c & 0xffff, len = (int)(c >> 16) - q0;
-          double acc = 0.0;
+        wsync();
+        // ---- v = bt_i - A_{c,w_i}^T t
+        const uint32_t* cc = reinterpret_cast<const uint32_t*>(P + an[i].ccp);
 #pragma unroll
-          for (int k = 0; k < PL_CHUNK; ++k)
-            if (k < len) {
-              const uint32_t w = rw[q0 + k];
-              acc += asb[w & 0xffff] * y[w >> 16];
+        for (int mm = 0; mm < MV; ++mm) {
+          const int c = lane + 64 * mm;
+          if (c < nw) {
+            const int q0 = P[an[i].ccptr + c], q1 = P[an[i].ccptr + c + 1];
+            v[c] = E.vv[mm] - range_sum<4>(q0, q1, [&](int qq) {
+                     const uint32_t w = cc[qq];
+                     return A(w & 0xffff) * tcpl[w >> 16];
+                   });
+          } else if (c < T4) {
+            v[c] = 0.0;
+          }
+        }
+      });
+      if (lane < ndx) y[nw + lane] = xn[lane];  // x~_{i+1} (dx) behind x~_i for the row gathers
+      wsync();
+    } else if (kind == KF0) {
+#pragma unroll
+      for (int mm = 0; mm < MV; ++mm) {
+        const int c = lane + 64 * mm;
+        if (c < nw) {
+          gst(bt, x_off + c, E.vv[mm]);
+          v[c] = E.vv[mm];
+        } else if (c < T4) {
+          v[c] = 0.0;
+        }
+      }
+      wsync();
+    } else {  // KFWD, KTN: coupling rows of node g = i - 1
+      const int g = i - 1;
+      const uint16_t* Pg = PG + an[g].prog;
+      const int ncp = an[g].ncpl;
+      const double* __restrict__ Ag = As + an[g].ent_off;
+      const bool fx = fix1 && i == 1;
+      fix1 = false;
+      auto fwd_gathers = [&](auto A, bool dense) __attribute__((always_inline)) {
+        if (lane < ncp) {  // t_s = rho_s a_s(w_{i-1}) . w_{i-1}
+          const uint32_t* cw = reinterpret_cast<const uint32_t*>(Pg + an[g].cwp);
+          const int q0 = Pg[an[g].cwptr + lane], q1 = Pg[an[g].cwptr + lane + 1];
+          double acc = 0.0;
+          if (dense) {
+            for (int qq = q0; qq < q1; ++qq) {
+              const uint32_t w = cw[qq];
+              acc += A(w & 0xffff) * y[w >> 16];
             }
-          part[t] = acc;
-        }
-      }
-      __syncthreads();
-      if (tid < g_nrow) {  // update_z, update_y (relaxed)
-        const int k0 = pg[g_rchptr + tid], k1 = pg[g_rchptr + tid + 1];
-        double zt = 0.0;
-#pragma unroll 4
-        for (int k = k0; k < k1; ++k) zt += part[k];
-        const double zrel = alpha * zt + (1.0 - alpha) * LT.z;
-        double zn = zrel + (1.0 / LT.rho) * LT.y;
-        zn = fmin(fmax(zn, LT.l), LT.u);
-        const double dy = LT.rho * (zrel - zn);
-        const double yn = LT.y + dy;
-        const int r = g_row_off + tid;
-        za[r] = zn;
-        ya[r] = yn;
-        if (store_delta) dys[r] = dy;
-        trow[tid] = LT.rho * zn - yn;
-      }
-      __syncthreads();
-      T(14);
-      // A^T (rho z - y) over column chunks
-      if (i < N) {
-        const uint16_t* colr = pg + g_colr;
-        const uint32_t* cch = reinterpret_cast<const uint32_t*>(pg + g_cch);
-        for (int t = tid; t < g_cchn; t += NT) {
-          const uint32_t c = cch[t];
-          const int e0 = c & 0xffff, len = (int)(c >> 16) - e0;
-          double acc = 0.0;
+          } else {
 #pragma unroll
-          for (int k = 0; k < PL_CHUNK; ++k)
-            if (k < len) acc += asb[e0 + k] * trow[colr[e0 + k]];
-          part[t] = acc;
+            for (int k = 0; k < CWM; ++k)
+              if (q0 + k < q1) acc += E.acw[k] * y[cw[q0 + k] >> 16];
+          }
+          tcpl[lane] = E.rhoc * acc;
         }
-        __syncthreads();
-      }
-      if (tid < nw) {  // update_x and next rhs = sigma x - q + A^T (rho z - y)
-        const int j = x_off + tid;
-        const double xnew = alpha * y[tid] + (1.0 - alpha) * LT.xa;
-        xa[j] = xnew;
-        if (store_delta) dxs[j] = xnew - LT.xa;
-        double acc = sigma * xnew - LT.qs;
-        if (i < N) {
-          const int k0 = pg[g_cchptr + tid], k1 = pg[g_cchptr + tid + 1];
-#pragma unroll 4
-          for (int k = k0; k < k1; ++k) acc += part[k];
-          if (tid < ndx) {  // rows of node i on dx_{i+1} complete rhs_{i+1}
-            double a2 = 0.0;
-            const int f0 = pg[g_cchptr + nw + tid], f1 = pg[g_cchptr + nw + tid + 1];
-#pragma unroll 4
-            for (int k = f0; k < f1; ++k) a2 += part[k];
-            rhs[x_next + tid] = rhs_keep + a2;
+        wsync();
+        const uint32_t* xc = reinterpret_cast<const uint32_t*>(Pg + an[g].xcp);
+#pragma unroll
+        for (int mm = 0; mm < MV; ++mm) {
+          const int c = lane + 64 * mm;
+          if (c < nw) {  // bt_i = rhs_i - A_{c,dx_i}^T t
+            double vv = (fx && c < ndx) ? r1[c] : E.vv[mm];
+            if (c < ndx) {
+              const int q0 = Pg[an[g].xcptr + c], q1 = Pg[an[g].xcptr + c + 1];
+              if (dense) {
+                for (int qq = q0; qq < q1; ++qq) {
+                  const uint32_t w = xc[qq];
+                  vv -= A(w & 0xffff) * tcpl[w >> 16];
+                }
+              } else {
+#pragma unroll
+                for (int k = 0; k < XCM; ++k)
+                  if (q0 + k < q1) vv -= E.axc[k] * tcpl[xc[q0 + k] >> 16];
+              }
+            }
+            gst(bt, x_off + c, vv);
+            v[c] = vv;
+          } else if (c < T4) {
+            v[c] = 0.0;
           }
         }
-        if (tid < ndx && i > 0) rhs_keep = acc;
-        else rhs[j] = acc;
-        // forward node 0 of the next iteration prefetched rhs_0 before it was written here
-        if (i == 0) v0fix[tid] = acc;
-        if (tid < ndx) xn[tid] = y[tid];
-      }
-      T(15);
+      };
+      if (fwd_asb) with_A(an[g].nent, Ag, [&](auto A) __attribute__((always_inline)) { fwd_gathers(A, true); });
+      else fwd_gathers([&](int e) __attribute__((always_inline)) { return asb[e]; }, false);
+      wsync();
     }
-    prefetch_late(p + 1);
+    // ---- operands of step q+1 (this step's E and las are consumed), then w_i / x~_i
+    // with the factor block of step q+1 streamed in behind the mat-vec
+    T(2);
+    prefetch_E(kind1, i1, En);
+    prefetch_as(kind1, i1);
+    prefetch_LR(kind1, i1, LRn);
+    prefetch_LC(kind1, i1, LCn);
+    T(3);
+    matvec(SR, i, false, kind == KT0 ? i : i1);
+    T(4);
+    if (bw) {
+      with_A(ne, Ai, [&](auto A) __attribute__((always_inline)) {
+        // ---- z~ = A x~ over balanced row chunks
+        {
+          const uint16_t* rowe = P + an[i].rowe;
+          const uint8_t* rowc = reinterpret_cast<const uint8_t*>(P + an[i].rowc);
+          const uint32_t* rch = reinterpret_cast<const uint32_t*>(P + an[i].rch);
+          const int rchn = an[i].rchn;
+          for (int c0 = 0; c0 < rchn; c0 += 128) {  // two rounds of chunks per batch
+            double acc[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int ch = c0 + lane + 64 * u;
+              const uint32_t cw = rch[min(ch, rchn - 1)];
+              const int q0 = cw & 0xffff, len = ch < rchn ? (int)(cw >> 16) - q0 : 0;
+              double a = 0.0;
+#pragma unroll
+              for (int k = 0; k < PL_CHUNK; ++k) {
+                const int qq = q0 + min(k, max(len - 1, 0));
+                const double t = A(rowe[qq]) * y[rowc[qq]];
+                a += k < len ? t : 0.0;
+              }
+              acc[u] = a;
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+              if (c0 + lane + 64 * u < rchn) part[c0 + lane + 64 * u] = acc[u];
+          }
+        }
+        wsync();
+        T(5);
+        // ---- update_z, update_y (relaxed)
+        {
+          const int nrow = an[i].nrow, ro = an[i].row_off, rcp = an[i].rchptr;
+#pragma unroll
+          for (int mm = 0; mm < MR; ++mm) {
+            const int r = lane + 64 * mm;
+            if (r < nrow) {
+              const int k0 = P[rcp + r], k1 = P[rcp + r + 1];
+              const double zt = range_sum<4>(k0, k1, [&](int k) { return part[k]; });
+              const double zrel = alpha * zt + (1.0 - alpha) * LR.z[mm];
+              double zn = zrel + (1.0 / LR.rho[mm]) * LR.y[mm];
+              zn = fmin(fmax(zn, LR.l[mm]), LR.u[mm]);
+              const double dy = LR.rho[mm] * (zrel - zn);
+              const double yn = LR.y[mm] + dy;
+              gst(za, ro + r, zn);
+              gst(ya, ro + r, yn);
+              if (store_delta) gst(dys, ro + r, dy);
+              trow[r] = LR.rho[mm] * zn - yn;
+            }
+          }
+        }
+        wsync();
+        T(6);
+        // ---- A^T (rho z - y) over column chunks
+        {
+          const uint8_t* colr = reinterpret_cast<const uint8_t*>(P + an[i].colr);
+          const uint32_t* cch = reinterpret_cast<const uint32_t*>(P + an[i].cch);
+          const int cchn = an[i].cchn;
+          for (int c0 = 0; c0 < cchn; c0 += 128) {  // two rounds of chunks per batch
+            double acc[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int ch = c0 + lane + 64 * u;
+              const uint32_t cw = cch[min(ch, cchn - 1)];
+              const int e0 = cw & 0xffff, len = ch < cchn ? (int)(cw >> 16) - e0 : 0;
+              double a = 0.0;
+#pragma unroll
+              for (int k = 0; k < PL_CHUNK; ++k) {
+                const int e = e0 + min(k, max(len - 1, 0));
+                const double t = A(e) * trow[colr[e]];
+                a += k < len ? t : 0.0;
+              }
+              acc[u] = a;
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+              if (c0 + lane + 64 * u < cchn) part[c0 + lane + 64 * u] = acc[u];
+          }
+        }
+      });
+      wsync();
+      T(7);
+      // ---- update_x and the next rhs = sigma x - q + A^T (rho z - y) (stores deferred)
+      {
+        const int ccp0 = an[i].cchptr;
+#pragma unroll
+        for (int mm = 0; mm < MV; ++mm) {
+          const int c = lane + 64 * mm;
+          if (c < nw) {
+            const double xnew = alpha * y[c] + (1.0 - alpha) * LC.x[mm];
+            set2(pxa, mm, xnew);
+            set2(pdx, mm, xnew - LC.x[mm]);
+            double acc = sigma * xnew - LC.q[mm];
+            const int k0 = P[ccp0 + c], k1 = P[ccp0 + c + 1];
+            acc += range_sum<4>(k0, k1, [&](int k) { return part[k]; });
+            if (c < ndx) {  // rows of node i on dx_{i+1} complete rhs_{i+1}
+              const int f0 = P[ccp0 + nw + c], f1 = P[ccp0 + nw + c + 1];
+              const double a2 = range_sum<4>(f0, f1, [&](int k) { return part[k]; });
+              prn = rkeep + a2;
+              if (i == 0) r1[c] = prn;
+            }
+            set2(prh, mm, acc);
+            if (c < ndx && i > 0) rkeep = acc;
+            set2(r0v, mm, acc);
+            if (c < ndx) xn[c] = y[c];
+          }
+        }
+        pnode = i;
+        pkind = kind;
+        psd = store_delta;
+      }
+    } else if (kind == KTN) {
+      // ---- backward N: x~_N = w_N; node N has no rows
+#pragma unroll
+      for (int mm = 0; mm < MV; ++mm) {
+        const int c = lane + 64 * mm;
+        if (c < nw) {
+          const double xnew = alpha * y[c] + (1.0 - alpha) * LC.x[mm];
+          set2(pxa, mm, xnew);
+          set2(pdx, mm, xnew - LC.x[mm]);
+          rkeep = sigma * xnew - LC.q[mm];
+          xn[c] = y[c];
+        }
+      }
+      pnode = i;
+      pkind = kind;
+      psd = store_delta;
+    }
+    T(8);
+    if (kind == KT0) {
+      // ---- forward 0 of the next iteration with the same S_0
+      wsync();
+#pragma unroll
+      for (int mm = 0; mm < MV; ++mm) {
+        const int c = lane + 64 * mm;
+        if (c < nw) {
+          gst(bt, x_off + c, sel2(r0v, mm));
+          v[c] = sel2(r0v, mm);
+        } else if (c < T4) {
+          v[c] = 0.0;
+        }
+      }
+      wsync();
+      matvec(SR, 0, an[0].nunit > KM, i1);
+      fix1 = true;
+    }
+    wsync();
+    T(9);
   };
 
-  if (tid < an[0].nw) v0fix[tid] = rhs[tid];  // rhs_0 (node 0 starts at x_off 0)
-  prefetch_small(0, QA);
-  __builtin_amdgcn_sched_barrier(0);
-  prefetch_S(0);
-  for (int p = 0; p < P; p += 2) {
-    step(std::integral_constant<bool, false>(), p);
-    if (p + 1 < P) step(std::integral_constant<bool, true>(), p + 1);
-  }
-  if (tid == 0) info->iter += niter;
+  prefetch_E(KF0, 0, En);  // operands of step 0 (F0)
+  prefetch_as(KF0, 0);
+  prefetch_LR(KF0, 0, LRn);
+  prefetch_LC(KF0, 0, LCn);
+  load_S(0, 0, SR);
+  for (int q = 0; q < Q; ++q) step(q);
+  flush();
+  if (lane == 0) info->iter += niter;
   if constexpr (TIMING) {
-    if (tid == 0 && d.dbg)
-      for (int k = 0; k < 16; ++k) d.dbg[(size_t)b * 16 + k] += (double)tacc[k];
+    if (lane == 0 && d.dbg)
+      for (int k = 0; k < 10; ++k) d.dbg[(size_t)b * 16 + k] += (double)tacc[k];
   }
 }
 
 namespace {
-template <int ASR, bool TIMING>
-void launch_admm_t(PlOcpHandle* h, int niter, int check, size_t lds, const LdsMap& lm) {
+
+struct AdmmCfg {
+  AdmmLds lm;
+  int ppw;
+  size_t lds;
+};
+
+AdmmCfg admm_config(const PlOcpHandle* h) {
+  AdmmCfg c{};
+  AdmmLds& lm = c.lm;
+  auto up2 = [](int x) { return (x + 1) & ~1; };
+  lm.prog_dbl = up2((h->aprog_len + 3) / 4);
+  const int T = h->ntile_max;
+  int o = 0;
+  lm.v = o;
+  o += up2(4 * T);
+  lm.y = o;
+  o += up2(h->nw_max + h->ndx);
+  lm.xn = o;
+  o += up2(h->ndx);
+  lm.r1 = o;
+  o += up2(h->ndx);
+  // `red` is time-shared: coupling products (gathers) | mat-vec segments and column
+  // partials (mat-vec) | chunk sums and rho z - y (row / column gathers)
+  lm.red = o;
+  lm.tcpl = o;
+  const int segn = (64 + T) * 4;
+  lm.colp = o + segn;
+  lm.trow = o + up2(h->chunk_max);
+  o += up2(std::max(std::max(segn + T * (T - 1) / 2 * 4, up2(h->chunk_max) + h->nrow_max),
+                    std::max(h->ncpl_max, 1)));
+  lm.asb = o;
+  // problems per workgroup: 4 puts one wave on every SIMD of every CU once B >= 4 x 256
+  c.ppw = h->B >= 1024 ? 4 : (h->B >= 512 ? 2 : 1);
+  const int budget = 160 * 1024 / 8;
+  int cap = ((budget - lm.prog_dbl) / c.ppw - o) & ~1;
+  cap = std::max(0, std::min(up2(std::max(h->nent_max, 1)), cap));
+  lm.asb_cap = cap;
+  lm.per_wave = o + cap;
+  c.lds = (size_t)(lm.prog_dbl + c.ppw * lm.per_wave) * sizeof(double);
+  return c;
+}
+
+template <int PPW, int ASR, bool TIMING = false>
+void launch_admm_t(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)k_admm<ASR, TIMING>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    hipFuncSetAttribute((const void*)k_admm<PPW, ASR, TIMING>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((k_admm<ASR, TIMING>), dim3(h->B), dim3(256), lds, h->stream, h->d, h->N, h->n, h->m, h->nnz,
-                     h->ndx, h->S_stride, lm, niter, check, h->set.sigma, h->set.alpha);
+  const int grid = (h->B + PPW - 1) / PPW;
+  hipLaunchKernelGGL((k_admm<PPW, ASR, TIMING>), dim3(grid), dim3(64 * PPW), c.lds, h->stream, h->d, h->B, h->N, h->n, h->m,
+                     h->nnz, h->ndx, h->S_stride, std::max(h->ncpl_max, 1), c.lm, niter, check, h->admm_fwd_asb,
+                     h->set.sigma, h->set.alpha);
 }
+
+template <int ASR>
+void launch_admm_a(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
+  if (c.ppw == 4 && ASR == 16 && h->d.dbg) launch_admm_t<4, 16, true>(h, niter, check, c);
+  else if (c.ppw == 4) launch_admm_t<4, ASR>(h, niter, check, c);
+  else if (c.ppw == 2) launch_admm_t<2, ASR>(h, niter, check, c);
+  else launch_admm_t<1, ASR>(h, niter, check, c);
+}
+
 }  // namespace
 
-static LdsMap admm_lds_map(const PlOcpHandle* h) {
-  return LdsMap{((h->nw_max + h->ndx + 7) / 8) * 8, std::max(h->ncpl_max, 1), std::max(h->nrow_max, 1), h->nunit_max,
-                std::max(h->nent_max, 1), h->admm_dom_len, h->chunk_max};
-}
+int admm_lds_bytes(const PlOcpHandle* h) { return (int)admm_config(h).lds; }
 
-int admm_lds_bytes(const PlOcpHandle* h) { return (int)admm_lds_map(h).total(); }
+int admm_ppw(const PlOcpHandle* h) { return admm_config(h).ppw; }
 
 void launch_admm(PlOcpHandle* h, int niter, int check, int it_base) {
   (void)it_base;
-  const LdsMap lm = admm_lds_map(h);
-  const size_t lds = lm.total();
+  const AdmmCfg c = admm_config(h);
   const bool prof = h->profile && h->prof_n < 64;
   if (prof) hipEventRecord(h->prof_ev[h->prof_n][0], h->stream);
-  if (h->d.dbg && h->admm_asr <= 4) launch_admm_t<4, true>(h, niter, check, lds, lm);
-  else if (h->admm_asr <= 4) launch_admm_t<4, false>(h, niter, check, lds, lm);
-  else if (h->admm_asr <= 6) launch_admm_t<6, false>(h, niter, check, lds, lm);
-  else launch_admm_t<8, false>(h, niter, check, lds, lm);
+  if (h->admm_asr <= 16) launch_admm_a<16>(h, niter, check, c);
+  else launch_admm_a<32>(h, niter, check, c);
   if (prof) {
     hipEventRecord(h->prof_ev[h->prof_n][1], h->stream);
     h->prof_n++;

@@ -90,16 +90,16 @@ __global__ __launch_bounds__(256) void k_factor(PlDev d, int N, int n, int m, in
   for (int i = 0; i <= N; ++i) {
     const int nw = an[i].nw, nrow = an[i].nrow, ncpl = an[i].ncpl, nent = an[i].nent, ncol = an[i].ncol;
     const int ent_off = an[i].ent_off, row_off = an[i].row_off, x_off = an[i].x_off;
-    const int prog = an[i].prog, flen = an[i].flen, p_rowptr = an[i].rowptr, p_cplr = an[i].cplr,
-              p_rowp = an[i].rowp;
-    const int ntile = an[i].ntile, nunit = an[i].nunit, s_off = an[i].s_off;
+    const int prog = an[i].fprog, flen = an[i].flen, p_rowptr = an[i].f_rowptr, p_cplr = an[i].f_cplr,
+              p_rowp = an[i].f_rowp;
+    const int ntile = an[i].ntile, nunit = an[i].nunit, ntl = an[i].ntl, s_off = an[i].s_off;
     __syncthreads();
     T(-1);
     // ---- stage the node's A values, rho and row program
     for (int k = tid; k < nent; k += NT) asb[k] = As[ent_off + k];
     for (int k = tid; k < nrow; k += NT) rwb[k] = rho[row_off + k];
     {
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(d.aprog + prog);
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(d.fprog + prog);
       uint32_t* dst = reinterpret_cast<uint32_t*>(pg);
       for (int k = tid; k < (flen >> 1); k += NT) dst[k] = src[k];
     }
@@ -344,22 +344,24 @@ __global__ __launch_bounds__(256) void k_factor(PlDev d, int N, int n, int m, in
       }
     __syncthreads();
     T(5);
-    // ---- store S_i in the ADMM tile layout: unit u = (lower tile t, half h),
-    // pair kk of unit u at s_off + (kk * nunit + u) * 2 (coalesced over o)
+    // ---- store S_i in the ADMM lane-tile layout (state.h): 4x4 tile t = K l + k of
+    // lane l, pair j at s_off + ((k * 8 + j) * 64 + l) * 2 (coalesced over o)
     {
       double* Sn = Sg + s_off;
-      const int total = nunit * 32;
+      const int total = nunit * 64 * 16;
       for (int o = tid; o < total; o += NT) {
-        const int slot = o & 1, q = o >> 1;
-        const int kk = q / nunit, u = q - kk * nunit;
-        const int t = u >> 1, h = u & 1;
-        int I = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-        while (I * (I + 1) / 2 > t) --I;
-        while ((I + 1) * (I + 2) / 2 <= t) ++I;
-        const int J = t - I * (I + 1) / 2;
-        const int pos = 2 * kk + slot;
-        const int gi = 8 * I + (pos >> 2), gj = 8 * J + 4 * h + (pos & 3);
-        Sn[o] = (gi < nw && gj < nw) ? sym_at(Sl, gi, gj) : 0.0;
+        const int slot = o & 1, l = (o >> 1) & 63, j = (o >> 7) & 7, k = o >> 10;
+        const int t = nunit * l + k;
+        double val = 0.0;
+        if (t < ntl) {
+          int I = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+          while (I * (I + 1) / 2 > t) --I;
+          while ((I + 1) * (I + 2) / 2 <= t) ++I;
+          const int J = t - I * (I + 1) / 2;
+          const int gi = 4 * I + (j >> 1), gj = 4 * J + 2 * (j & 1) + slot;
+          if (gi < nw && gj < nw) val = sym_at(Sl, gi, gj);
+        }
+        Sn[o] = val;
       }
     }
     (void)ntile;

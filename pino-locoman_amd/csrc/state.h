@@ -24,36 +24,54 @@ struct PlNode {
   int colptr_off;  // into colptr (ncol + 1 values, relative to ent_off)
   int rowptr_off;  // into rowptr (nrow + 1 values, relative to the node's CSR list)
   int csr_off;     // into rowent
-  int ntile;       // 8x8 tiles per dimension of the node's KKT block
-  int nunit;       // (lower tile, half) work units = 2 * ntile (ntile + 1) / 2
+  int ntile;       // 4-row tile rows of the node's KKT block: T = ceil(nw / 4)
+  int nunit;       // factor tile slots per lane: K = ceil(T (T + 1) / 2 / 64)
   int s_off;       // offset (doubles) of the node's factor block inside a problem's factor
   int cpl_off;     // coupling rows (rows with a dx_{i+1} entry): offset into cplrow
   int ncpl;
   int pad[2];
 };
 
-// Gather program of one node for the ADMM sweeps (k_admm.hip).  All lists are
-// u16 offsets relative to `prog`; nodes with identical local structure share
-// one program (3-4 programs per OCP).  Pair lists hold (entry, index) as two
-// consecutive u16 (one 32-bit read; their offsets are even):
-//   rows (CSR over the node's rows):             rowptr[nrow+1], rowp[] = (entry, local col)
-//   cols (CSC, entries in storage order):        colptr[ncol+1], colr[] = local row
-//   coupling rows (rows with a dx_{i+1} entry):  cplr[ncpl]
-//     w part of each coupling row:               cwptr[ncpl+1], cwp[] = (entry, col)
-//     dx_{i+1} part of each coupling row:        cxptr[ncpl+1], cxp[] = (entry, col - nw)
+// Per-node tables of the factor and ADMM kernels.  Nodes with identical local
+// structure share their programs (3-4 distinct programs per OCP).
+//
+// Factor program (k_factor.hip), u16 offsets relative to `fprog` in d.fprog:
+//   f_rowptr[nrow+1], f_cplr[ncpl] (coupling rows = rows with a dx_{i+1} entry),
+//   f_rowp[] = (entry, local col) pairs in CSR order; flen = total u16 words.
+// ADMM program (k_admm.hip), u16 offsets relative to `prog` in d.aprog; every
+// distinct program is resident in LDS for the whole sweep kernel.  Pair lists hold
+// (entry, index) as two consecutive u16 (one 32-bit read; their offsets are even):
+//   rows (CSR over the node's rows):             rowe[] = entry (u16), rowc[] = local col (u8)
+//   cols (CSC, entries in storage order):        colr[] = local row of each entry (u8)
+//   w part of each coupling row s:               cwptr[ncpl+1], cwp[] = (entry, col)
+//   dx_{i+1} part of each coupling row:          cxptr[ncpl+1], cxp[] = (entry, col - nw)
 //   per column c < nw, entries in coupling rows: ccptr[nw+1],   ccp[] = (entry, coupling index)
 //   per dx_{i+1} column c < ndx:                 xcptr[ndx+1],  xcp[] = (entry, coupling index)
-//   row chunks (<= PL_CHUNK entries of one row): rchn chunks rch[] = (q0, q1) into rowp,
+//   row chunks (<= PL_CHUNK entries of one row): rchn chunks rch[] = (q0, q1) into rowe/rowc,
 //                                                rchptr[nrow+1] = first chunk of each row
 //   column chunks (<= PL_CHUNK entries):         cchn chunks cch[] = (e0, e1), cchptr[ncol+1]
+//
+// Factor layout (k_factor writes, k_admm streams): the lower triangle of S_i in
+// 4x4 tiles (I, J), J <= I < T, packed row-major t = I (I + 1) / 2 + J (diagonal
+// tiles stored full).  Tile t belongs to lane l = t / K, slot k = t % K; its 16
+// elements are 8 double2 (row r, cols 2h, 2h + 1 -> pair j = 2 r + h) stored at
+// s_off + ((k * 8 + j) * 64 + l) * 2, so each 16-byte load of a wave is 1 KiB contiguous.
 #define PL_CHUNK 6
+// ADMM sweep kernel limits (one wave per problem, k_admm.hip)
+#define PL_ADMM_KM 4        // factor tile slots per lane held in registers (more: extra passes)
+#define PL_ADMM_CWM 4       // w entries per coupling row
+#define PL_ADMM_XCM 2       // coupling entries per dx_{i+1} column
+#define PL_ADMM_MV 2        // columns per lane: nw <= 128
+#define PL_ADMM_MR 3        // rows per lane: nrow <= 192
+#define PL_ADMM_ASR_MAX 32  // A values per lane staged through registers (entries past 64 x ASR: global)
 struct PlAdmmNode {
-  int nw, nrow, ncol, ncpl, nent, nunit, ntile;
+  int nw, nrow, ncol, ncpl, nent, nunit, ntile, ntl;  // nunit = K slots, ntile = T, ntl = tiles
+  unsigned kmagic;  // ceil(2^32 / K): t / K == umulhi(t, kmagic) for the tile counts used
   int x_off, row_off, ent_off, s_off;
   int prog, prog_len;
-  int rowptr, rowp, colptr, colr, cplr, cwptr, cwp, cxptr, cxp, ccptr, ccp, xcptr, xcp;
+  int rowe, rowc, colr, cwptr, cwp, cxptr, cxp, ccptr, ccp, xcptr, xcp;
   int rchn, rch, rchptr, cchn, cch, cchptr;
-  int flen;        // u16 words of the prefix [rowptr, cplr, rowp] the factor kernel stages
+  int fprog, flen, f_rowptr, f_cplr, f_rowp;
 };
 
 struct PlSettings {
@@ -90,8 +108,9 @@ struct PlDev {
   int* cplrow;       // coupling rows (local row ids)
   int* rownode;      // global row -> node
   int* colnode;      // global column -> node
-  PlAdmmNode* anodes;    // N + 1 ADMM gather programs
-  uint16_t* aprog;
+  PlAdmmNode* anodes;    // N + 1 node tables (ADMM and factor programs)
+  uint16_t* aprog;       // distinct ADMM programs, concatenated
+  uint16_t* fprog;       // distinct factor programs, concatenated
   // per problem [B][*]
   double* p;         // params
   double* x;         // SQP iterate (decision vector)
@@ -135,12 +154,14 @@ struct PlOcpHandle {
   hipStream_t stream;
   int B;
   int N, n, m, np, nnz, nx, ndx, nw_max, ncol_max, nrow_max, S_stride;
-  int nunit_max;
+  int nunit_max;                    // max factor tile slots per lane (K)
+  int ntile_max;                    // max 4-row tile rows (T)
   int ncpl_max, nent_max;
   int chunk_max;                    // max(rchn, cchn) over nodes (ADMM partial-sum buffer)
-  int flen_max;                     // longest factor program prefix (u16)
-  int admm_dom_prog, admm_dom_len;  // most frequent ADMM gather program (kept in LDS)
-  int admm_asr;                     // A values per thread staged through registers
+  int flen_max;                     // longest factor program (u16)
+  int aprog_len;                    // all ADMM programs (u16), resident in LDS
+  int admm_asr;                     // A values per lane staged through registers (x 64 lanes)
+  int admm_fwd_asb;                 // coupling rows too dense for registers: forward steps stage A in LDS
   PlSettings set;
   PlModel model;
   PlOcpConst oc;

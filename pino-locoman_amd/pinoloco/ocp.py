@@ -284,7 +284,7 @@ class BatchedOCP:
     def sizes(self):
         out = (C.c_longlong * 10)()
         _lib.check(_lib.lib().pl_ocp_sizes(self.h, out))
-        return dict(zip(("n", "m", "nnz", "S_stride", "nw_max", "N", "admm_prog", "admm_prog_lds", "admm_lds_bytes",
+        return dict(zip(("n", "m", "nnz", "S_stride", "nw_max", "N", "admm_prog", "admm_ppw", "admm_lds_bytes",
                          "admm_asr"), [int(v) for v in out]))
 
     def close(self):

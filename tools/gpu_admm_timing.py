@@ -30,15 +30,14 @@ print("solve s", time.time() - t, "phase_ms", st["phase_ms"], "iters", np.bincou
 ALL = bo.debug("admm_t", B * 32)
 T = ALL[:B * 16].reshape(B, 16)
 it = st["admm_iters"].astype(float)
-steps = it * (N + 1)  # per direction
-names = ["f:bar0", "f:stageA", "f:gather+bar", "f:mv+bar", "f:issue", "f:reduce", "-", "-",
-         "b:bar0", "b:stageA", "b:gather+bar", "b:mv+bar", "b:issue", "b:reduce+bar", "b:rows+bar", "b:cols"]
-per = T / steps[:, None]
+steps = it * (2 * N)  # one factor block per step
+names = ["start(wait+stage)", "flush stores", "gathers+v", "prefetch issue", "matvec", "rows gather",
+         "z update", "cols gather", "x update", "T0 + end"]
+per = T[:, :10] / steps[:, None]
 for k, nm in enumerate(names):
-    if nm != "-":
-        print(f"{nm:14s} mean cycles/step {per[:, k].mean():9.1f}  p10 {np.percentile(per[:, k], 10):9.1f}  "
-              f"p90 {np.percentile(per[:, k], 90):9.1f}")
-print("total cycles/step fwd", per[:, :6].sum(1).mean(), "bwd", per[:, 8:].sum(1).mean())
+    print(f"{nm:18s} mean cycles/step {per[:, k].mean():9.1f}  p10 {np.percentile(per[:, k], 10):9.1f}  "
+          f"p90 {np.percentile(per[:, k], 90):9.1f}")
+print("total cycles/step", per.sum(1).mean())
 F = ALL[B * 16:].reshape(B, 16)[:, :9] / (N + 1)
 fn = ["stage", "Kc+D", "init", "assemble", "GJ", "symm", "store", "U", "C"]
 for k, nm in enumerate(fn):
