@@ -42,6 +42,7 @@ struct pl_ocp {
   std::vector<int> colptr, rowidx, entcol, rowptr, rowent, cplrow, rownode, colnode;
   std::vector<PlAdmmNode> anodes;
   std::vector<uint16_t> aprog, fprog;
+  std::vector<uint32_t> ttab;
   std::vector<double> h_params;  // host copy of the parameters (B x np)
   std::vector<void*> allocs;
   hipEvent_t ev[5];
@@ -516,6 +517,39 @@ int build_admm_prog(pl_ocp* o) {
     h.ncpl_max = std::max(h.ncpl_max, nd.ncpl);
     h.nent_max = std::max(h.nent_max, nd.nent);
   }
+  // lane-tile tables of the ADMM mat-vec: slot k of lane l holds 4x4 tile t = K l + k,
+  // (I, J) its tile row / column and cidx its column-major off-diagonal index
+  o->ttab.clear();
+  {
+    std::vector<std::pair<int, int>> keys;
+    std::vector<int> offs;
+    for (int i = 0; i <= N; ++i) {
+      PlAdmmNode& a = o->anodes[i];
+      const int T = a.ntile, K = a.nunit;
+      if (K > PL_ADMM_KM) { a.ttab = -1; continue; }
+      size_t k = 0;
+      while (k < keys.size() && keys[k] != std::make_pair(T, K)) ++k;
+      if (k == keys.size()) {
+        keys.push_back({T, K});
+        offs.push_back((int)o->ttab.size());
+        for (int l = 0; l < 64; ++l)
+          for (int s = 0; s < PL_ADMM_KM; ++s) {
+            const int t = K * l + s;
+            uint32_t w = 0xff000000u;  // invalid slot
+            if (s < K && t < a.ntl) {
+              int I = 0;
+              while ((I + 1) * (I + 2) / 2 <= t) ++I;
+              const int J = t - I * (I + 1) / 2;
+              const int cidx = I > J ? (J * (2 * T - J - 1)) / 2 + I - J - 1 : 0;
+              w = ((uint32_t)I << 24) | ((uint32_t)J << 16) | (uint32_t)cidx;
+            }
+            o->ttab.push_back(w);
+          }
+      }
+      a.ttab = offs[k];
+    }
+    if (o->ttab.empty()) o->ttab.assign(64 * PL_ADMM_KM, 0xff000000u);
+  }
   h.aprog_len = (int)o->aprog.size();
   {  // A values staged through registers: enough for the most frequent node program
     std::vector<int> cnt;
@@ -698,6 +732,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= upload(o, &D.anodes, o->anodes);
   rc |= upload(o, &D.aprog, o->aprog);
   rc |= upload(o, &D.fprog, o->fprog);
+  rc |= upload(o, &D.ttab, o->ttab);
   const size_t n = h.n, m = h.m, nnz = h.nnz;
   rc |= dalloc(o, &D.p, B * h.np);
   rc |= dalloc(o, &D.x, B * n);

@@ -98,6 +98,21 @@ __device__ __forceinline__ void wsync() {
 
 // sum_{k0 <= k < k1} f(k), 8 clamped independent reads per round (branch-free within a
 // round, so the LDS reads of a round issue back to back)
+// sum_{k0 <= k < k1} p[k * stride], U reads per round; reads past k1 go to a zero slot
+// (an index select instead of a select on the double)
+template <int U = 8>
+__device__ __forceinline__ double lds_sum(const double* p, int k0, int k1, int stride, const double* zero) {
+  double acc = 0.0;
+  for (int b = k0; b < k1; b += U) {
+    double t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[u] = *(b + u < k1 ? p + (b + u) * stride : zero);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += t[u];
+  }
+  return acc;
+}
+
 template <int U = 8, class F>
 __device__ __forceinline__ double range_sum(int k0, int k1, F f) {
   double acc = 0.0;
@@ -140,6 +155,7 @@ struct Early {
   double axc[XCM];  // forward: A of the coupling entries of dx_i column `lane`
   double rhoc;      // rho of coupling row `lane` (node i-1 forward, node i backward)
   double vv[MV];    // forward: rhs_i, backward: bt_i (columns lane, lane + 64)
+  uint4 tt;         // lane-tile table words of the step's factor block (k_factor layout)
 };
 struct LateR {  // backward rows of node i (lane, lane + 64, lane + 128)
   double z[MR], y[MR], rho[MR], l[MR], u[MR];
@@ -152,7 +168,7 @@ struct LateC {  // backward columns of node i
 struct AdmmLds {
   int prog_dbl;  // all ADMM programs (u16), rounded to 16 bytes, in doubles
   int per_wave;
-  int v, y, xn, r1, tcpl, trow, red, colp, asb, asb_cap;
+  int v, y, xn, r1, tcpl, trow, red, colp, zero, asb, asb_cap;
 };
 
 }  // namespace
@@ -195,6 +211,8 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   double* colp = W + lm.colp;  // mat-vec column partials, off-diagonal tiles in column-major order
   double* part = W + lm.red;   // chunk sums of the row / column gathers (after the mat-vec)
   double* asb = W + lm.asb;    // A values of the backward node
+  double* zslot = W + lm.zero; // a 0.0 read by the clamped reductions
+  if (lane == 0) *zslot = 0.0;
 
   const double* __restrict__ As = d.As + (size_t)b * nnz;
   const double* __restrict__ rho = d.rho + (size_t)b * m;
@@ -228,11 +246,6 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   double rkeep = 0.0;           // rhs of node i (dx part, lane < ndx) completed at node i-1
   double2 r0v = make_double2(0.0, 0.0);  // rhs_0 of the backward-0 half of T0 (columns lane, lane + 64)
   bool fix1 = false;
-  // deferred end-of-step stores (x update and rhs of a backward / TN step)
-  double2 pxa = make_double2(0.0, 0.0), pdx = pxa, prh = pxa;
-  double prn = 0.0;
-  int pnode = -1, pkind = KF0;
-  bool psd = false;
 
   // ---------------- loads (unconditional and clamped: exact vmcnt accounting)
   auto load_S = [&](int i, int kbase, Sbuf& R) __attribute__((always_inline)) {
@@ -272,6 +285,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
       }
     }
     E.rhoc = gld(rhoc, g * cpl_stride + s);
+    E.tt = gld(reinterpret_cast<const uint4*>(d.ttab), max(an[i1].ttab, 0) / 4 + lane);
     const double* src = (kind1 == KF0 || fw) ? rhs : bt;
     const int xo = an[i1].x_off, nw1 = an[i1].nw;
 #pragma unroll
@@ -313,7 +327,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   // ---------------- y[0..nw) = S_i v  (R holds slots 0..KM-1 unless reload).  Slot k
   // of node next's block is loaded into R as soon as the last pass has consumed slot
   // k (the software pipeline of the factor stream; next = i re-reads the block).
-  auto matvec = [&](Sbuf& R, int i, bool reload, int next) __attribute__((always_inline)) {
+  auto matvec = [&](Sbuf& R, int i, bool reload, int next, uint4 tt) __attribute__((always_inline)) {
     const int K = an[i].nunit, T = an[i].ntile, ntl = an[i].ntl, nw = an[i].nw;
     const int Kn = an[next].nunit;
     const double2* pn = reinterpret_cast<const double2*>(Sg + an[next].s_off);
@@ -321,14 +335,26 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     const double2* v2 = reinterpret_cast<const double2*>(v);
     int curI = -1;
     double sa[4] = {0.0, 0.0, 0.0, 0.0};
+    bool use_tt = false;
     auto pass = [&](int kb, bool last_pass) __attribute__((always_inline)) {
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
         const int kk = kb + k;
         const int t = K * lane + kk;
-        if (kk < K && t < ntl) {
-          int I, J;
+        int I, J, cidx;
+        bool valid;
+        if (use_tt) {  // precomputed (uniform choice)
+          const uint32_t w = k == 0 ? tt.x : (k == 1 ? tt.y : (k == 2 ? tt.z : tt.w));
+          I = (int)(w >> 24);
+          J = (int)((w >> 16) & 0xff);
+          cidx = (int)(w & 0xffff);
+          valid = I != 0xff;
+        } else {
+          valid = kk < K && t < ntl;
           tile_ij(t, I, J);
+          cidx = (J * (2 * T - J - 1)) / 2 + I - J - 1;
+        }
+        if (valid) {
           const double2 a0 = v2[2 * J], a1 = v2[2 * J + 1];
           double rp[4];
 #pragma unroll
@@ -348,7 +374,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
             }
             // column-major packed off-diagonal index: the partials of one output tile
             // column are contiguous
-            double2* cpp = reinterpret_cast<double2*>(colp + ((J * (2 * T - J - 1)) / 2 + I - J - 1) * 4);
+            double2* cpp = reinterpret_cast<double2*>(colp + cidx * 4);
             cpp[0] = make_double2(cp[0], cp[1]);
             cpp[1] = make_double2(cp[2], cp[3]);
           }
@@ -374,6 +400,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
       }
     };
     if (K <= KM && !reload) {
+      use_tt = true;
       pass(0, true);  // the common case, straight-line: the refill loads never force a wait
     } else {
       for (int kb = 0; kb < K; kb += KM) {
@@ -394,38 +421,28 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
         const int I = o >> 2, r = o & 3;
         const int t0 = I * (I + 1) / 2;
         const int lf = div_k(t0, K, km), ll = div_k(t0 + I, K, km);
-        const double rs = range_sum(lf, ll + 1, [&](int lp) { return seg[(lp + I) * 4 + r]; });
+        const double rs = lds_sum(seg + I * 4 + r, lf, ll + 1, 4, zslot);
         const int cb = (I * (2 * T - I - 1)) / 2;
-        const double cs = range_sum(cb, cb + T - 1 - I, [&](int c) { return colp[c * 4 + r]; });
+        const double cs = lds_sum(colp + r, cb, cb + T - 1 - I, 4, zslot);
         y[o] = rs + cs;
       }
     }
     wsync();
   };
 
-  // ---------------- deferred stores of the previous step
-  auto flush = [&]() __attribute__((always_inline)) {
-    if (pnode < 0) return;
-    const int ip = pnode, nwp = an[ip].nw, xo = an[ip].x_off;
-    const bool pb = bwd_kind(pkind);
-    const int xnx = pb ? an[ip + 1].x_off : 0;
-#pragma unroll
-    for (int mm = 0; mm < MV; ++mm) {
-      const int c = lane + 64 * mm;
-      if (c < nwp) {
-        gst(xa, xo + c, sel2(pxa, mm));
-        if (psd) gst(dxs, xo + c, sel2(pdx, mm));
-        if (pb) {
-          if (c < ndx) gst(rhs, xnx + c, prn);
-          if (!(c < ndx && ip > 0)) gst(rhs, xo + c, sel2(prh, mm));
-        }
-      }
-    }
-    pnode = -1;
-  };
-
   // ---------------- one step of the schedule
   auto step = [&](int q) __attribute__((always_inline)) {
+    // Every store of a step is issued at its end: on CDNA4 a store's source VGPRs may be
+    // reused only after its vmcnt retires, so a mid-step store followed by register
+    // reuse would wait vmcnt(0) and drain the factor stream.  At the end the reuse
+    // happens after the next step's own vmcnt(0).
+    double kz[MR], ky[MR], kd[MR], kb[MV];
+#pragma unroll
+    for (int mm = 0; mm < MR; ++mm) kz[mm] = ky[mm] = kd[mm] = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < MV; ++mm) kb[mm] = 0.0;
+    double2 pxa = make_double2(0.0, 0.0), pdx = pxa, prh = pxa;
+    double prn = 0.0;
     int i, it;
     const int kind = step_kind(q, N, niter, i, it);
     const bool has_next = q + 1 < Q;
@@ -471,7 +488,6 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     if (bw) stage(ne, Ai);
     else if (fwd_asb && kind != KF0) stage(an[i - 1].nent, As + an[i - 1].ent_off);
     T(0);
-    flush();
     T(1);
     if (bw) {
       with_A(ne, Ai, [&](auto A) __attribute__((always_inline)) {
@@ -510,7 +526,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
       for (int mm = 0; mm < MV; ++mm) {
         const int c = lane + 64 * mm;
         if (c < nw) {
-          gst(bt, x_off + c, E.vv[mm]);
+          kb[mm] = E.vv[mm];
           v[c] = E.vv[mm];
         } else if (c < T4) {
           v[c] = 0.0;
@@ -561,7 +577,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
                   if (q0 + k < q1) vv -= E.axc[k] * tcpl[xc[q0 + k] >> 16];
               }
             }
-            gst(bt, x_off + c, vv);
+            kb[mm] = vv;
             v[c] = vv;
           } else if (c < T4) {
             v[c] = 0.0;
@@ -577,11 +593,13 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     T(2);
     prefetch_E(kind1, i1, En);
     prefetch_as(kind1, i1);
-    prefetch_LR(kind1, i1, LRn);
-    prefetch_LC(kind1, i1, LCn);
     T(3);
-    matvec(SR, i, false, kind == KT0 ? i : i1);
+    matvec(SR, i, false, kind == KT0 ? i : i1, E.tt);
     T(4);
+    if (!bw) {
+      prefetch_LR(kind1, i1, LRn);
+      prefetch_LC(kind1, i1, LCn);
+    }
     if (bw) {
       with_A(ne, Ai, [&](auto A) __attribute__((always_inline)) {
         // ---- z~ = A x~ over balanced row chunks
@@ -613,6 +631,9 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
         }
         wsync();
         T(5);
+        // row / column operands of step q+1 (behind the factor stream, inside the vmcnt window)
+        prefetch_LR(kind1, i1, LRn);
+        prefetch_LC(kind1, i1, LCn);
         // ---- update_z, update_y (relaxed)
         {
           const int nrow = an[i].nrow, ro = an[i].row_off, rcp = an[i].rchptr;
@@ -621,16 +642,16 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
             const int r = lane + 64 * mm;
             if (r < nrow) {
               const int k0 = P[rcp + r], k1 = P[rcp + r + 1];
-              const double zt = range_sum<4>(k0, k1, [&](int k) { return part[k]; });
+              const double zt = lds_sum<4>(part, k0, k1, 1, zslot);
               const double zrel = alpha * zt + (1.0 - alpha) * LR.z[mm];
               double zn = zrel + (1.0 / LR.rho[mm]) * LR.y[mm];
               zn = fmin(fmax(zn, LR.l[mm]), LR.u[mm]);
               const double dy = LR.rho[mm] * (zrel - zn);
               const double yn = LR.y[mm] + dy;
-              gst(za, ro + r, zn);
-              gst(ya, ro + r, yn);
-              if (store_delta) gst(dys, ro + r, dy);
               trow[r] = LR.rho[mm] * zn - yn;
+              kz[mm] = zn;
+              ky[mm] = yn;
+              kd[mm] = dy;
             }
           }
         }
@@ -677,10 +698,10 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
             set2(pdx, mm, xnew - LC.x[mm]);
             double acc = sigma * xnew - LC.q[mm];
             const int k0 = P[ccp0 + c], k1 = P[ccp0 + c + 1];
-            acc += range_sum<4>(k0, k1, [&](int k) { return part[k]; });
+            acc += lds_sum<4>(part, k0, k1, 1, zslot);
             if (c < ndx) {  // rows of node i on dx_{i+1} complete rhs_{i+1}
               const int f0 = P[ccp0 + nw + c], f1 = P[ccp0 + nw + c + 1];
-              const double a2 = range_sum<4>(f0, f1, [&](int k) { return part[k]; });
+              const double a2 = lds_sum<4>(part, f0, f1, 1, zslot);
               prn = rkeep + a2;
               if (i == 0) r1[c] = prn;
             }
@@ -690,9 +711,6 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
             if (c < ndx) xn[c] = y[c];
           }
         }
-        pnode = i;
-        pkind = kind;
-        psd = store_delta;
       }
     } else if (kind == KTN) {
       // ---- backward N: x~_N = w_N; node N has no rows
@@ -707,9 +725,6 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
           xn[c] = y[c];
         }
       }
-      pnode = i;
-      pkind = kind;
-      psd = store_delta;
     }
     T(8);
     if (kind == KT0) {
@@ -719,17 +734,50 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
       for (int mm = 0; mm < MV; ++mm) {
         const int c = lane + 64 * mm;
         if (c < nw) {
-          gst(bt, x_off + c, sel2(r0v, mm));
+          kb[mm] = sel2(r0v, mm);
           v[c] = sel2(r0v, mm);
         } else if (c < T4) {
           v[c] = 0.0;
         }
       }
       wsync();
-      matvec(SR, 0, an[0].nunit > KM, i1);
+      matvec(SR, 0, an[0].nunit > KM, i1, E.tt);
       fix1 = true;
     }
     wsync();
+    // ---- the step's stores
+    if (!bw || kind == KT0) {  // bt_i of a forward (part of a) step
+#pragma unroll
+      for (int mm = 0; mm < MV; ++mm)
+        if (lane + 64 * mm < nw) gst(bt, x_off + lane + 64 * mm, kb[mm]);
+    }
+    if (bw) {  // rows of node i
+      const int nrow = an[i].nrow, ro = an[i].row_off;
+#pragma unroll
+      for (int mm = 0; mm < MR; ++mm) {
+        const int r = lane + 64 * mm;
+        if (r < nrow) {
+          gst(za, ro + r, kz[mm]);
+          gst(ya, ro + r, ky[mm]);
+          if (store_delta) gst(dys, ro + r, kd[mm]);
+        }
+      }
+    }
+    if (bw || kind == KTN) {  // x update and rhs of node i
+      const int xnx = bw ? an[i + 1].x_off : 0;
+#pragma unroll
+      for (int mm = 0; mm < MV; ++mm) {
+        const int c = lane + 64 * mm;
+        if (c < nw) {
+          gst(xa, x_off + c, sel2(pxa, mm));
+          if (store_delta) gst(dxs, x_off + c, sel2(pdx, mm));
+          if (bw) {
+            if (c < ndx) gst(rhs, xnx + c, prn);
+            if (!(c < ndx && i > 0)) gst(rhs, x_off + c, sel2(prh, mm));
+          }
+        }
+      }
+    }
     T(9);
   };
 
@@ -739,7 +787,6 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   prefetch_LC(KF0, 0, LCn);
   load_S(0, 0, SR);
   for (int q = 0; q < Q; ++q) step(q);
-  flush();
   if (lane == 0) info->iter += niter;
   if constexpr (TIMING) {
     if (lane == 0 && d.dbg)
@@ -768,6 +815,8 @@ AdmmCfg admm_config(const PlOcpHandle* h) {
   o += up2(h->nw_max + h->ndx);
   lm.xn = o;
   o += up2(h->ndx);
+  lm.zero = o;
+  o += 2;
   lm.r1 = o;
   o += up2(h->ndx);
   // `red` is time-shared: coupling products (gathers) | mat-vec segments and column

@@ -59,8 +59,8 @@ struct PlNode {
 #define PL_CHUNK 6
 // ADMM sweep kernel limits (one wave per problem, k_admm.hip)
 #define PL_ADMM_KM 4        // factor tile slots per lane held in registers (more: extra passes)
-#define PL_ADMM_CWM 4       // w entries per coupling row
-#define PL_ADMM_XCM 2       // coupling entries per dx_{i+1} column
+#define PL_ADMM_CWM 2       // w entries per coupling row held in registers (more: LDS path)
+#define PL_ADMM_XCM 1       // coupling entries per dx_{i+1} column held in registers
 #define PL_ADMM_MV 2        // columns per lane: nw <= 128
 #define PL_ADMM_MR 3        // rows per lane: nrow <= 192
 #define PL_ADMM_ASR_MAX 32  // A values per lane staged through registers (entries past 64 x ASR: global)
@@ -72,6 +72,7 @@ struct PlAdmmNode {
   int rowe, rowc, colr, cwptr, cwp, cxptr, cxp, ccptr, ccp, xcptr, xcp;
   int rchn, rch, rchptr, cchn, cch, cchptr;
   int fprog, flen, f_rowptr, f_cplr, f_rowp;
+  int ttab;  // offset (u32) of the node's lane-tile table in d.ttab (-1: more than PL_ADMM_KM slots)
 };
 
 struct PlSettings {
@@ -111,6 +112,7 @@ struct PlDev {
   PlAdmmNode* anodes;    // N + 1 node tables (ADMM and factor programs)
   uint16_t* aprog;       // distinct ADMM programs, concatenated
   uint16_t* fprog;       // distinct factor programs, concatenated
+  uint32_t* ttab;        // lane-tile tables [64][PL_ADMM_KM] per distinct (T, K): (I << 24) | (J << 16) | cidx
   // per problem [B][*]
   double* p;         // params
   double* x;         // SQP iterate (decision vector)
