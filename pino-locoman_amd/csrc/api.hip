@@ -420,6 +420,42 @@ int build_admm_prog(pl_ocp* o) {
     for (int s = 0; s < nd.ncpl; ++s) P.push_back((uint16_t)cpl[s]);
     mark2(a.f_rowp);
     for (int q = 0; nd.nrow && q < rp[nd.nrow]; ++q) pair(re[q], ecol[re[q]]);
+    {  // coupling lists: w part / dx_{i+1} part of each coupling row, coupling rows of each dx_{i+1} column
+      std::vector<int> cpl_idx(nd.nrow, -1);
+      for (int s = 0; s < nd.ncpl; ++s) cpl_idx[cpl[s]] = s;
+      std::vector<int> wp{0}, xp{0};
+      std::vector<std::pair<int, int>> wl, xl;
+      for (int s = 0; s < nd.ncpl; ++s) {
+        const int r = cpl[s];
+        for (int q = rp[r]; q < rp[r + 1]; ++q) {
+          const int e = re[q], c = ecol[e];
+          if (c < nd.nw) wl.push_back({e, c});
+          else xl.push_back({e, c - nd.nw});
+        }
+        wp.push_back((int)wl.size());
+        xp.push_back((int)xl.size());
+      }
+      std::vector<int> cp2{0};
+      std::vector<std::pair<int, int>> cl;
+      for (int c = 0; c < ndx && nd.ncol; ++c) {
+        for (int e = cp[nd.nw + c]; e < cp[nd.nw + c + 1]; ++e)
+          if (cpl_idx[rid[e]] >= 0) cl.push_back({e, cpl_idx[rid[e]]});
+        cp2.push_back((int)cl.size());
+      }
+      if (!nd.ncol) cp2.assign(ndx + 1, 0);
+      mark(a.f_cwptr);
+      for (int x : wp) P.push_back((uint16_t)x);
+      mark2(a.f_cwp);
+      for (auto& pr : wl) pair(pr.first, pr.second);
+      mark(a.f_xcptr);
+      for (int x : cp2) P.push_back((uint16_t)x);
+      mark2(a.f_xcp);
+      for (auto& pr : cl) pair(pr.first, pr.second);
+      mark(a.f_cxptr);
+      for (int x : xp) P.push_back((uint16_t)x);
+      mark2(a.f_cxp);
+      for (auto& pr : xl) pair(pr.first, pr.second);
+    }
     a.fprog = intern(fprogs, foff, o->fprog, P);
     a.flen = (int)P.size();
     h.flen_max = std::max(h.flen_max, a.flen);

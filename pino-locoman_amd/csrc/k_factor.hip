@@ -123,47 +123,6 @@ __global__ __launch_bounds__(256) void k_factor(PlDev d, int N, int n, int m, in
     };
 
     T(0);
-    // ---- Kc_i and D_{i+1} from the coupling rows of node i (chunk width ncol)
-    double D[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
-    if (i < N) {
-      // thread (ty, tx) owns Kc[3ty..3ty+2][7tx..7tx+6] and D[3ty..][3tx..]
-      double KcR[3][FB];
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = 0; c < FB; ++c) KcR[r][c] = 0.0;
-      for (int r0 = 0; r0 < ncpl; r0 += FCH) {
-        const int nr = min(FCH, ncpl - r0);
-        fill(r0, nr, true, 0, ncol);
-        if (3 * ty < ndx) {
-          for (int s = 0; s < nr; ++s) {
-            const double* a = Sl + s * ncol;
-            double xa[3], wc[FB], xb[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-              xa[k] = (3 * ty + k < ndx) ? rw[s] * a[nw + 3 * ty + k] : 0.0;
-              xb[k] = (3 * tx + k < ndx) ? a[nw + 3 * tx + k] : 0.0;
-            }
-#pragma unroll
-            for (int c = 0; c < FB; ++c) wc[c] = (FB * tx + c < nw) ? a[FB * tx + c] : 0.0;
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-#pragma unroll
-              for (int c = 0; c < FB; ++c) KcR[r][c] += xa[r] * wc[c];
-#pragma unroll
-              for (int c = 0; c < 3; ++c) D[r][c] += xa[r] * xb[c];
-            }
-          }
-        }
-      }
-      if (3 * ty < ndx && FB * tx < nw) {
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int c = 0; c < FB; ++c)
-            if (3 * ty + r < ndx && FB * tx + c < nw) Kc[(3 * ty + r) * nw + FB * tx + c] = KcR[r][c];
-      }
-    }
     __syncthreads();
     T(1);
     // ---- Kt_ii: diagonal (identity on the padding), E_i on the dx block
@@ -179,12 +138,26 @@ __global__ __launch_bounds__(256) void k_factor(PlDev d, int N, int n, int m, in
         Kr[rr][cc] = v;
       }
     __syncthreads();  // E_i consumed: the buffer now carries D_{i+1}
-    if (i < N && ty * 3 < ndx && tx * 3 < ndx) {
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-          if (3 * ty + r < ndx && 3 * tx + c < ndx) Cb[(3 * ty + r) * ndx + 3 * tx + c] = D[r][c];
+    // coupling lists (state.h): rho_s A of the coupling rows of node i
+    const uint32_t* f_cw = reinterpret_cast<const uint32_t*>(pg + an[i].f_cwp);
+    const uint32_t* f_xc = reinterpret_cast<const uint32_t*>(pg + an[i].f_xcp);
+    const uint32_t* f_cx = reinterpret_cast<const uint32_t*>(pg + an[i].f_cxp);
+    const int p_cwptr = an[i].f_cwptr, p_xcptr = an[i].f_xcptr, p_cxptr = an[i].f_cxptr;
+    if (i < N) {
+      // D_{i+1}[a][b] = sum_s rho_s x_{s,a} x_{s,b} over the coupling rows s with an entry in column a
+      for (int k = tid; k < ndx * ndx; k += NT) {
+        const int ra = k / ndx, cb = k - ra * ndx;
+        double acc = 0.0;
+        for (int q = pg[p_xcptr + ra]; q < pg[p_xcptr + ra + 1]; ++q) {
+          const uint32_t w = f_xc[q];
+          const int sidx = (int)(w >> 16);
+          for (int q2 = pg[p_cxptr + sidx]; q2 < pg[p_cxptr + sidx + 1]; ++q2) {
+            const uint32_t w2 = f_cx[q2];
+            if ((int)(w2 >> 16) == cb) acc += rwb[pg[p_cplr + sidx]] * asb[w & 0xffff] * asb[w2 & 0xffff];
+          }
+        }
+        Cb[k] = acc;
+      }
     }
     T(2);
     // ---- rows of node i on the w_i columns
@@ -367,59 +340,40 @@ __global__ __launch_bounds__(256) void k_factor(PlDev d, int N, int n, int m, in
     (void)ntile;
     T(6);
     if (i == N) break;
-    // ---- U = Kc S (ndx x nw) in 3 x 7 register blocks
-    double U[3][FB];
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int c = 0; c < FB; ++c) U[r][c] = 0.0;
-    const bool uown = 3 * ty < ndx && FB * tx < nw;
-    if (uown) {
-      for (int k = 0; k < nw; ++k) {
-        double ka[3], sk[FB];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) ka[r] = (3 * ty + r < ndx) ? Kc[(3 * ty + r) * nw + k] : 0.0;
-#pragma unroll
-        for (int c = 0; c < FB; ++c) sk[c] = (FB * tx + c < nw) ? sym_at(Sl, k, FB * tx + c) : 0.0;
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int c = 0; c < FB; ++c) U[r][c] += ka[r] * sk[c];
+    // ---- U = Kc S (ndx x nw), Kc = sum_s rho_s x_s w_s^T from the coupling lists:
+    // U[a][j] = sum_{(e, s) in xc(a)} rho_s A_e sum_{(e', p) in cw(s)} A_e' S[p][j]
+    for (int k = tid; k < ndx * nw; k += NT) {
+      const int ra = k / nw, j = k - ra * nw;
+      double acc = 0.0;
+      for (int q = pg[p_xcptr + ra]; q < pg[p_xcptr + ra + 1]; ++q) {
+        const uint32_t w = f_xc[q];
+        const int sidx = (int)(w >> 16);
+        double t = 0.0;
+        for (int q2 = pg[p_cwptr + sidx]; q2 < pg[p_cwptr + sidx + 1]; ++q2) {
+          const uint32_t w2 = f_cw[q2];
+          t += asb[w2 & 0xffff] * sym_at(Sl, (int)(w2 >> 16), j);
+        }
+        acc += rwb[pg[p_cplr + sidx]] * asb[w & 0xffff] * t;
       }
+      Kc[k] = acc;  // the (now unused) Kc buffer holds U
     }
     T(7);
-    __syncthreads();  // S consumed: U replaces it
-    if (uown) {
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = 0; c < FB; ++c)
-          if (3 * ty + r < ndx && FB * tx + c < nw) Sl[(3 * ty + r) * nw + FB * tx + c] = U[r][c];
-    }
     __syncthreads();
-    // ---- E_{i+1} = D_{i+1} - U Kc^T  (3 x 3 register blocks)
-    if (3 * ty < ndx && 3 * tx < ndx) {
-      double Cr[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
-      for (int k = 0; k < nw; ++k) {
-        double ua[3], kb[3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          ua[r] = (3 * ty + r < ndx) ? Sl[(3 * ty + r) * nw + k] : 0.0;
-          kb[r] = (3 * tx + r < ndx) ? Kc[(3 * tx + r) * nw + k] : 0.0;
+    // ---- E_{i+1} = D_{i+1} - U Kc^T:  (U Kc^T)[a][b] = sum_{(e, s) in xc(b)} rho_s A_e (U w_s)[a]
+    for (int k = tid; k < ndx * ndx; k += NT) {
+      const int ra = k / ndx, cb = k - ra * ndx;
+      double acc = 0.0;
+      for (int q = pg[p_xcptr + cb]; q < pg[p_xcptr + cb + 1]; ++q) {
+        const uint32_t w = f_xc[q];
+        const int sidx = (int)(w >> 16);
+        double t = 0.0;
+        for (int q2 = pg[p_cwptr + sidx]; q2 < pg[p_cwptr + sidx + 1]; ++q2) {
+          const uint32_t w2 = f_cw[q2];
+          t += asb[w2 & 0xffff] * Kc[ra * nw + (int)(w2 >> 16)];
         }
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int c = 0; c < 3; ++c) Cr[r][c] += ua[r] * kb[c];
+        acc += rwb[pg[p_cplr + sidx]] * asb[w & 0xffff] * t;
       }
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-          if (3 * ty + r < ndx && 3 * tx + c < ndx) {
-            double* p = Cb + (3 * ty + r) * ndx + 3 * tx + c;
-            *p = *p - Cr[r][c];
-          }
+      Cb[k] -= acc;
     }
     T(8);
   }

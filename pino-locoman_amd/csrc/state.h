@@ -37,7 +37,10 @@ struct PlNode {
 //
 // Factor program (k_factor.hip), u16 offsets relative to `fprog` in d.fprog:
 //   f_rowptr[nrow+1], f_cplr[ncpl] (coupling rows = rows with a dx_{i+1} entry),
-//   f_rowp[] = (entry, local col) pairs in CSR order; flen = total u16 words.
+//   f_rowp[] = (entry, local col) pairs in CSR order;
+//   coupling lists (same meaning as the ADMM program's cw / xc / cx):
+//   f_cwptr[ncpl+1] f_cwp[] = (entry, col < nw), f_xcptr[ndx+1] f_xcp[] = (entry, coupling
+//   index), f_cxptr[ncpl+1] f_cxp[] = (entry, dx_{i+1} col); flen = total u16 words.
 // ADMM program (k_admm.hip), u16 offsets relative to `prog` in d.aprog; every
 // distinct program is resident in LDS for the whole sweep kernel.  Pair lists hold
 // (entry, index) as two consecutive u16 (one 32-bit read; their offsets are even):
@@ -72,6 +75,7 @@ struct PlAdmmNode {
   int rowe, rowc, colr, cwptr, cwp, cxptr, cxp, ccptr, ccp, xcptr, xcp;
   int rchn, rch, rchptr, cchn, cch, cchptr;
   int fprog, flen, f_rowptr, f_cplr, f_rowp;
+  int f_cwptr, f_cwp, f_xcptr, f_xcp, f_cxptr, f_cxp;  // coupling lists of the factor program
   int ttab;  // offset (u32) of the node's lane-tile table in d.ttab (-1: more than PL_ADMM_KM slots)
 };
 
