@@ -4,9 +4,9 @@
 // Replaces the CasADi functions sqp_data / f_data / g_data / hess_data
 // (optimization/ocp.py:283-296, 386, 441-452).  One horizon node of one problem
 // is the unit of work: values use one thread per (problem, node); the Jacobian
-// uses one workgroup per (problem, node) and one thread per local column, each
-// thread seeding the tangent of its column and writing the column's entries of
-// the fixed sparsity pattern (CSC order inside the node).
+// uses one single-wave workgroup per (problem, node, 64-column chunk) and one
+// thread per local column, each thread seeding the tangent of its column and
+// writing the column's entries of the fixed sparsity pattern (CSC order inside the node).
 #include "state.h"
 #include "targets.h"
 
@@ -69,13 +69,16 @@ __global__ void k_eval_values(PlDev d, int B, int N, int n, int m, int np, const
   pl::node_rows<double, DYN>(M, O, i, p, dx, u, dxn, e);
 }
 
-// Constraint Jacobian values on the fixed pattern.  Block = (problem, node),
-// thread = local column.
+// Constraint Jacobian values on the fixed pattern.  Block = one wave = (problem, node,
+// chunk of 64 local columns), thread = local column.  Single-wave blocks retire
+// independently, so the cheap chunks (dx_{i+1} columns skip the tree pass) free their
+// SIMD slot at once.
 template <int DYN>
-__global__ __launch_bounds__(256) void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz) {
-  const int b = blockIdx.x / N, i = blockIdx.x - (blockIdx.x / N) * N;
+__global__ __launch_bounds__(64) void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz) {
+  const int bi = blockIdx.x;
+  const int b = bi / N, i = bi - (bi / N) * N;
   const PlNode nd = d.nodes[i];
-  const int lc = threadIdx.x;
+  const int lc = (int)blockIdx.y * 64 + threadIdx.x;  // chunk y: dispatched after every chunk y - 1
   if (lc >= nd.ncol) return;
   const int* cp = d.colptr + nd.colptr_off;
   const int e0 = cp[lc], e1 = cp[lc + 1];
@@ -187,8 +190,8 @@ void launch_eval_values(PlOcpHandle* h, const double* xsrc) {
 }
 
 void launch_eval_jac(PlOcpHandle* h) {
-  PL_DISPATCH_DYN(h->oc.dyn, k_eval_jac, dim3(h->B * h->N), dim3(h->ncol_max <= 192 ? 192 : 256), 0, h->stream,
-                  h->d, h->B, h->N, h->n, h->np, h->nnz);
+  PL_DISPATCH_DYN(h->oc.dyn, k_eval_jac, dim3(h->B * h->N, (h->ncol_max + 63) / 64), dim3(64), 0, h->stream, h->d,
+                  h->B, h->N, h->n, h->np, h->nnz);
 }
 
 void launch_objective(PlOcpHandle* h) {

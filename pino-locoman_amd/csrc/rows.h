@@ -11,6 +11,8 @@
 // The block list per node type is built on the host (api.cpp: build_blocks) so
 // the row order has one definition shared by the layout code and this emitter.
 #pragma once
+#include <type_traits>
+
 #include "rbd.h"
 
 namespace pl {
@@ -95,9 +97,22 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
   const bool state_rows = (type != 0);
   NodeKin<S> kin;
   constexpr bool want_tau = (DYN != PL_DYN_ABA);
-  if (want_tau || state_rows) tree_pass<S>(M, O, q, v, a, forces, want_tau, state_rows, kin);
+  // A Jacobian column seeded on dx_{i+1}, or (rnea) on tau_j, has a zero tangent in the
+  // tree pass and the ABA: every row that reads them then has a zero derivative, so
+  // the pass is skipped (its values are not emitted for such a column's pattern).
+  bool tree = true;
+  if constexpr (!std::is_same<S, double>::value) {
+    const bool seed_dxn = dxn.seed >= 0 && dxn.seed < O.ndx;
+    const bool seed_tau = DYN == PL_DYN_RNEA && u.seed >= O.na + O.nf && u.seed < O.na + O.nf + nj;
+    tree = !(seed_dxn || seed_tau);
+  }
+  if (tree && (want_tau || state_rows)) tree_pass<S>(M, O, q, v, a, forces, want_tau, state_rows, kin);
   S aba_a[DYN == PL_DYN_ABA ? PL_MAXV : 1];
-  if constexpr (DYN == PL_DYN_ABA) aba_forward<S>(M, O, q, v, tau_j, forces, aba_a);
+  if constexpr (DYN == PL_DYN_ABA) {
+    if (tree) aba_forward<S>(M, O, q, v, tau_j, forces, aba_a);
+    else
+      for (int k = 0; k < nv; ++k) aba_a[k] = S(0.0);
+  }
 
   const int nb = O.nblk[type];
   for (int bi = 0; bi < nb; ++bi) {
