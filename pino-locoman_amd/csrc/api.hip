@@ -587,6 +587,8 @@ int build_admm_prog(pl_ocp* o) {
     if (o->ttab.empty()) o->ttab.assign(64 * PL_ADMM_KM, 0xff000000u);
   }
   h.aprog_len = (int)o->aprog.size();
+  h.prog_len_max = 0;
+  for (int i = 0; i <= N; ++i) h.prog_len_max = std::max(h.prog_len_max, o->anodes[i].prog_len);
   {  // A values staged through registers: enough for the most frequent node program
     std::vector<int> cnt;
     std::vector<int> nmax;

@@ -132,48 +132,96 @@ __global__ __launch_bounds__(256) void k_ruiz_init(PlDev d, int n, int m) {
   if (threadIdx.x == 0) d.cs[b] = 1.0;
 }
 
-__global__ __launch_bounds__(256) void k_ruiz_norms(PlDev d, int N, int n, int m, int nnz) {
+// Norms of one pass for node i, from its A slice, D / E slices and its ADMM program
+// staged in LDS (balanced chunk maxima, as the ADMM gathers):
+//   Dt_j = max(c D_j^2 |P_jj|, D_j max over node i's entries of column j)  for j in w_i
+//   Dx_j = max over node i's entries of column j                        for j in dx_{i+1}
+//   Et_r = E_r max_j |A_rj| D_j                                         for the rows of node i
+// k_ruiz_update folds D_j Dx_j into Dt_j (max is exact in any order).
+__global__ __launch_bounds__(256) void k_ruiz_norms(PlDev d, int N, int n, int m, int nnz, int ndx, int nent_max,
+                                                    int ncol_max, int nrow_max, int chunk_max) {
+  extern __shared__ double lds[];
   const int b = blockIdx.x / (N + 1), i = blockIdx.x - b * (N + 1);
-  const PlNode nd = d.nodes[i];
-  const double* A = d.Araw + (size_t)b * nnz;
-  const double* P = d.P + (size_t)b * n;
+  typedef const __attribute__((address_space(4))) PlAdmmNode* CNode;
+  CNode an = (CNode)d.anodes;
+  const int nw = an[i].nw, nrow = an[i].nrow, nent = an[i].nent, ncol = an[i].ncol;
+  const int x_off = an[i].x_off, row_off = an[i].row_off, ent_off = an[i].ent_off;
+  const int prog = an[i].prog, plen = an[i].prog_len;
+  double* As = lds;
+  double* Dl = As + nent_max;
+  double* El = Dl + ncol_max;
+  double* cm = El + nrow_max;
+  uint16_t* P = reinterpret_cast<uint16_t*>(cm + chunk_max);
+  const double* A = d.Araw + (size_t)b * nnz + ent_off;
+  const double* Pd = d.P + (size_t)b * n;
   const double* D = d.D + (size_t)b * n;
   const double* E = d.E + (size_t)b * m;
   double* Dt = d.dxs + (size_t)b * n;  // scratch
+  double* Dx = d.aty + (size_t)b * n;  // scratch: dx_{i+1} column maxima of node i
   double* Et = d.dys + (size_t)b * m;  // scratch
   const double c = d.cs[b];
-  for (int lc = threadIdx.x; lc < nd.nw; lc += blockDim.x) {
-    double mx = 0.0;
-    if (i < N) {
-      const int* cp = d.colptr + nd.colptr_off;
-      for (int e = cp[lc]; e < cp[lc + 1]; ++e)
-        mx = fmax(mx, fabs(A[nd.ent_off + e]) * E[nd.row_off + d.rowidx[nd.ent_off + e]]);
-    }
-    if (i > 0 && lc < d.oc->ndx) {
-      const PlNode pv = d.nodes[i - 1];
-      const int* cp = d.colptr + pv.colptr_off;
-      for (int e = cp[pv.nw + lc]; e < cp[pv.nw + lc + 1]; ++e)
-        mx = fmax(mx, fabs(A[pv.ent_off + e]) * E[pv.row_off + d.rowidx[pv.ent_off + e]]);
-    }
-    const int j = nd.x_off + lc;
-    const double dj = D[j];
-    Dt[j] = fmax(c * dj * dj * fabs(P[j]), dj * mx);
+  const int tid = threadIdx.x;
+  for (int k = tid; k < nent; k += 256) As[k] = A[k];
+  for (int k = tid; k < ncol; k += 256) Dl[k] = D[x_off + k];  // w_i then dx_{i+1}: contiguous
+  for (int k = tid; k < nrow; k += 256) El[k] = E[row_off + k];
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(d.aprog + prog);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(P);
+    for (int k = tid; k < (plen >> 1); k += 256) dst[k] = src[k];
   }
-  if (i < N) {
-    const PlNode nn = d.nodes[i + 1];
-    const int* rp = d.rowptr + nd.rowptr_off;
-    const int* re = d.rowent + nd.csr_off;
-    for (int lr = threadIdx.x; lr < nd.nrow; lr += blockDim.x) {
+  __syncthreads();
+  // ---- columns
+  const int cchn = an[i].cchn;
+  {
+    const uint8_t* colr = reinterpret_cast<const uint8_t*>(P + an[i].colr);
+    const uint32_t* cch = reinterpret_cast<const uint32_t*>(P + an[i].cch);
+    for (int ch = tid; ch < cchn; ch += 256) {
+      const uint32_t w = cch[ch];
+      const int e0 = w & 0xffff, e1 = (int)(w >> 16);
       double mx = 0.0;
-      for (int q = rp[lr]; q < rp[lr + 1]; ++q) {
-        const int e = re[q];
-        const int lc = d.entcol[nd.ent_off + e];
-        const int j = lc < nd.nw ? nd.x_off + lc : nn.x_off + (lc - nd.nw);
-        mx = fmax(mx, fabs(A[nd.ent_off + e]) * D[j]);
-      }
-      const int r = nd.row_off + lr;
-      Et[r] = E[r] * mx;
+      for (int e = e0; e < e1; ++e) mx = fmax(mx, fabs(As[e]) * El[colr[e]]);
+      cm[ch] = mx;
     }
+  }
+  __syncthreads();
+  for (int lc = tid; lc < nw; lc += 256) {
+    double mx = 0.0;
+    if (ncol) {
+      const int k0 = P[an[i].cchptr + lc], k1 = P[an[i].cchptr + lc + 1];
+      for (int k = k0; k < k1; ++k) mx = fmax(mx, cm[k]);
+    }
+    const int j = x_off + lc;
+    const double dj = D[j];
+    Dt[j] = fmax(c * dj * dj * fabs(Pd[j]), dj * mx);
+    if (lc >= ndx || i == 0) Dx[j] = 0.0;  // no predecessor entries on these columns
+  }
+  for (int lc = nw + tid; lc < ncol; lc += 256) {  // dx_{i+1}: node i's share
+    const int k0 = P[an[i].cchptr + lc], k1 = P[an[i].cchptr + lc + 1];
+    double mx = 0.0;
+    for (int k = k0; k < k1; ++k) mx = fmax(mx, cm[k]);
+    Dx[x_off + lc] = mx;
+  }
+  __syncthreads();
+  // ---- rows
+  const int rchn = an[i].rchn;
+  {
+    const uint16_t* rowe = P + an[i].rowe;
+    const uint8_t* rowc = reinterpret_cast<const uint8_t*>(P + an[i].rowc);
+    const uint32_t* rch = reinterpret_cast<const uint32_t*>(P + an[i].rch);
+    for (int ch = tid; ch < rchn; ch += 256) {
+      const uint32_t w = rch[ch];
+      const int q0 = w & 0xffff, q1 = (int)(w >> 16);
+      double mx = 0.0;
+      for (int q = q0; q < q1; ++q) mx = fmax(mx, fabs(As[rowe[q]]) * Dl[rowc[q]]);
+      cm[ch] = mx;
+    }
+  }
+  __syncthreads();
+  for (int lr = tid; lr < nrow; lr += 256) {
+    const int k0 = P[an[i].rchptr + lr], k1 = P[an[i].rchptr + lr + 1];
+    double mx = 0.0;
+    for (int k = k0; k < k1; ++k) mx = fmax(mx, cm[k]);
+    Et[row_off + lr] = El[lr] * mx;
   }
 }
 
@@ -185,11 +233,13 @@ __global__ __launch_bounds__(256) void k_ruiz_update(PlDev d, int n, int m) {
   double* D = d.D + (size_t)b * n;
   double* E = d.E + (size_t)b * m;
   const double* Dt = d.dxs + (size_t)b * n;
+  const double* Dx = d.aty + (size_t)b * n;
   const double* Et = d.dys + (size_t)b * m;
   const double c = d.cs[b];
   double sum = 0.0, qmax = 0.0;
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
-    const double dj = D[j] * (1.0 / sqrt(limit_scaling(Dt[j])));
+    const double dt = fmax(Dt[j], D[j] * Dx[j]);  // + node i-1's entries on dx_i
+    const double dj = D[j] * (1.0 / sqrt(limit_scaling(dt)));
     D[j] = dj;
     sum += c * dj * dj * fabs(P[j]);
     qmax = fmax(qmax, fabs(c * dj * q[j]));
@@ -265,8 +315,17 @@ __global__ __launch_bounds__(256) void k_qp_finish(PlDev d, int N, int n, int m,
 void launch_qp_setup(PlOcpHandle* h) {
   const dim3 nodes_grid(h->B * (h->N + 1));
   hipLaunchKernelGGL(k_ruiz_init, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, h->m);
+  const int nent_max = (std::max(h->nent_max, 1) + 1) & ~1, ncol_max = (std::max(h->ncol_max, h->nw_max) + 1) & ~1;
+  const int nrow_max = (std::max(h->nrow_max, 1) + 1) & ~1, chunk_max = (std::max(h->chunk_max, 1) + 1) & ~1;
+  const size_t lds = (size_t)(nent_max + ncol_max + nrow_max + chunk_max) * 8 + ((2 * (size_t)h->prog_len_max + 15) & ~(size_t)15);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)k_ruiz_norms, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
   for (int pass = 0; pass < h->set.scaling; ++pass) {
-    hipLaunchKernelGGL(k_ruiz_norms, nodes_grid, dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz);
+    hipLaunchKernelGGL(k_ruiz_norms, nodes_grid, dim3(256), lds, h->stream, h->d, h->N, h->n, h->m, h->nnz,
+                       h->ndx, nent_max, ncol_max, nrow_max, chunk_max);
     hipLaunchKernelGGL(k_ruiz_update, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, h->m);
   }
   hipLaunchKernelGGL(k_qp_finish, nodes_grid, dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz,

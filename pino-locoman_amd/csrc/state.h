@@ -166,6 +166,7 @@ struct PlOcpHandle {
   int chunk_max;                    // max(rchn, cchn) over nodes (ADMM partial-sum buffer)
   int flen_max;                     // longest factor program (u16)
   int aprog_len;                    // all ADMM programs (u16), resident in LDS
+  int prog_len_max;                 // longest single ADMM program (u16)
   int admm_asr;                     // A values per lane staged through registers (x 64 lanes)
   int admm_fwd_asb;                 // coupling rows too dense for registers: forward steps stage A in LDS
   PlSettings set;
