@@ -135,6 +135,9 @@ int pl_ocp_init_solver(pl_ocp* o);                   /* Hessian diag + reset ADM
 /* One SQP iteration in place for the whole batch.  stats: [batch] or NULL;
  * phase_ms: [4] (data, update+factor, admm, line search) or NULL. */
 int pl_ocp_solve(pl_ocp* o, pl_stats* stats, double* phase_ms);
+/* SQP iterations per pl_ocp_solve / pl_mpc_step (default 1 = the reference's
+ * `for _ in range(1)`, optimization/ocp.py:382-383). */
+int pl_ocp_set_sqp_iters(pl_ocp* o, int sqp_iters);
 /* Evaluate sqp_data at the current x: any output may be NULL. */
 int pl_eval_sqp_data(pl_ocp* o, double* grad, double* Jvals, double* g, double* lbg, double* ubg);
 /* f_data value at the current x. */

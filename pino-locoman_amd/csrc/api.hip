@@ -738,6 +738,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   h.set.scaling = d->scaling;
   h.set.check_termination = d->check_termination;
   h.set.warm_start = d->warm_start;
+  h.sqp_iters = 1;
   h.gait_type = d->gait_type;
   h.gait_period = d->gait_period;
   h.swing_period = d->gait_type == 0 ? 0.5 * d->gait_period : (d->gait_type == 1 ? 0.25 * d->gait_period : d->gait_period);
@@ -746,7 +747,12 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   h.device = device;
   if (!o->on_device) { *out = o; return 0; }
 
-  if (hipSetDevice(device) != hipSuccess) { pl_set_error("hipSetDevice(%d) failed", device); delete o; return -2; }
+  if (hipSetDevice(device) != hipSuccess) {
+    (void)hipGetLastError();  // do not leave the failure as the thread's sticky last error
+    pl_set_error("hipSetDevice(%d) failed", device);
+    delete o;
+    return -2;
+  }
   if (hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking) != hipSuccess) {
     pl_set_error("hipStreamCreate failed");
     delete o;
@@ -862,6 +868,7 @@ static void prof_collect(PlOcpHandle* h);
       return -1;                                                       \
     }                                                                  \
     (void)hipSetDevice((o)->h.device);                                 \
+    (void)hipGetLastError(); /* errors of earlier calls were reported there */ \
   } while (0)
 
 extern "C" int pl_ocp_set_params(pl_ocp* o, const double* P) {
@@ -972,9 +979,20 @@ static int fetch_stats(pl_ocp* o, pl_stats* stats) {
   return 0;
 }
 
+// SQP iterations per solve.  The reference runs one (`for _ in range(1)` with a TODO,
+// optimization/ocp.py:382-383); k > 1 repeats eval -> osqp.update -> warm-started
+// osqp.solve -> line search from the accepted point.  Phase times are those of the
+// last iteration.
+extern "C" int pl_ocp_set_sqp_iters(pl_ocp* o, int sqp_iters) {
+  if (!o) { pl_set_error("null handle"); return -1; }
+  if (sqp_iters < 1 || sqp_iters > 1000) { pl_set_error("sqp_iters %d outside [1, 1000]", sqp_iters); return -1; }
+  o->h.sqp_iters = sqp_iters;
+  return 0;
+}
+
 extern "C" int pl_ocp_solve(pl_ocp* o, pl_stats* stats, double* phase_ms) {
   REQUIRE_DEVICE(o);
-  enqueue_solve(o, phase_ms != nullptr);
+  for (int k = 0; k < o->h.sqp_iters; ++k) enqueue_solve(o, phase_ms != nullptr);
   PL_CHECK_HIP(hipGetLastError());
   PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
   if (phase_ms) {
@@ -1028,7 +1046,7 @@ extern "C" int pl_mpc_step(pl_ocp* o, int k) {
   REQUIRE_DEVICE(o);
   if (o->h.profile && o->h.prof_n > 48) prof_collect(&o->h);
   launch_mpc_prepare(&o->h, k);
-  enqueue_solve(o, false);
+  for (int it = 0; it < o->h.sqp_iters; ++it) enqueue_solve(o, false);
   launch_mpc_finish(&o->h);
   PL_CHECK_HIP(hipGetLastError());
   return 0;

@@ -169,6 +169,7 @@ struct PlOcpHandle {
   int prog_len_max;                 // longest single ADMM program (u16)
   int admm_asr;                     // A values per lane staged through registers (x 64 lanes)
   int admm_fwd_asb;                 // coupling rows too dense for registers: forward steps stage A in LDS
+  int sqp_iters;                    // SQP iterations per solve (reference: 1, ocp.py:382-383)
   PlSettings set;
   PlModel model;
   PlOcpConst oc;

@@ -226,6 +226,10 @@ class BatchedOCP:
     def init_solver(self):
         _lib.check(_lib.lib().pl_ocp_init_solver(self.h))
 
+    def set_sqp_iters(self, k):
+        """SQP iterations per solve / MPC step (reference: 1, ocp.py:382-383)."""
+        _lib.check(_lib.lib().pl_ocp_set_sqp_iters(self.h, int(k)))
+
     def solve(self, timed=False):
         stats = (_lib.Stats * self.batch)()
         phase = np.zeros(4)
@@ -469,8 +473,10 @@ class OCP:
         self._backend.set_params(self.param_vector())
         self._backend.init_solver()
 
-    def solve(self, retract_all=True):
-        """ocp.py:375-422 (OSQP branch): one SQP iteration on the GPU."""
+    def solve(self, retract_all=True, sqp_iters=1):
+        """ocp.py:375-422 (OSQP branch) on the GPU: `sqp_iters` SQP iterations (the
+        reference runs one, `for _ in range(1)`, ocp.py:382-383)."""
+        self._backend.set_sqp_iters(sqp_iters)
         self._backend.set_params(self.param_vector())
         self._backend.set_x(self._x_initial)
         start = time.time()

@@ -120,6 +120,12 @@ def test_bad_arguments_are_errors():
         make_ocp("nonsense", OCP_ARGS, robot=R, nodes=10, solver="osqp")
     with pytest.raises(_lib.PinolocoError):
         BatchedOCP(R, "whole_body_rnea", 10, batch=0, device=-1)
+    bo = BatchedOCP(R, "whole_body_rnea", 10, batch=1, device=-1)
+    bo.set_sqp_iters(3)  # a setting: allowed on a host-only handle
+    for bad in (0, -1, 1001):
+        with pytest.raises(_lib.PinolocoError):
+            bo.set_sqp_iters(bad)
+    bo.close()
 
 
 @pytest.mark.parametrize("rname", ["go2", "b2g"])

@@ -197,3 +197,34 @@ def test_device_errors_are_loud():
     with pytest.raises(_lib.PinolocoError):
         BatchedOCP(R, "whole_body_rnea", 10, batch=1, device=64)
     bo.close()
+
+
+def test_multi_iteration_sqp_matches_oracle():
+    """k SQP iterations per solve (the reference's `for _ in range(1)`
+    generalised, ocp.py:382-383): eval -> osqp.update -> warm-started osqp.solve ->
+    line search, repeated from the accepted point.  The oracle repeats sqp_step with
+    the same OSQP object (warm start kept).  Last-iteration stats exact, x <= 1e-7."""
+    from pinoloco.ocp import BatchedOCP
+    from oracle.ocp import OracleOCP
+    G = golden("sqp_go2_rnea_n20.npz")
+    R = make_robot("go2")
+    B, K = 2, 3
+    bo = BatchedOCP(R, "whole_body_rnea", 20, batch=B, device=0)
+    bo.set_params(G["P"][:B])
+    bo.set_x(G["X"][:B])
+    bo.init_solver()
+    bo.set_sqp_iters(K)
+    st = bo.solve()
+    xg = bo.get_x()
+    for b in range(B):
+        o = OracleOCP(R, "whole_body_rnea", 20)
+        x, p = G["X"][b].copy(), G["P"][b]
+        o.init_solver(x, p)
+        for _ in range(K):
+            x, _, sto = o.sqp_step(x, p)
+        assert st["status"][b] == sto["status"] and st["admm_iters"][b] == sto["iter"]
+        assert st["ls_branch"][b] == sto["branch"] and st["ls_trials"][b] == sto["trials"]
+        assert _rel(xg[b], x) < 1e-7
+    with pytest.raises(Exception):
+        bo.set_sqp_iters(0)
+    bo.close()
