@@ -138,6 +138,13 @@ int pl_ocp_solve(pl_ocp* o, pl_stats* stats, double* phase_ms);
 /* SQP iterations per pl_ocp_solve / pl_mpc_step (default 1 = the reference's
  * `for _ in range(1)`, optimization/ocp.py:382-383). */
 int pl_ocp_set_sqp_iters(pl_ocp* o, int sqp_iters);
+
+/* CasADi external-function ABI (include/pinoloco_casadi.h): bind the OCP whose
+ * shapes / sparsity the exported sqp_data, f_data, g_data, hess_data and
+ * retract_solution describe (replaces the generated code of ocp.py:299-302 and
+ * ocp_whole_body_rnea.py:326-366; retract_steps = num_steps of compile_solution). */
+int pl_casadi_bind(pl_ocp* o, int retract_steps);
+void pl_casadi_unbind(void);
 /* Evaluate sqp_data at the current x: any output may be NULL. */
 int pl_eval_sqp_data(pl_ocp* o, double* grad, double* Jvals, double* g, double* lbg, double* ubg);
 /* f_data value at the current x. */

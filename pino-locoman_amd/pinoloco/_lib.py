@@ -58,6 +58,8 @@ EXPORTS = {
     "pl_ocp_init_solver": (C.c_int, [C.c_void_p]),
     "pl_ocp_solve": (C.c_int, [C.c_void_p, C.POINTER(Stats), _dp]),
     "pl_ocp_set_sqp_iters": (C.c_int, [C.c_void_p, C.c_int]),
+    "pl_casadi_bind": (C.c_int, [C.c_void_p, C.c_int]),
+    "pl_casadi_unbind": (None, []),
     "pl_eval_sqp_data": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),
     "pl_eval_f": (C.c_int, [C.c_void_p, _dp]),
     "pl_ocp_get_step": (C.c_int, [C.c_void_p, _dp]),

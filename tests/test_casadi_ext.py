@@ -1,0 +1,96 @@
+"""CasADi external-function ABI (include/pinoloco_casadi.h) without a GPU: exported
+symbols, n_in/n_out/work, compressed-column sparsity of every input/output, and
+retract_solution (host computation) against the oracle's state integrate."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import make_robot
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    txt = open(os.path.join(ROOT, "include", "pinoloco_casadi.h")).read()
+    names = re.findall(r"^PL_CASADI_DECLARE\((\w+)\)", txt, re.M)
+    suffixes = re.findall(r"NAME##_(\w+)\(", txt)
+    return names, suffixes
+
+
+def test_casadi_symbols_exported():
+    from pinoloco import _lib, casadi_ext
+    names, suffixes = _declared()
+    assert tuple(names) == casadi_ext.FUNCTIONS
+    L = _lib.lib()
+    for n in names:
+        getattr(L, n)
+        for s in suffixes:
+            getattr(L, f"{n}_{s}")
+
+
+def test_unbound_is_an_error():
+    from pinoloco import _lib, casadi_ext
+    casadi_ext.unbind()
+    with pytest.raises(_lib.PinolocoError):
+        casadi_ext.ExternalFunction("sqp_data")
+
+
+@pytest.mark.parametrize("rname,dyn,N", [("go2", "whole_body_rnea", 10), ("b2g", "whole_body_rnea", 8)])
+def test_shapes_and_sparsity(rname, dyn, N):
+    from pinoloco import casadi_ext
+    from pinoloco.ocp import BatchedOCP
+    R = make_robot(rname)
+    bo = BatchedOCP(R, dyn, N, batch=1, device=-1)
+    casadi_ext.bind(bo, 3)
+    f = casadi_ext.ExternalFunction("sqp_data")
+    assert (f.n_in, f.n_out, f.sz_arg, f.sz_res, f.sz_iw, f.sz_w) == (2, 5, 2, 5, 0, 0)
+    assert f.sp_in[0][:2] == (bo.n, 1) and f.sp_in[1][:2] == (bo.np, 1)
+    nrow, ncol, colind, row = f.sp_out[1]
+    assert (nrow, ncol, int(colind[-1])) == (bo.m, bo.n, bo.nnz)
+    assert np.all(np.diff(colind) >= 0)
+    for j in range(ncol):  # rows strictly increasing inside each column
+        assert np.all(np.diff(row[colind[j]:colind[j + 1]]) > 0)
+    # same pattern as the library's (rows, cols) listing
+    rows, cols = bo.pattern()
+    got = set(zip(row.tolist(), np.repeat(np.arange(ncol), np.diff(colind)).tolist()))
+    assert got == set(zip(rows.tolist(), cols.tolist()))
+    assert [s[:2] for s in f.sp_out[2:]] == [(bo.m, 1)] * 3
+    h = casadi_ext.ExternalFunction("hess_data")
+    assert h.sp_out[0][:2] == (bo.n, bo.n) and int(h.sp_out[0][2][-1]) == bo.n
+    fd = casadi_ext.ExternalFunction("f_data")
+    assert fd.sp_out[0][:2] == (1, 1) and fd.sp_out[1][:2] == (bo.n, 1)
+    casadi_ext.unbind()
+    bo.close()
+
+
+def test_retract_solution_matches_oracle():
+    """retract_solution (ocp_whole_body_rnea.py:326-366): node-major rows of q, v, a,
+    forces, tau over the first 3 nodes, q/v by the Lie-group integrate."""
+    from oracle.ocp import OracleOCP
+    from pinoloco import casadi_ext
+    from pinoloco.ocp import BatchedOCP
+    R = make_robot("b2g")
+    N = 8
+    bo = BatchedOCP(R, "whole_body_rnea", N, batch=1, device=-1)
+    casadi_ext.bind(bo, 3)
+    fr = casadi_ext.ExternalFunction("retract_solution")
+    rng = np.random.default_rng(3)
+    sol = rng.normal(size=bo.n) * 0.1
+    x_init = np.concatenate([R.q0, rng.normal(size=R.nv) * 0.1])
+    q, v, a, f, tau = fr(sol, x_init)
+    o = OracleOCP(R, "whole_body_rnea", N)
+    DX, U = o.split(sol)
+    assert q.shape == (3, R.nq) and v.shape == (3, R.nv)
+    for i in range(3):
+        xs = o.integrate_state(x_init, DX[i])
+        assert np.abs(q[i] - xs[:R.nq]).max() < 1e-12
+        assert np.abs(v[i] - xs[R.nq:]).max() < 1e-12
+        assert np.array_equal(a[i], U[i][:o.na])
+        assert np.array_equal(f[i], U[i][o.na:o.na + o.nf])
+        assert np.array_equal(tau[i], U[i][o.na + o.nf:])
+    with pytest.raises(Exception):
+        casadi_ext.ExternalFunction("sqp_data")(sol, np.zeros(bo.np))  # no device on this handle
+    casadi_ext.unbind()
+    bo.close()

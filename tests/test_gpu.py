@@ -228,3 +228,35 @@ def test_multi_iteration_sqp_matches_oracle():
     with pytest.raises(Exception):
         bo.set_sqp_iters(0)
     bo.close()
+
+
+def test_casadi_external_functions_match_golden():
+    """sqp_data / f_data / g_data / hess_data through the CasADi external ABI
+    (ca.external drop-in, include/pinoloco_casadi.h) on the GPU vs the golden vectors;
+    J_g in CasADi compressed-column order."""
+    from pinoloco import casadi_ext
+    from pinoloco.ocp import BatchedOCP
+    G = golden("sqp_go2_rnea_n20.npz")
+    R = make_robot("go2")
+    bo = BatchedOCP(R, "whole_body_rnea", 20, batch=1, device=0)
+    bo.set_params(G["P"][:1])
+    bo.set_x(G["X"][:1])
+    casadi_ext.bind(bo, 3)
+    x, p = G["X"][0], G["P"][0]
+    grad, J, g, lbg, ubg = casadi_ext.ExternalFunction("sqp_data")(x, p)
+    assert _rel(grad.ravel(), G["grad"][0]) < 1e-12
+    assert _rel(g.ravel(), G["g"][0]) < 1e-12
+    assert np.array_equal(lbg.ravel(), G["lbg"][0]) and np.array_equal(ubg.ravel(), G["ubg"][0])
+    Jg = sp.csr_matrix((G["J_data_0"], G["J_indices_0"], G["J_indptr_0"]), shape=J.shape)
+    assert abs(J - Jg).max() <= 1e-12 * abs(Jg).max()
+    f, grad2 = casadi_ext.ExternalFunction("f_data")(x, p)
+    assert float(f[0, 0]) == pytest.approx(float(G["f"][0]), rel=1e-12)
+    assert np.array_equal(grad2, grad)
+    g2, l2, u2 = casadi_ext.ExternalFunction("g_data")(x, p)
+    assert np.array_equal(g2, g) and np.array_equal(l2, lbg)
+    (H,) = casadi_ext.ExternalFunction("hess_data")(x, p)
+    from oracle.ocp import OracleOCP
+    hd = OracleOCP(R, "whole_body_rnea", 20).compute_hess_diag(p)
+    assert np.array_equal(H.diagonal(), hd)
+    casadi_ext.unbind()
+    bo.close()
