@@ -43,6 +43,9 @@ struct pl_ocp {
   std::vector<PlAdmmNode> anodes;
   std::vector<uint16_t> aprog, fprog;
   std::vector<uint32_t> ttab;
+  std::vector<PlFacNode> fnodes;
+  std::vector<uint32_t> kasm, kcpl;
+  std::vector<uint16_t> kfl;
   std::vector<double> h_params;  // host copy of the parameters (B x np)
   std::vector<void*> allocs;
   hipEvent_t ev[5];
@@ -606,8 +609,8 @@ int build_admm_prog(pl_ocp* o) {
       if (cnt[k] > cnt[dom]) dom = k;
     h.admm_asr = nmax[dom] <= 16 * 64 ? 16 : PL_ADMM_ASR_MAX;
   }
-  if (ndx > 48) {
-    pl_set_error("state dimension 2 nv = %d > 48 is not supported by the factor kernel", ndx);
+  if (!factor_supports_ndx(ndx)) {
+    pl_set_error("state dimension ndx = %d is not supported by the factor kernel (36, 48)", ndx);
     return -1;
   }
   if (h.nrow_max > 64 * PL_ADMM_MR || h.nw_max > 64 * PL_ADMM_MV || h.ncpl_max > 64) {
@@ -620,6 +623,196 @@ int build_admm_prog(pl_ocp* o) {
     pl_set_error("terminal node must own exactly dx_N and no rows");
     return -1;
   }
+  return 0;
+}
+
+
+// Programs of the two-stage factor (PlFacNode, state.h): the slot-owner assembly
+// streams of Kt_ii and the coupling program of the Schur chain, one per distinct
+// local structure, plus the launch groups of k_fnode.
+int build_factor_prog(pl_ocp* o) {
+  PlOcpHandle& h = o->h;
+  const int N = h.oc.N, X = h.oc.ndx;
+  const int NT = PL_FAC_NT;
+  o->fnodes.assign(N + 1, PlFacNode());
+  o->kasm.clear();
+  o->kfl.clear();
+  o->kcpl.clear();
+  std::vector<std::vector<uint32_t>> asms, cpls;
+  std::vector<std::vector<uint16_t>> fls;
+  std::vector<int> asm_offs, fl_offs, cpl_offs;
+  auto intern32 = [](std::vector<std::vector<uint32_t>>& progs, std::vector<int>& offs, std::vector<uint32_t>& all,
+                     const std::vector<uint32_t>& P) {
+    for (size_t k = 0; k < progs.size(); ++k)
+      if (progs[k] == P) return offs[k];
+    progs.push_back(P);
+    offs.push_back((int)all.size());
+    all.insert(all.end(), P.begin(), P.end());
+    return offs.back();
+  };
+  long long fs = 0;
+  std::vector<int> lds_of(N + 1), um_of(N + 1);
+  int npc_max = 1, ncw_max = 2;
+  for (int i = 0; i <= N; ++i) {
+    const PlNode& nd = o->nodes[i];
+    PlFacNode& f = o->fnodes[i];
+    memset(&f, 0, sizeof(f));
+    const int nw = nd.nw, U = nd.nu;
+    f.nw = nw; f.nu = U; f.nrow = nd.nrow; f.nent = nd.nent; f.ent_off = nd.ent_off; f.row_off = nd.row_off;
+    f.x_off = nd.x_off; f.s_off = nd.s_off; f.nunit = nd.nunit; f.ntl = nd.ntile * (nd.ntile + 1) / 2;
+    f.ttab = o->anodes[i].ttab;
+    if (U > 64) { pl_set_error("factor kernel: node with %d > 64 inputs", U); return -1; }
+    if (nd.nent >= 0x7fff) { pl_set_error("factor kernel: node with %d entries", nd.nent); return -1; }
+    const int* cp = o->colptr.data() + nd.colptr_off;
+    const int* rp = o->rowptr.data() + nd.rowptr_off;
+    const int* re = o->rowent.data() + nd.csr_off;
+    const int* rid = o->rowidx.data() + nd.ent_off;
+    const int* ecol = o->entcol.data() + nd.ent_off;
+    // ---- assembly: triples (rho_r a_e1, a_e2) of every lower slot of Kt_ii, rows in order
+    const int nslot = nw * (nw + 1) / 2;
+    std::vector<std::vector<uint32_t>> trip(nslot);
+    for (int r = 0; r < nd.nrow; ++r) {
+      for (int q1 = rp[r]; q1 < rp[r + 1]; ++q1) {
+        const int e1 = re[q1], c1 = ecol[e1];
+        if (c1 >= nw) continue;
+        for (int q2 = rp[r]; q2 < rp[r + 1]; ++q2) {
+          const int e2 = re[q2], c2 = ecol[e2];
+          if (c2 > c1) continue;
+          trip[c1 * (c1 + 1) / 2 + c2].push_back((uint32_t)e1 | ((uint32_t)e2 << 16));
+        }
+      }
+    }
+    std::vector<int> order;
+    for (int sl = 0; sl < nslot; ++sl)
+      if (!trip[sl].empty()) order.push_back(sl);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return trip[a].size() > trip[b].size(); });
+    std::vector<std::vector<uint32_t>> lane_w(NT);
+    std::vector<std::vector<uint16_t>> lane_f(NT);
+    std::vector<int> load(NT, 0);
+    for (int sl : order) {
+      int best = 0;
+      for (int t = 1; t < NT; ++t)
+        if (load[t] < load[best]) best = t;
+      for (size_t k = 0; k < trip[sl].size(); ++k)
+        lane_w[best].push_back(trip[sl][k] | (k + 1 == trip[sl].size() ? 0x8000u : 0u));
+      lane_f[best].push_back((uint16_t)sl);
+      load[best] += (int)trip[sl].size();
+    }
+    int L = 0, F = 0;
+    for (int t = 0; t < NT; ++t) {
+      L = std::max(L, (int)lane_w[t].size());
+      F = std::max(F, (int)lane_f[t].size());
+    }
+    const uint32_t zero = (uint32_t)nd.nent | ((uint32_t)nd.nent << 16);
+    std::vector<uint32_t> A((size_t)L * NT, zero);
+    std::vector<uint16_t> Fl((size_t)std::max(F, 1) * NT, 0);
+    for (int t = 0; t < NT; ++t) {
+      for (size_t k = 0; k < lane_w[t].size(); ++k) A[k * NT + t] = lane_w[t][k];
+      for (size_t k = 0; k < lane_f[t].size(); ++k) Fl[k * NT + t] = lane_f[t][k];
+    }
+    if (nslot > 65535) { pl_set_error("factor kernel: node block too large"); return -1; }
+    f.asm_len = L;
+    f.fl_len = F;
+    f.asm_off = A.empty() ? 0 : intern32(asms, asm_offs, o->kasm, A);
+    {
+      size_t k = 0;
+      for (; k < fls.size(); ++k)
+        if (fls[k] == Fl) break;
+      if (k == fls.size()) {
+        fls.push_back(Fl);
+        fl_offs.push_back((int)o->kfl.size());
+        o->kfl.insert(o->kfl.end(), Fl.begin(), Fl.end());
+      }
+      f.fl_off = fl_offs[k];
+    }
+    // ---- coupling program (i < N)
+    std::vector<uint32_t> C;
+    if (i < N) {
+      std::vector<int> crow(X), cent(X);
+      std::vector<int> owner(nd.nrow, -1);
+      for (int a = 0; a < X; ++a) {
+        const int c = nw + a;
+        if (cp[c + 1] - cp[c] != 1) {
+          pl_set_error("factor kernel: dx_{i+1} column %d of node %d is not owned by exactly one row", a, i);
+          return -1;
+        }
+        const int e = cp[c];
+        crow[a] = rid[e];
+        cent[a] = e;
+        if (owner[crow[a]] >= 0) {
+          pl_set_error("factor kernel: row %d of node %d couples more than one dx_{i+1} column", crow[a], i);
+          return -1;
+        }
+        owner[crow[a]] = a;
+      }
+      std::vector<int> used(nw, 0);
+      std::vector<std::vector<std::pair<int, int>>> cw(X);
+      for (int a = 0; a < X; ++a) {
+        const int r = crow[a];
+        for (int q = rp[r]; q < rp[r + 1]; ++q) {
+          const int e = re[q], c = ecol[e];
+          if (c < nw) { cw[a].push_back({e, c}); used[c] = 1; }
+        }
+      }
+      std::vector<int> pcl, pcof(nw, -1);
+      for (int c = 0; c < nw; ++c)
+        if (used[c]) { pcof[c] = (int)pcl.size(); pcl.push_back(c); }
+      if (nw > 255 || pcl.size() > 255) { pl_set_error("factor kernel: node too wide"); return -1; }
+      for (int a = 0; a < X; ++a) C.push_back((uint32_t)crow[a]);
+      for (int a = 0; a < X; ++a) C.push_back((uint32_t)cent[a]);
+      uint32_t q = 0;
+      for (int a = 0; a <= X; ++a) {
+        C.push_back(q);
+        if (a < X) q += (uint32_t)cw[a].size();
+      }
+      for (int c : pcl) C.push_back((uint32_t)c);
+      for (int a = 0; a < X; ++a)
+        for (auto& pr : cw[a])
+          C.push_back((uint32_t)pr.first | ((uint32_t)pr.second << 16) | ((uint32_t)pcof[pr.second] << 24));
+      f.npc = (int)pcl.size();
+      npc_max = std::max(npc_max, f.npc);
+      ncw_max = std::max(ncw_max, (int)q);
+      f.cp_off = intern32(cpls, cpl_offs, o->kcpl, C);
+    }
+    f.fs_off = fs;
+    fs += (long long)X * X + (long long)U * X + (long long)U * U;
+    fs = (fs + 31) & ~31LL;
+    // k_fnode LDS: packed lower Kt (even) | max(A values x 2, G) | pivot buffer [2][64]
+    const int nK = (nslot + 1) & ~1;
+    const int r2 = (std::max(2 * (nd.nent + 1), U * X) + 1) & ~1;
+    lds_of[i] = (nK + r2 + 128) * 8;
+    um_of[i] = U <= 40 ? 40 : 64;
+  }
+  h.fs_stride = std::max(fs, 32LL);
+  // launch groups: maximal runs of consecutive nodes with the same LDS size and register class
+  h.nfgroup = 0;
+  for (int i = 0; i <= N;) {
+    int j = i + 1;
+    while (j <= N && lds_of[j] == lds_of[i] && um_of[j] == um_of[i]) ++j;
+    if (h.nfgroup == PL_FAC_MAXGROUPS) { pl_set_error("factor kernel: too many node groups"); return -1; }
+    h.fg_i0[h.nfgroup] = i;
+    h.fg_n[h.nfgroup] = j - i;
+    h.fg_lds[h.nfgroup] = lds_of[i];
+    h.fg_um[h.nfgroup] = um_of[i];
+    ++h.nfgroup;
+    i = j;
+  }
+  for (int g = 0; g < h.nfgroup; ++g)
+    if (h.fg_lds[g] > 160 * 1024) { pl_set_error("factor kernel: node needs %d bytes of LDS", h.fg_lds[g]); return -1; }
+  // k_fchain LDS: packed lower S (even) | Y / transpose buffer | E | pivot buffer |
+  // staged coupling values (ncw + 2 X) | staged G (U x X) | staged C^-1 (packed lower)
+  const int nS = (h.nw_max * (h.nw_max + 1) / 2 + 1) & ~1;
+  const int ny = (std::max(npc_max * X, X * (X + 1)) + 1) & ~1;
+  h.fchain_ny = ny;
+  h.fchain_ncw = (ncw_max + 1) & ~1;
+  int umax = 0;
+  for (int i = 0; i <= N; ++i) umax = std::max(umax, o->nodes[i].nu);
+  h.fchain_gsz = (umax * X + 1) & ~1;
+  const int csz = (umax * (umax + 1) / 2 + 1) & ~1;
+  h.fchain_lds = (nS + ny + X * X + 128 + h.fchain_ncw + 2 * X + h.fchain_gsz + csz) * 8;
+  if (h.fchain_lds > 160 * 1024) { pl_set_error("factor kernel: chain needs %d bytes of LDS", h.fchain_lds); return -1; }
+  if (o->kasm.empty()) o->kasm.assign(NT, 0);
+  if (o->kcpl.empty()) o->kcpl.assign(4, 0);
   return 0;
 }
 
@@ -719,7 +912,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
     O.P.tau_prev = O.P.W_diag = -1;
   }
   O.P.np = off;
-  if (build_layout(o) || build_admm_prog(o)) { delete o; return -1; }
+  if (build_layout(o) || build_admm_prog(o) || build_factor_prog(o)) { delete o; return -1; }
   O.n = h.n;
   O.m = h.m;
   h.B = batch;
@@ -777,6 +970,10 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= upload(o, &D.aprog, o->aprog);
   rc |= upload(o, &D.fprog, o->fprog);
   rc |= upload(o, &D.ttab, o->ttab);
+  rc |= upload(o, &D.fnodes, o->fnodes);
+  rc |= upload(o, &D.kasm, o->kasm);
+  rc |= upload(o, &D.kfl, o->kfl);
+  rc |= upload(o, &D.kcpl, o->kcpl);
   const size_t n = h.n, m = h.m, nnz = h.nnz;
   rc |= dalloc(o, &D.p, B * h.np);
   rc |= dalloc(o, &D.x, B * n);
@@ -807,6 +1004,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= dalloc(o, &D.aty, B * n);
   rc |= dalloc(o, &D.step, B * n);
   rc |= dalloc(o, &D.S, B * (size_t)h.S_stride);
+  rc |= dalloc(o, &D.FS, B * (size_t)h.fs_stride);
   rc |= dalloc(o, &D.work, B * 8);
   rc |= dalloc(o, &D.info, B);
   rc |= dalloc(o, &D.t0, B);

@@ -79,6 +79,29 @@ struct PlAdmmNode {
   int ttab;  // offset (u32) of the node's lane-tile table in d.ttab (-1: more than PL_ADMM_KM slots)
 };
 
+// Per-node table of the two-stage factor (k_factor.hip).  X = ndx, U = nu, w_i = [dx_i, u_i].
+//   k_fnode  (parallel over problem x node): Kt_ii = diag(P) + sigma + sum_rows rho a a^T on w_i,
+//            then C^-1 (u block), G = C^-1 B^T (U x X) and A' = A - B G (X x X), into d.FS;
+//   k_fchain (one workgroup per problem, sequential over nodes): S_xx = (A' + E_i)^-1,
+//            S_ux = -G S_xx, S_uu = C^-1 + G S_xx G^T, E_{i+1} = D - Kc S_i Kc^T.
+// Assembly program: slot-owner streams over 256 threads, word [t][256] =
+//   e1 | FLUSH << 15 | e2 << 16 (Kt slot += rho a_e1 * a_e2; e = nent is a zero entry),
+//   flush slots (packed lower index) [f][256] in d.kfl.
+// Coupling program (u32, at cp_off in d.kcpl), every dx_{i+1} column a owned by exactly
+// one coupling row and every coupling row owning one dx_{i+1} column:
+//   crow[X] local row, cent[X] its dx_{i+1} entry, cwptr[X+1], pcl[npc] (support columns
+//   of the coupling rows' w parts), cw[] = e | p << 16 | pc << 24.
+struct PlFacNode {
+  int nw, nu, nrow, nent, ent_off, row_off, x_off, s_off, nunit, ntl;
+  int asm_off, asm_len, fl_off, fl_len;
+  int cp_off, npc;
+  int ttab;          // lane-tile table of the node's block in d.ttab (-1: none)
+  int pad;
+  long long fs_off;  // doubles: A' (X x X, full) | G (U x X) | C^-1 (U x U), row-major
+};
+#define PL_FAC_NT 256
+#define PL_FAC_MAXGROUPS 16
+
 struct PlSettings {
   double rho, sigma, alpha, eps_abs, eps_rel, eps_prim_inf, eps_dual_inf;
   int max_iter, scaling, check_termination, warm_start;
@@ -116,6 +139,11 @@ struct PlDev {
   PlAdmmNode* anodes;    // N + 1 node tables (ADMM and factor programs)
   uint16_t* aprog;       // distinct ADMM programs, concatenated
   uint16_t* fprog;       // distinct factor programs, concatenated
+  PlFacNode* fnodes;     // N + 1 (k_factor.hip)
+  uint32_t* kasm;        // factor assembly streams
+  uint16_t* kfl;         // factor flush slots
+  uint32_t* kcpl;        // factor coupling programs
+  double* FS;            // factor scratch [B][fs_stride]: A', G, C^-1 per node
   uint32_t* ttab;        // lane-tile tables [64][PL_ADMM_KM] per distinct (T, K): (I << 24) | (J << 16) | cidx
   // per problem [B][*]
   double* p;         // params
@@ -170,6 +198,11 @@ struct PlOcpHandle {
   int admm_asr;                     // A values per lane staged through registers (x 64 lanes)
   int admm_fwd_asb;                 // coupling rows too dense for registers: forward steps stage A in LDS
   int sqp_iters;                    // SQP iterations per solve (reference: 1, ocp.py:382-383)
+  long long fs_stride;              // factor scratch per problem (doubles)
+  int nfgroup;                      // k_fnode launches: consecutive nodes with one program
+  int fg_i0[PL_FAC_MAXGROUPS], fg_n[PL_FAC_MAXGROUPS], fg_lds[PL_FAC_MAXGROUPS], fg_um[PL_FAC_MAXGROUPS];
+  int fchain_lds;                   // k_fchain LDS bytes
+  int fchain_ny, fchain_ncw, fchain_gsz;  // k_fchain Y buffer, staged coupling values, staged G (doubles)
   PlSettings set;
   PlModel model;
   PlOcpConst oc;
@@ -195,6 +228,7 @@ void launch_objective(PlOcpHandle* h);
 void launch_hess(PlOcpHandle* h);
 void launch_qp_setup(PlOcpHandle* h);
 void launch_factor(PlOcpHandle* h);
+bool factor_supports_ndx(int ndx);
 void launch_admm_init(PlOcpHandle* h);
 void launch_admm(PlOcpHandle* h, int niter, int check, int it_base);
 void launch_check(PlOcpHandle* h, int it, int final_check);
