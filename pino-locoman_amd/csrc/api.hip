@@ -660,7 +660,6 @@ int build_factor_prog(pl_ocp* o) {
     const int nw = nd.nw, U = nd.nu;
     f.nw = nw; f.nu = U; f.nrow = nd.nrow; f.nent = nd.nent; f.ent_off = nd.ent_off; f.row_off = nd.row_off;
     f.x_off = nd.x_off; f.s_off = nd.s_off; f.nunit = nd.nunit; f.ntl = nd.ntile * (nd.ntile + 1) / 2;
-    f.ttab = o->anodes[i].ttab;
     if (U > 64) { pl_set_error("factor kernel: node with %d > 64 inputs", U); return -1; }
     if (nd.nent >= 0x7fff) { pl_set_error("factor kernel: node with %d entries", nd.nent); return -1; }
     const int* cp = o->colptr.data() + nd.colptr_off;
@@ -777,10 +776,10 @@ int build_factor_prog(pl_ocp* o) {
     f.fs_off = fs;
     fs += (long long)X * X + (long long)U * X + (long long)U * U;
     fs = (fs + 31) & ~31LL;
-    // k_fnode LDS: packed lower Kt (even) | max(A values x 2, G) | pivot buffer [2][64]
+    // k_fnode LDS: packed lower Kt (even) | max(A values x 2, G) | pivot buffer [2][128][4]
     const int nK = (nslot + 1) & ~1;
     const int r2 = (std::max(2 * (nd.nent + 1), U * X) + 1) & ~1;
-    lds_of[i] = (nK + r2 + 128) * 8;
+    lds_of[i] = (nK + r2 + 1024) * 8;
     um_of[i] = U <= 40 ? 40 : 64;
   }
   h.fs_stride = std::max(fs, 32LL);
@@ -800,16 +799,12 @@ int build_factor_prog(pl_ocp* o) {
   for (int g = 0; g < h.nfgroup; ++g)
     if (h.fg_lds[g] > 160 * 1024) { pl_set_error("factor kernel: node needs %d bytes of LDS", h.fg_lds[g]); return -1; }
   // k_fchain LDS: packed lower S (even) | Y / transpose buffer | E | pivot buffer |
-  // staged coupling values (ncw + 2 X) | staged G (U x X) | staged C^-1 (packed lower)
+  // staged coupling values (ncw + 2 X) | timing stamps
   const int nS = (h.nw_max * (h.nw_max + 1) / 2 + 1) & ~1;
   const int ny = (std::max(npc_max * X, X * (X + 1)) + 1) & ~1;
   h.fchain_ny = ny;
   h.fchain_ncw = (ncw_max + 1) & ~1;
-  int umax = 0;
-  for (int i = 0; i <= N; ++i) umax = std::max(umax, o->nodes[i].nu);
-  h.fchain_gsz = (umax * X + 1) & ~1;
-  const int csz = (umax * (umax + 1) / 2 + 1) & ~1;
-  h.fchain_lds = (nS + ny + X * X + 128 + h.fchain_ncw + 2 * X + h.fchain_gsz + csz) * 8;
+  h.fchain_lds = (nS + ny + X * X + 1024 + h.fchain_ncw + 2 * X + 10) * 8;  // + timing stamps
   if (h.fchain_lds > 160 * 1024) { pl_set_error("factor kernel: chain needs %d bytes of LDS", h.fchain_lds); return -1; }
   if (o->kasm.empty()) o->kasm.assign(NT, 0);
   if (o->kcpl.empty()) o->kcpl.assign(4, 0);

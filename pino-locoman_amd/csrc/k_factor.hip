@@ -64,6 +64,108 @@ __device__ __forceinline__ double rcp_nr(double p) {
   return r;
 }
 
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// v_mfma_f64_16x16x4_f64 (tools/native/mfma_f64_check.hip pins the layout): lane l
+// supplies A[l & 15][l >> 4] and B[l >> 4][l & 15]; D register r of lane l is
+// D[(l >> 4) + 4 r][l & 15].
+__device__ __forceinline__ f64x4 mfma4(double a, double b, f64x4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Blocked sweep of the first 4 nblocks pivots of a symmetric matrix whose columns are
+// held one per lane (R rows in registers), four pivots P = [k, k + 4) per block:
+//   Q = M_PP^-1;  non-pivot column j: t = Q M_Pj, M_rj -= M_rP t, M_Pj = t;
+//   pivot column j = k + q: M_rj = (M_rP Q)_q, M_Pj = -Q_:q.
+// After all pivots the swept block holds -M^-1 (Schur complements / G elsewhere).
+// The loop is rolled (small code: the instruction cache holds it) and the register
+// column rotates by four rows per block, so the current pivot rows are always
+// col[0..3]: at block B, col[r] holds row (r + 4 B) mod R.  The publishing wave
+// writes its pivot-row entries (M_{k+p, l} = M_{l, k+p} by symmetry) twice, at lane l
+// and lane l + R, so row (r + k) needs no modulo.  pb: 2 x [2 R_pub][4] doubles.
+// kSync: 0 = one wave (wave-scope fence), 1 = workgroup barrier (publisher and
+// readers are different waves; every wave of the group must call).
+template <int R, int kSync, int kBatch>
+__device__ __forceinline__ void sweep_rot(double (&col)[R], double* pb, int pbstride, int l, int nblocks,
+                                          bool publish, bool active, bool pivcols) {
+#pragma unroll 1
+  for (int B = 0; B < nblocks; ++B) {
+    const int k = 4 * B;
+    double* pk = pb + (B & 1) * pbstride;
+    if (publish && l < R) {  // lanes past R hold no row of the swept block
+      const double2 v0 = make_double2(col[0], col[1]), v1 = make_double2(col[2], col[3]);
+      double2* pw = reinterpret_cast<double2*>(pk + 4 * l);
+      pw[0] = v0;
+      pw[1] = v1;
+      double2* pw2 = reinterpret_cast<double2*>(pk + 4 * (l + R));
+      pw2[0] = v0;
+      pw2[1] = v1;
+    }
+    if constexpr (kSync == 0) wsync();
+    else __syncthreads();
+    if (active) {
+      const double2* pr = reinterpret_cast<const double2*>(pk + 4 * k);  // row k + r at pr[2 r]
+      double m[4][4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const double2 a = pr[2 * p], b = pr[2 * p + 1];
+        m[p][0] = a.x; m[p][1] = a.y; m[p][2] = b.x; m[p][3] = b.y;
+      }
+      // m <- -M_PP^-1 (4-pivot sweep, wave-uniform values)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const double pinv = rcp_nr(m[p][p]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (r != p && c != p) m[r][c] = fma(-m[r][p] * pinv, m[p][c], m[r][c]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (r != p) { m[r][p] *= pinv; m[p][r] *= pinv; }
+        m[p][p] = -pinv;
+      }
+      // branch-free: e_s = [q == s] on pivot lanes (0 elsewhere), pv = [pivot lane]
+      const int q = l - k;
+      const bool piv = pivcols && (unsigned)q < 4u;
+      const double pv = piv ? 1.0 : 0.0;
+      double e[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) e[p] = (piv && q == p) ? 1.0 : 0.0;
+      double t[4], nb[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const double qf = -(m[p][0] * col[0] + m[p][1] * col[1] + m[p][2] * col[2] + m[p][3] * col[3]);
+        const double qcol = m[p][0] * e[0] + m[p][1] * e[1] + m[p][2] * e[2] + m[p][3] * e[3];  // -Q_pq
+        nb[p] = fma(1.0 - pv, qf, qcol);
+        t[p] = nb[p] + e[p];
+      }
+      // rank-4 update of the other rows, rotated into place: col[r - 4] <- row r, the
+      // broadcast reads issued kBatch rows at a time (registers vs. latency), two-deep chains
+#pragma unroll
+      for (int r0 = 4; r0 < R; r0 += kBatch) {
+        double2 ra[kBatch], rb[kBatch];
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j)
+          if (r0 + j < R) {
+            ra[j] = pr[2 * (r0 + j)];
+            rb[j] = pr[2 * (r0 + j) + 1];
+          }
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j)
+          if (r0 + j < R) {
+            const double h0 = fma(ra[j].y, t[1], ra[j].x * t[0]);
+            const double h1 = fma(rb[j].y, t[3], rb[j].x * t[2]);
+            col[r0 + j - 4] = col[r0 + j] - (h0 + h1);
+          }
+        if (kBatch < R) __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) col[R - 4 + p] = nb[p];
+    }
+  }
+}
+
 typedef const __attribute__((address_space(4))) PlFacNode* CFac;
 typedef const __attribute__((address_space(4))) uint32_t* CU32;
 typedef const __attribute__((address_space(4))) double* CF64;
@@ -78,7 +180,8 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
   const int task = blockIdx.x;
   const int b = task / ni;
   const int i = i0 + (task - b * ni);
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int tid = threadIdx.x, l = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
   CFac fn = (CFac)d.fnodes + i;
   const int nw = fn->nw, U = fn->nu, nent = fn->nent;
   const int nK = (nw * (nw + 1) / 2 + 1) & ~1;
@@ -132,28 +235,22 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
     double col[UM];
     if (w == 0) {
 #pragma unroll
-      for (int r = 0; r < UM; ++r) col[r] = (r < U && l < U) ? K[sidx(X + r, X + l)] : (r == l ? 1.0 : 0.0);
+      for (int r = 0; r < UM; ++r) {  // clamped unconditional loads, then select (no per-element branches)
+        const double v = K[sidx(X + min(r, U - 1), X + min(l, U - 1))];
+        // arithmetic masks, not selects: a select lets the compiler sink each load
+        // into its own branch (one serialised round trip per element)
+        col[r] = fma(v, (r < U && l < U) ? 1.0 : 0.0, (r == l && l >= U) ? 1.0 : 0.0);
+      }
     } else if (w == 1) {
 #pragma unroll
-      for (int r = 0; r < UM; ++r) col[r] = (r < U && l < X) ? K[lidx(X + r, l)] : 0.0;
-    }
-    // pivots k >= U meet an identity pad (wave 0) and zero rows (wave 1): no-ops
-    static_for<0, UM>([&](auto kc) {
-      constexpr int k = decltype(kc)::value;
-      double* pk = pb + (k & 1) * 64;
-      if (w == 0) pk[l] = col[k];
-      __syncthreads();
-      if (w < 2) {
-        const double pinv = 1.0 / pk[k];
-        const double f = col[k];
-        const bool piv = (w == 0 && l == k);
-        const double g = piv ? 1.0 - pinv : f * pinv;
-#pragma unroll
-        for (int r = 0; r < UM; ++r)
-          if (r != k) col[r] = fma(-pk[r], g, col[r]);
-        col[k] = piv ? -pinv : f * pinv;
+      for (int r = 0; r < UM; ++r) {
+        const double v = K[lidx(X + min(r, U - 1), min(l, X - 1))];
+        col[r] = v * ((r < U && l < X) ? 1.0 : 0.0);
       }
-    });
+    }
+    // pivots k >= U meet an identity pad (wave 0) and zero rows (wave 1): no-ops;
+    // the rotation is back to the identity once all UM / 4 blocks are swept
+    sweep_rot<UM, 1, 8>(col, pb, 8 * 64, l, UM / 4, w == 0, w < 2, w == 0);
     if (w == 0 && l < U) {
 #pragma unroll
       for (int r = 0; r < UM; ++r)
@@ -168,14 +265,36 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
     }
     __syncthreads();
   }
-  // ---- A' = A - B G (lower, written to both triangles)
-  if (l < X) {
-    for (int r = w; r < X; r += 4) {
-      if (r < l) continue;
-      double acc = K[lidx(r, l)];
-      for (int u = 0; u < U; ++u) acc = fma(-K[lidx(X + u, r)], Gs[u * X + l], acc);
-      Ag[r * X + l] = acc;
-      Ag[l * X + r] = acc;
+  // ---- A' = A - B G (X x X) on the f64 MFMA: lower 16 x 16 tiles (mt >= nt), K = U in
+  // steps of 4; written to both triangles
+  {
+    constexpr int NX = (X + 15) / 16;
+    constexpr int NTL = NX * (NX + 1) / 2;
+    const int ku = (U + 3) / 4;
+    for (int tt = w; tt < NTL; tt += 4) {
+      int mt = 0;
+      while ((mt + 1) * (mt + 2) / 2 <= tt) ++mt;
+      const int nt = tt - mt * (mt + 1) / 2;
+      const int ar = 16 * mt + (l & 15), bcol = 16 * nt + (l & 15);
+      f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+      for (int kk = 0; kk < ku; ++kk) {
+        const int u = 4 * kk + (l >> 4);
+        const int uc = min(u, U - 1);
+        const double av0 = K[lidx(X + uc, min(ar, X - 1))];
+        const double bv0 = Gs[uc * X + min(bcol, X - 1)];
+        const double av = av0 * ((u < U && ar < X) ? 1.0 : 0.0);
+        const double bv = bv0 * ((u < U && bcol < X) ? 1.0 : 0.0);
+        acc = mfma4(av, bv, acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * mt + (l >> 4) + 4 * r;
+        if (row < X && bcol < X && bcol <= row) {
+          const double v = K[lidx(row, bcol)] - acc[r];
+          Ag[row * X + bcol] = v;
+          Ag[bcol * X + row] = v;
+        }
+      }
     }
   }
 }
@@ -188,24 +307,16 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
 __device__ __forceinline__ void store_tiles(const PlDev& d, CFac fn, const double* Sl, double* Sg, int t0, int nt) {
   double* Sn = Sg + fn->s_off;
   const int nunit = fn->nunit, ntl = fn->ntl, nw = fn->nw;
-  const int tt = fn->ttab;
   const int total = nunit * 64 * 16;
   for (int o = (int)threadIdx.x - t0; o < total; o += nt) {
     const int slot = o & 1, ln = (o >> 1) & 63, j = (o >> 7) & 7, k = o >> 10;
     const int t = nunit * ln + k;
     double val = 0.0;
     if (t < ntl) {
-      int I, J;
-      if (tt >= 0) {
-        const uint32_t e = d.ttab[tt + ln * PL_ADMM_KM + k];
-        I = (int)(e >> 24);
-        J = (int)((e >> 16) & 0xff);
-      } else {
-        I = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-        while (I * (I + 1) / 2 > t) --I;
-        while ((I + 1) * (I + 2) / 2 <= t) ++I;
-        J = t - I * (I + 1) / 2;
-      }
+      int I = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+      I -= (I * (I + 1) / 2 > t);
+      I += ((I + 1) * (I + 2) / 2 <= t);
+      const int J = t - I * (I + 1) / 2;
       const int gi = 4 * I + (j >> 1), gj = 4 * J + 2 * (j & 1) + slot;
       if (gi < nw && gj < nw) val = Sl[sidx(gi, gj)];
     }
@@ -213,30 +324,31 @@ __device__ __forceinline__ void store_tiles(const PlDev& d, CFac fn, const doubl
   }
 }
 
-template <int X, bool TIMING>
+template <int X>
 __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, int S_stride, long long fs_stride,
-                                               int nwm, int ny, int ncw, int gsz) {
+                                               int nwm, int ny, int ncw) {
   const int b = blockIdx.x;
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int tid = threadIdx.x, l = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
   extern __shared__ double lds[];
   const int nS = (nwm * (nwm + 1) / 2 + 1) & ~1;
   double* Sl = lds;       // packed lower S_i
   double* Yb = Sl + nS;   // transpose buffer [X][X + 1], then Y [npc][X]
   double* Eb = Yb + ny;   // E_i [X][X]
-  double* pb = Eb + X * X;  // pivot rows [2][64]
-  double* Acw = pb + 128;   // A values of the coupling rows' w parts (ncw)
+  double* pb = Eb + X * X;  // pivot block rows [2][128][4]
+  double* Acw = pb + 1024;  // A values of the coupling rows' w parts (ncw)
   double* cv = Acw + ncw;   // rho_a A_{e_a} (X)
   double* ev = cv + X;      // A_{e_a} (X)
-  double* Gs = ev + X;      // G (U x X), staged
-  double* Cs = Gs + gsz;    // C^-1, packed lower, staged
-  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long tlast = 0;
+  // optional phase timing (thread 0, s_memtime): 8 accumulators + last stamp in LDS
+  unsigned long long* tacc = reinterpret_cast<unsigned long long*>(ev + X);
+  const bool TIMING = d.dbg != nullptr;  // optional phase timing (PL_ADMM_TIMING=1)
+  if (TIMING && tid < 9) tacc[tid] = 0;
   auto T = [&](int slot) {
-    if constexpr (TIMING) {
+    if (TIMING) {
       if (tid == 0) {
         const unsigned long long now = __builtin_amdgcn_s_memtime();
-        if (slot >= 0) tacc[slot] += now - tlast;
-        tlast = now;
+        if (slot >= 0) tacc[slot] += now - tacc[8];
+        tacc[8] = now;
       }
     }
   };
@@ -247,6 +359,7 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
     CFac fn = (CFac)d.fnodes + i;
     const int U = fn->nu;
     const double* __restrict__ Ag = FSb + fn->fs_off;
+    CF64 Gg = (CF64)(Ag + X * X);
     const double* __restrict__ Cg = Ag + X * X + U * X;
     CU32 cp = (CU32)d.kcpl + fn->cp_off;
     CU32 crow = cp;
@@ -260,55 +373,35 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
     __syncthreads();
     T(-1);
     if (w == 0) {
-      // ---- S_xx = (A' + E_i)^-1, one column per lane (identity past X)
+      // ---- S_xx = (A' + E_i)^-1, one column per lane
       double col[X];
 #pragma unroll
       for (int r = 0; r < X; ++r)
-        col[r] = l < X ? Ag[r * X + l] + Eb[r >= l ? r * X + l : l * X + r] : (r == l ? 1.0 : 0.0);
-      static_for<0, X>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        double* pk = pb + (k & 1) * 64;
-        pk[l] = col[k];
-        wsync();
-        const double2* pk2 = reinterpret_cast<const double2*>(pk);
-        double c[X];
-#pragma unroll
-        for (int r = 0; r < X / 2; ++r) {
-          const double2 v = pk2[r];
-          c[2 * r] = v.x;
-          c[2 * r + 1] = v.y;
-        }
-        const double pinv = rcp_nr(c[k]);
-        const double f = col[k];
-        const bool piv = (l == k);
-        const double g = piv ? 1.0 - pinv : f * pinv;
-#pragma unroll
-        for (int r = 0; r < X; ++r)
-          if (r != k) col[r] = fma(-c[r], g, col[r]);
-        col[k] = piv ? -pinv : f * pinv;
-      });
+      {
+        // lanes >= X duplicate column X - 1: never pivots, never published, never stored
+        const int lc = min(l, X - 1);
+        col[r] = Ag[r * X + lc] + Eb[r >= lc ? r * X + lc : lc * X + r];
+      }
+      unsigned long long ts0 = 0;
+      if (TIMING) ts0 = __builtin_amdgcn_s_memtime();
+      sweep_rot<X, 0, X>(col, pb, 8 * 64, l, X / 4, true, true, true);
+      if (TIMING) {
+        const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+        if (l == 0) tacc[5] += ts1 - ts0;
+      }
       // symmetrise -col (sweep round-off) through the transpose buffer
       constexpr int XP = X + 1;
       if (l < X) {
 #pragma unroll
         for (int r = 0; r < X; ++r) Yb[r * XP + l] = -col[r];
       }
-      wsync();
-#pragma unroll
-      for (int r = 0; r < X; ++r) col[r] = 0.5 * (Yb[l * XP + r] - col[r]);
       __syncthreads();  // (a) the other waves are done with Sl (tile store of S_{i-1})
-      if (l < X) {
-#pragma unroll
-        for (int r = 0; r < X; ++r)
-          if (r >= l) Sl[lidx(r, l)] = col[r];
-      }
+      if (l < X)
+        for (int r = l; r < X; ++r) Sl[lidx(r, l)] = 0.5 * (Yb[r * XP + l] + Yb[l * XP + r]);
     } else {
       // ---- waves 1-3, while wave 0 sweeps: store S_{i-1}, stage node i's coupling values
-      for (int k = tid - 64; k < U * X; k += NT - 64) Gs[k] = Ag[X * X + k];
-      for (int k = tid - 64; k < U * U; k += NT - 64) {
-        const int u = k / U, j = k - u * U;
-        if (u >= j) Cs[lidx(u, j)] = Cg[k];
-      }
+      unsigned long long ts0 = 0;
+      if (TIMING) ts0 = __builtin_amdgcn_s_memtime();
       if (i > 0) store_tiles(d, (CFac)d.fnodes + (i - 1), Sl, Sg, 64, NT - 64);
       if (i < N) {
         const int ncwi = (int)cwptr[X];
@@ -319,46 +412,71 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
           cv[a] = rhob[crow[a]] * ea;
         }
       }
+      if (TIMING) {
+        const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+        if (tid == 64) tacc[7] += ts1 - ts0;
+      }
       __syncthreads();  // (a)
     }
     __syncthreads();
     T(0);
-    // ---- S_ux = -G S_xx: thread (w, l) -> column l, rows u = w (mod 4); four partial
-    // sums over r (mod 4) keep the FMA chains short
-    if (l < X && U > 0) {
-      double sx[X];
+    // ---- S_ux = -G S_xx (U x X) and S_uu = C^-1 - G S_ux^T (U x U, lower) on the f64
+    // MFMA: wave w owns the 16-row tile mt = w of both; K = X in steps of 4.
+    {
+      constexpr int KX = X / 4;
+      constexpr int NX = (X + 15) / 16;
+      const int mt = w;
+      const bool act = 16 * mt < U;
+      const int arow = 16 * mt + (l & 15);
+      double ga[KX];  // G[16 mt + (l & 15)][4 kk + (l >> 4)]
 #pragma unroll
-      for (int r = 0; r < X; ++r) sx[r] = Sl[sidx(r, l)];
-      for (int u = w; u < U; u += 4) {
-        const double2* gr = reinterpret_cast<const double2*>(Gs + u * X);
-        double a[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int r = 0; r < X / 2; ++r) {
-          const double2 g = gr[r];
-          a[(2 * r) & 3] = fma(g.x, sx[2 * r], a[(2 * r) & 3]);
-          a[(2 * r + 1) & 3] = fma(g.y, sx[2 * r + 1], a[(2 * r + 1) & 3]);
-        }
-        Sl[lidx(X + u, l)] = -((a[0] + a[1]) + (a[2] + a[3]));
+      for (int kk = 0; kk < KX; ++kk) {
+        const double v = Ag[X * X + min(arow, max(U - 1, 0)) * X + 4 * kk + (l >> 4)];
+        ga[kk] = v * ((act && arow < U) ? 1.0 : 0.0);
       }
-    }
-    __syncthreads();
-    T(1);
-    // ---- S_uu = C^-1 - G S_ux^T (lower): thread (w, l) -> column l, rows u >= l, u = w (mod 4)
-    if (l < U) {
-      double wv[X];
+      if (act) {
 #pragma unroll
-      for (int r = 0; r < X; ++r) wv[r] = Sl[lidx(X + l, r)];
-      for (int u = w; u < U; u += 4) {
-        if (u < l) continue;
-        const double2* gr = reinterpret_cast<const double2*>(Gs + u * X);
-        double a[4] = {Cs[lidx(u, l)], 0.0, 0.0, 0.0};
+        for (int nt = 0; nt < NX; ++nt) {
+          f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+          const int bc = 16 * nt + (l & 15);
 #pragma unroll
-        for (int r = 0; r < X / 2; ++r) {
-          const double2 g = gr[r];
-          a[(2 * r) & 3] = fma(-g.x, wv[2 * r], a[(2 * r) & 3]);
-          a[(2 * r + 1) & 3] = fma(-g.y, wv[2 * r + 1], a[(2 * r + 1) & 3]);
+          for (int kk = 0; kk < KX; ++kk) {
+            const double bv0 = Sl[sidx(4 * kk + (l >> 4), min(bc, X - 1))];
+            const double bv = bv0 * (bc < X ? 1.0 : 0.0);
+            acc = mfma4(ga[kk], bv, acc);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * mt + (l >> 4) + 4 * r;
+            if (row < U && bc < X) Sl[lidx(X + row, bc)] = -acc[r];
+          }
         }
-        Sl[lidx(X + u, X + l)] = (a[0] + a[1]) + (a[2] + a[3]);
+      }
+      __syncthreads();
+      T(1);
+      if (act) {
+        for (int nt = 0; nt <= mt; ++nt) {
+          f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+          const int bu = 16 * nt + (l & 15);
+          double ci[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * mt + (l >> 4) + 4 * r;
+            const double v = Cg[min(row, U - 1) * U + min(bu, U - 1)];
+            ci[r] = v * ((row < U && bu <= row) ? 1.0 : 0.0);
+          }
+#pragma unroll
+          for (int kk = 0; kk < KX; ++kk) {
+            const double bv0 = Sl[lidx(X + min(bu, U - 1), 4 * kk + (l >> 4))];
+            const double bv = bv0 * (bu < U ? 1.0 : 0.0);
+            acc = mfma4(ga[kk], bv, acc);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * mt + (l >> 4) + 4 * r;
+            if (row < U && bu <= row) Sl[lidx(X + row, X + bu)] = ci[r] - acc[r];
+          }
+        }
       }
     }
     __syncthreads();
@@ -401,10 +519,10 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
     T(4);
   }
   store_tiles(d, (CFac)d.fnodes + N, Sl, Sg, 0, NT);
-  T(5);
-  if constexpr (TIMING) {
-    if (tid == 0 && d.dbg)
-      for (int k = 0; k < 6; ++k) d.dbg[(size_t)b * 16 + 16 * (size_t)gridDim.x + k] = (double)tacc[k];
+  T(6);
+  if (TIMING) {
+    if (tid == 0)
+      for (int k = 0; k < 8; ++k) d.dbg[(size_t)b * 16 + 16 * (size_t)gridDim.x + k] = (double)tacc[k];
   }
 }
 
@@ -425,20 +543,11 @@ template <int X>
 void launch_fchain(PlOcpHandle* h) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)k_fchain<X, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)k_fchain<X, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_fchain<X>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  const int nS = (h->nw_max * (h->nw_max + 1) / 2 + 1) & ~1;
-  const int ny = h->fchain_ny;
-  const int ncw = h->fchain_ncw;
-  const int gsz = h->fchain_gsz;
-  if (h->d.dbg)
-    hipLaunchKernelGGL((k_fchain<X, true>), dim3(h->B), dim3(NT), h->fchain_lds, h->stream, h->d, h->N, h->m, h->nnz,
-                       h->S_stride, h->fs_stride, h->nw_max, ny, ncw, gsz);
-  else
-    hipLaunchKernelGGL((k_fchain<X, false>), dim3(h->B), dim3(NT), h->fchain_lds, h->stream, h->d, h->N, h->m, h->nnz,
-                       h->S_stride, h->fs_stride, h->nw_max, ny, ncw, gsz);
+  hipLaunchKernelGGL((k_fchain<X>), dim3(h->B), dim3(NT), h->fchain_lds, h->stream, h->d, h->N, h->m, h->nnz,
+                     h->S_stride, h->fs_stride, h->nw_max, h->fchain_ny, h->fchain_ncw);
 }
 
 template <int X>

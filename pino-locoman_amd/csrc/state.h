@@ -95,8 +95,6 @@ struct PlFacNode {
   int nw, nu, nrow, nent, ent_off, row_off, x_off, s_off, nunit, ntl;
   int asm_off, asm_len, fl_off, fl_len;
   int cp_off, npc;
-  int ttab;          // lane-tile table of the node's block in d.ttab (-1: none)
-  int pad;
   long long fs_off;  // doubles: A' (X x X, full) | G (U x X) | C^-1 (U x U), row-major
 };
 #define PL_FAC_NT 256
@@ -202,7 +200,7 @@ struct PlOcpHandle {
   int nfgroup;                      // k_fnode launches: consecutive nodes with one program
   int fg_i0[PL_FAC_MAXGROUPS], fg_n[PL_FAC_MAXGROUPS], fg_lds[PL_FAC_MAXGROUPS], fg_um[PL_FAC_MAXGROUPS];
   int fchain_lds;                   // k_fchain LDS bytes
-  int fchain_ny, fchain_ncw, fchain_gsz;  // k_fchain Y buffer, staged coupling values, staged G (doubles)
+  int fchain_ny, fchain_ncw;        // k_fchain Y buffer and staged coupling values (doubles)
   PlSettings set;
   PlModel model;
   PlOcpConst oc;
