@@ -52,7 +52,7 @@ __device__ inline void node_inputs(const PlDev& d, const PlNode& nd, const PlNod
 
 // g, lbg, ubg at xsrc for every (problem, node).
 template <int DYN>
-__global__ void k_eval_values(PlDev d, int B, int N, int n, int m, int np, const double* __restrict__ xsrc) {
+__global__ __launch_bounds__(64) void k_eval_values(PlDev d, int B, int N, int n, int m, int np, const double* __restrict__ xsrc) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= B * N) return;
   const int b = tid / N, i = tid - b * N;
@@ -66,7 +66,8 @@ __global__ void k_eval_values(PlDev d, int B, int N, int n, int m, int np, const
   node_inputs(d, nd, nn, x, nullptr, 0.0, -1, &dx, &u, &dxn, O.ndx);
   ValueEmit e{d.g + (size_t)b * m + nd.row_off, d.lbg + (size_t)b * m + nd.row_off,
               d.ubg + (size_t)b * m + nd.row_off, 0};
-  pl::node_rows<double, DYN>(M, O, i, p, dx, u, dxn, e);
+  __shared__ double kst[PL_KIN_STORE * 64];
+  pl::node_rows<double, DYN>(M, O, i, p, dx, u, dxn, e, kst + threadIdx.x, 64);
 }
 
 // Constraint Jacobian values on the fixed pattern.  Block = one wave = (problem, node,
@@ -93,7 +94,9 @@ __global__ __launch_bounds__(64) void k_eval_jac(PlDev d, int B, int N, int n, i
   VecIn<Dual> u{x + nd.x_off + ndx, nullptr, 0.0, lc - ndx};
   VecIn<Dual> dxn{x + nn.x_off, nullptr, 0.0, lc - nd.nw};
   JacEmit e{d.rowidx + nd.ent_off, d.Araw + (size_t)b * nnz + nd.ent_off, e0, e1, 0};
-  pl::node_rows<Dual, DYN>(M, O, i, p, dx, u, dxn, e);
+  __shared__ double2 kst_raw[PL_KIN_STORE * 64];  // Dual storage (Dual has constructors)
+  Dual* kst = reinterpret_cast<Dual*>(kst_raw);
+  pl::node_rows<Dual, DYN>(M, O, i, p, dx, u, dxn, e, kst + threadIdx.x, 64);
 }
 
 // Objective f and gradient at d.x (ocp.py:80-101; ocp_whole_body_rnea.py:108-136).
@@ -241,13 +244,14 @@ __device__ void violation_at(const PlDev& d, int b, int N, int n, int np, const 
   const PlOcpConst& O = *d.oc;
   const PlModel& M = *d.model;
   ViolEmit e{0.0, 0.0};
+  __shared__ double kst[PL_KIN_STORE * 256];
   for (int i = threadIdx.x; i < N; i += blockDim.x) {
     const PlNode nd = d.nodes[i];
     const PlNode nn = d.nodes[i + 1];
     VecIn<double> dx{x + nd.x_off, step ? step + nd.x_off : nullptr, alpha, -1};
     VecIn<double> u{x + nd.x_off + O.ndx, step ? step + nd.x_off + O.ndx : nullptr, alpha, -1};
     VecIn<double> dxn{x + nn.x_off, step ? step + nn.x_off : nullptr, alpha, -1};
-    pl::node_rows<double, DYN>(M, O, i, d.p + (size_t)b * np, dx, u, dxn, e);
+    pl::node_rows<double, DYN>(M, O, i, d.p + (size_t)b * np, dx, u, dxn, e, kst + threadIdx.x, 256);
   }
   double s = e.ss, mx = e.mx;
   block_sum_max(s, mx, red);

@@ -233,24 +233,49 @@ template <class S> PL_HD void motion_cross_force(const S* v, const S* f, S* out)
   for (int k = 0; k < 3; ++k) { out[k] = a[k]; out[3 + k] = b[k] + c[k]; }
 }
 
-// Per-node kinematic/dynamic outputs requested by the row function.
+// Per-node kinematic/dynamic outputs requested by the row function.  The arrays
+// the rows index at run time (joint torques, foot velocities) live in caller
+// storage (LDS on the device, interleaved with a stride), so no thread keeps a
+// dynamically indexed register array (which the compiler would put in scratch).
+#define PL_KIN_STORE (PL_MAXV - 6 + 3 * PL_MAXFEET)  // entries of a NodeKin store
 template <class S> struct NodeKin {
-  S tau[PL_MAXV];            // RNEA torques (if want_tau)
-  S foot_vel[PL_MAXFEET][3]; // LWA linear velocity of each foot frame
-  S arm_vel[3];              // relative arm velocity rows (ocp.py:177-179)
+  S tau[6];    // RNEA base torques (if want_tau)
+  S arm_vel[3];  // relative arm velocity rows (ocp.py:177-179)
+  S* store;    // [PL_KIN_STORE] x stride: joint torques, then foot velocities
+  int stride;
+  PL_HD S& tau_j(int k) { return store[k * stride]; }                          // tau[6 + k]
+  PL_HD S& foot_vel(int e, int c) { return store[(PL_MAXV - 6 + 3 * e + c) * stride]; }  // LWA lin. vel.
+};
+
+// q / v accessors over x_init + dx (ocp_whole_body_rnea.py:173-181): the free-flyer
+// part of q comes from integrate_ff, every revolute coordinate is x_init + dx.
+template <class S, class In> struct RevQ {
+  const double* q0;
+  In dq;
+  PL_HD S operator()(int k) const { return q0[k] + dq[k - 1]; }  // revolute q index k >= 7
+};
+template <class S, class In> struct VelAcc {
+  const double* v0;
+  In dv;
+  PL_HD S operator[](int k) const { return v0[k] + dv[k]; }
+};
+template <class S> struct RevQArr {  // same interface over a full q array
+  const S* q;
+  PL_HD S operator()(int k) const { return q[k]; }
 };
 
 // One pass over the tree: RNEA with contact forces (world frame, point forces at
 // the frames in `ee`) plus foot / arm frame velocities.
 //   q, v, a: full configuration / velocity / acceleration (a unused if !want_tau)
 //   forces: 3 * nee world-frame forces (FR, FL, RR, RL[, ee])
-template <class S, class InA, class InF>
-PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* q, const S* v, const InA& a, const InF& forces,
-                     bool want_tau, bool want_vel, NodeKin<S>& out) {
+//   qb: free-flyer q[0..7); qrev(k): revolute coordinate q[k]; v[k]: velocity
+template <class S, class QR, class VA, class InA, class InF>
+PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const QR& qrev, const VA& v, const InA& a,
+                     const InF& forces, bool want_tau, bool want_vel, NodeKin<S>& out) {
   // ---- root (free-flyer, joint 1)
   S R0[9];
-  quat_to_R(q + 3, R0);
-  S p0[3] = {q[0], q[1], q[2]};
+  quat_to_R(qb + 3, R0);
+  S p0[3] = {qb[0], qb[1], qb[2]};
   S v1[6], a1[6], f1[6];
   for (int k = 0; k < 6; ++k) v1[k] = v[k];
   if (want_tau) {
@@ -297,7 +322,7 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* q, const S*
     for (int kk = 0; kk < PL_MAXCL; ++kk) {
       if (kk >= L) break;
       const int j = first + kk;
-      S qj = q[M.idx_q[j]];
+      S qj = qrev(M.idx_q[j]);
       S s, c;
       sincos_s(qj, &s, &c);
       S Rl[9];
@@ -366,7 +391,9 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* q, const S*
           S pf[3] = {S(O.feet[e].p[0]), S(O.feet[e].p[1]), S(O.feet[e].p[2])};
           cross3(vj + 3, pf, wxp);
           S lv[3] = {vj[0] + wxp[0], vj[1] + wxp[1], vj[2] + wxp[2]};
-          matvec(oRj, lv, out.foot_vel[e]);
+          S fvw[3];
+          matvec(oRj, lv, fvw);
+          for (int k = 0; k < 3; ++k) out.foot_vel(e, k) = fvw[k];
         }
         if (O.arm.valid && O.arm.joint == j) {
           S wxp[3];
@@ -391,7 +418,7 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* q, const S*
         const int j = first + kk;
         S t = sw[kk][0] * P[0] + sw[kk][1] * P[1] + sw[kk][2] * P[2] + sw[kk][3] * P[3] + sw[kk][4] * P[4] +
               sw[kk][5] * P[5];
-        out.tau[M.idx_v[j]] = t - alpha[kk];
+        out.tau_j(M.idx_v[j] - 6) = t - alpha[kk];
       }
       for (int k = 0; k < 6; ++k) Fw[k] += P[k];
     }

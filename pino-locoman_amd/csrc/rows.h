@@ -79,23 +79,29 @@ template <class S> PL_HD VecIn<S> sub_in(const VecIn<S>& a, int off) {
   return r;
 }
 
+// kstore: caller storage for the run-time indexed kinematic outputs (NodeKin,
+// PL_KIN_STORE entries spaced by kstride).
 template <class S, int DYN, class Emit>
 PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double* p, const VecIn<S>& dx,
-                     const VecIn<S>& u, const VecIn<S>& dxn, Emit& emit) {
+                     const VecIn<S>& u, const VecIn<S>& dxn, Emit& emit, S* kstore, int kstride) {
   const int nv = O.nv, nq = O.nq, nj = O.nj;
   const double* xi = p + O.P.x_init;
   const double dt = node_dt(O, p, i);
   const int type = node_type(O, i);
-  // state: q = integrate(x_init.q, dq), v = x_init.v + dv   (ocp_whole_body_rnea.py:173-181)
-  S q[PL_MAXQ], v[PL_MAXV];
-  integrate_q<S>(M, xi, dx, q);
-  for (int k = 0; k < nv; ++k) v[k] = xi[nq + k] + dx[nv + k];
+  // state: q = integrate(x_init.q, dq), v = x_init.v + dv   (ocp_whole_body_rnea.py:173-181);
+  // the free-flyer part of q in registers, the rest read through accessors
+  S qb[7];
+  integrate_ff<S>(xi, dx, qb);
+  const RevQ<S, VecIn<S>> qrev{xi, dx};
+  const VelAcc<S, VecIn<S>> vel{xi + nq, sub_in(dx, nv)};
   const int f_off = (DYN == PL_DYN_RNEA) ? O.na : (DYN == PL_DYN_ACC ? nv : nj);
   const VecIn<S> a = u;                                   // rnea / acc: a = u[0:nv]
   const VecIn<S> forces = sub_in(u, f_off);
   const VecIn<S> tau_j = sub_in(u, DYN == PL_DYN_RNEA ? O.na + O.nf : 0);
   const bool state_rows = (type != 0);
   NodeKin<S> kin;
+  kin.store = kstore;
+  kin.stride = kstride;
   constexpr bool want_tau = (DYN != PL_DYN_ABA);
   // A Jacobian column seeded on dx_{i+1}, or (rnea) on tau_j, has a zero tangent in the
   // tree pass and the ABA: every row that reads them then has a zero derivative, so
@@ -106,12 +112,22 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
     const bool seed_tau = DYN == PL_DYN_RNEA && u.seed >= O.na + O.nf && u.seed < O.na + O.nf + nj;
     tree = !(seed_dxn || seed_tau);
   }
-  if (tree && (want_tau || state_rows)) tree_pass<S>(M, O, q, v, a, forces, want_tau, state_rows, kin);
+  if (tree && (want_tau || state_rows)) {
+    tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin);
+  } else {  // a skipped pass leaves zero (value and tangent) kinematic outputs
+    for (int k = 0; k < PL_KIN_STORE; ++k) kin.store[k * kstride] = S(0.0);
+  }
   S aba_a[DYN == PL_DYN_ABA ? PL_MAXV : 1];
   if constexpr (DYN == PL_DYN_ABA) {
-    if (tree) aba_forward<S>(M, O, q, v, tau_j, forces, aba_a);
-    else
+    if (tree) {
+      S q[PL_MAXQ], v[PL_MAXV];
+      for (int k = 0; k < 7; ++k) q[k] = qb[k];
+      for (int k = 7; k < nq; ++k) q[k] = qrev(k);
+      for (int k = 0; k < nv; ++k) v[k] = vel[k];
+      aba_forward<S>(M, O, q, v, tau_j, forces, aba_a);
+    } else {
       for (int k = 0; k < nv; ++k) aba_a[k] = S(0.0);
+    }
   }
 
   const int nb = O.nblk[type];
@@ -123,7 +139,7 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
         for (int r = 0; r < O.ndx; ++r) emit(dx[r], 0.0, 0.0);
         break;
       case PL_RB_DYNQ:
-        for (int r = 0; r < nv; ++r) emit(dxn[r] - (dx[r] + v[r] * dt), 0.0, 0.0);
+        for (int r = 0; r < nv; ++r) emit(dxn[r] - (dx[r] + vel[r] * dt), 0.0, 0.0);
         break;
       case PL_RB_DYNV:
         for (int r = 0; r < nv; ++r) {
@@ -137,7 +153,7 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
         for (int r = 0; r < 6; ++r) emit(kin.tau[r], 0.0, 0.0);
         break;
       case PL_RB_TAU_EQ:
-        for (int r = 0; r < nj; ++r) emit(kin.tau[6 + r] - tau_j[r], 0.0, 0.0);
+        for (int r = 0; r < nj; ++r) emit(kin.tau_j(r) - tau_j[r], 0.0, 0.0);
         break;
       case PL_RB_TAU_BND:
         for (int r = 0; r < nj; ++r) emit(tau_j[r], -O.tau_max[r], O.tau_max[r]);
@@ -157,15 +173,15 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
       } break;
       case PL_RB_FVXY: {
         double c = p[O.P.contact + 4 * i + k];
-        emit(c * kin.foot_vel[k][0], 0.0, 0.0);
-        emit(c * kin.foot_vel[k][1], 0.0, 0.0);
+        emit(c * kin.foot_vel(k, 0), 0.0, 0.0);
+        emit(c * kin.foot_vel(k, 1), 0.0, 0.0);
       } break;
       case PL_RB_FVZ: {
         double c = p[O.P.contact + 4 * i + k];
         double ph = p[O.P.swing + 4 * i + k];
         double vz_des = spline_vel_z(ph, p[O.P.swing_period], p[O.P.swing_height], p[O.P.swing_vel_limits],
                                      p[O.P.swing_vel_limits + 1]);
-        S vz = kin.foot_vel[k][2];
+        S vz = kin.foot_vel(k, 2);
         emit(c * vz + (1.0 - c) * (vz - vz_des), 0.0, 0.0);
       } break;
       case PL_RB_EXT:
@@ -175,10 +191,10 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
         for (int r = 0; r < 3; ++r) emit(kin.arm_vel[r] - p[O.P.arm_vel_des + r], 0.0, 0.0);
         break;
       case PL_RB_QJ:
-        for (int r = 0; r < nj; ++r) emit(q[7 + r], O.pos_min[r], O.pos_max[r]);
+        for (int r = 0; r < nj; ++r) emit(qrev(7 + r), O.pos_min[r], O.pos_max[r]);
         break;
       case PL_RB_VJ:
-        for (int r = 0; r < nj; ++r) emit(v[6 + r], -O.vel_max[r], O.vel_max[r]);
+        for (int r = 0; r < nj; ++r) emit(vel[6 + r], -O.vel_max[r], O.vel_max[r]);
         break;
     }
   }

@@ -20,13 +20,15 @@ int run(const PlModel& M, const PlOcpConst& O, int i, const double* p, const dou
   if (seed < 0) {
     pl::VecIn<double> a{dx, nullptr, 0.0, -1}, b{u, nullptr, 0.0, -1}, c{dxn, nullptr, 0.0, -1};
     VEmit e{g, lb, ub, 0};
-    pl::node_rows<double, DYN>(M, O, i, p, a, b, c, e);
+    double kst[PL_KIN_STORE];
+    pl::node_rows<double, DYN>(M, O, i, p, a, b, c, e, kst, 1);
     return e.r;
   }
   const int ndx = O.ndx, nw = ndx + pl::node_nu(O, i);
   pl::VecIn<Dual> a{dx, nullptr, 0.0, seed}, b{u, nullptr, 0.0, seed - ndx}, c{dxn, nullptr, 0.0, seed - nw};
   DEmit e{tan, 0};
-  pl::node_rows<Dual, DYN>(M, O, i, p, a, b, c, e);
+  Dual kst[PL_KIN_STORE];
+  pl::node_rows<Dual, DYN>(M, O, i, p, a, b, c, e, kst, 1);
   return e.r;
 }
 }  // namespace
