@@ -94,7 +94,7 @@ __global__ __launch_bounds__(64) void k_eval_jac(PlDev d, int B, int N, int n, i
   VecIn<Dual> u{x + nd.x_off + ndx, nullptr, 0.0, lc - ndx};
   VecIn<Dual> dxn{x + nn.x_off, nullptr, 0.0, lc - nd.nw};
   JacEmit e{d.rowidx + nd.ent_off, d.Araw + (size_t)b * nnz + nd.ent_off, e0, e1, 0};
-  __shared__ double2 kst_raw[PL_KIN_STORE * 64];  // Dual storage (Dual has constructors)
+  __shared__ double2 kst_raw[PL_KIN_STORE_DUAL * 64];  // Dual storage (Dual has constructors)
   Dual* kst = reinterpret_cast<Dual*>(kst_raw);
   pl::node_rows<Dual, DYN>(M, O, i, p, dx, u, dxn, e, kst + threadIdx.x, 64);
 }
@@ -244,14 +244,14 @@ __device__ void violation_at(const PlDev& d, int b, int N, int n, int np, const 
   const PlOcpConst& O = *d.oc;
   const PlModel& M = *d.model;
   ViolEmit e{0.0, 0.0};
-  __shared__ double kst[PL_KIN_STORE * 256];
-  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+  __shared__ double kst[PL_KIN_STORE * 64];
+  for (int i = threadIdx.x; threadIdx.x < 64 && i < N; i += 64) {  // nodes on the first wave
     const PlNode nd = d.nodes[i];
     const PlNode nn = d.nodes[i + 1];
     VecIn<double> dx{x + nd.x_off, step ? step + nd.x_off : nullptr, alpha, -1};
     VecIn<double> u{x + nd.x_off + O.ndx, step ? step + nd.x_off + O.ndx : nullptr, alpha, -1};
     VecIn<double> dxn{x + nn.x_off, step ? step + nn.x_off : nullptr, alpha, -1};
-    pl::node_rows<double, DYN>(M, O, i, d.p + (size_t)b * np, dx, u, dxn, e, kst + threadIdx.x, 256);
+    pl::node_rows<double, DYN>(M, O, i, d.p + (size_t)b * np, dx, u, dxn, e, kst + threadIdx.x, 64);
   }
   double s = e.ss, mx = e.mx;
   block_sum_max(s, mx, red);

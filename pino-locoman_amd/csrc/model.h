@@ -13,7 +13,7 @@
 #define PL_MAXQ 28
 #define PL_MAXV 28
 #define PL_MAXCHAIN 8
-#define PL_MAXCL 8      // longest chain (Z1 arm: 6)
+#define PL_MAXCL 6      // longest chain (Z1 arm: 6)
 #define PL_MAXNJ 32     // actuated joints
 #define PL_MAXFEET 4
 #define PL_MAXNU 128

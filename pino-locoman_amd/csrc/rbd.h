@@ -16,6 +16,8 @@
 // (prefix projection, sin, cos) stay live across the chain, which keeps the
 // dual-number Jacobian kernel in registers.
 #pragma once
+#include <type_traits>
+
 #include "ad.h"
 #include "model.h"
 
@@ -237,14 +239,18 @@ template <class S> PL_HD void motion_cross_force(const S* v, const S* f, S* out)
 // the rows index at run time (joint torques, foot velocities) live in caller
 // storage (LDS on the device, interleaved with a stride), so no thread keeps a
 // dynamically indexed register array (which the compiler would put in scratch).
-#define PL_KIN_STORE (PL_MAXV - 6 + 3 * PL_MAXFEET)  // entries of a NodeKin store
+#define PL_KIN_STORE (PL_MAXV - 6 + 3 * PL_MAXFEET + 7 * PL_MAXCL)  // entries of a NodeKin store
+#define PL_KIN_STORE_DUAL (PL_MAXV - 6 + 3 * PL_MAXFEET)           // without the chain scratch
 template <class S> struct NodeKin {
   S tau[6];    // RNEA base torques (if want_tau)
   S arm_vel[3];  // relative arm velocity rows (ocp.py:177-179)
-  S* store;    // [PL_KIN_STORE] x stride: joint torques, then foot velocities
+  S* store;    // [PL_KIN_STORE] x stride: joint torques, foot velocities, chain scratch
   int stride;
   PL_HD S& tau_j(int k) { return store[k * stride]; }                          // tau[6 + k]
   PL_HD S& foot_vel(int e, int c) { return store[(PL_MAXV - 6 + 3 * e + c) * stride]; }  // LWA lin. vel.
+  // per joint of the current chain: world motion subspace S_w (6) and S_w . prefix
+  PL_HD S& sw(int kk, int c) { return store[(PL_MAXV - 6 + 3 * PL_MAXFEET + 7 * kk + c) * stride]; }
+  PL_HD S& alpha(int kk) { return store[(PL_MAXV - 6 + 3 * PL_MAXFEET + 7 * kk + 6) * stride]; }
 };
 
 // q / v accessors over x_init + dx (ocp_whole_body_rnea.py:173-181): the free-flyer
@@ -316,8 +322,18 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
     for (int k = 0; k < 3; ++k) op[k] = p0[k];
     S P[6];
     for (int k = 0; k < 6; ++k) P[k] = S(0.0);
-    S alpha[PL_MAXCL];
-    S sw[PL_MAXCL][6];
+    // chain scratch (S_w, S_w . prefix per joint): registers for the dual-number
+    // Jacobian (LDS there is the occupancy limit), the NodeKin store for values
+    constexpr bool kRegSw = !std::is_same<S, double>::value;
+    S swr[kRegSw ? PL_MAXCL : 1][6], alr[kRegSw ? PL_MAXCL : 1];
+    auto SW = [&](int kk, int c) -> S& {
+      if constexpr (kRegSw) return swr[kk][c];
+      else return out.sw(kk, c);
+    };
+    auto AL = [&](int kk) -> S& {
+      if constexpr (kRegSw) return alr[kk];
+      else return out.alpha(kk);
+    };
 #pragma unroll
     for (int kk = 0; kk < PL_MAXCL; ++kk) {
       if (kk >= L) break;
@@ -378,9 +394,8 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
         matvec(oRj, ax, wax);
         S lax[3];
         cross3(opj, wax, lax);
-        for (int k = 0; k < 3; ++k) { sw[kk][k] = lax[k]; sw[kk][3 + k] = wax[k]; }
-        alpha[kk] = sw[kk][0] * P[0] + sw[kk][1] * P[1] + sw[kk][2] * P[2] + sw[kk][3] * P[3] + sw[kk][4] * P[4] +
-                    sw[kk][5] * P[5];
+        for (int k = 0; k < 3; ++k) { SW(kk, k) = lax[k]; SW(kk, 3 + k) = wax[k]; }
+        AL(kk) = lax[0] * P[0] + lax[1] * P[1] + lax[2] * P[2] + wax[0] * P[3] + wax[1] * P[4] + wax[2] * P[5];
         for (int k = 0; k < 6; ++k) P[k] += fwj[k];
         for (int k = 0; k < 6; ++k) pa[k] = aj[k];
       }
@@ -416,9 +431,9 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
       for (int kk = 0; kk < PL_MAXCL; ++kk) {
         if (kk >= L) break;
         const int j = first + kk;
-        S t = sw[kk][0] * P[0] + sw[kk][1] * P[1] + sw[kk][2] * P[2] + sw[kk][3] * P[3] + sw[kk][4] * P[4] +
-              sw[kk][5] * P[5];
-        out.tau_j(M.idx_v[j] - 6) = t - alpha[kk];
+        S t = SW(kk, 0) * P[0] + SW(kk, 1) * P[1] + SW(kk, 2) * P[2] + SW(kk, 3) * P[3] + SW(kk, 4) * P[4] +
+              SW(kk, 5) * P[5];
+        out.tau_j(M.idx_v[j] - 6) = t - AL(kk);
       }
       for (int k = 0; k < 6; ++k) Fw[k] += P[k];
     }

@@ -115,7 +115,7 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
   if (tree && (want_tau || state_rows)) {
     tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin);
   } else {  // a skipped pass leaves zero (value and tangent) kinematic outputs
-    for (int k = 0; k < PL_KIN_STORE; ++k) kin.store[k * kstride] = S(0.0);
+    for (int k = 0; k < PL_KIN_STORE_DUAL; ++k) kin.store[k * kstride] = S(0.0);
   }
   S aba_a[DYN == PL_DYN_ABA ? PL_MAXV : 1];
   if constexpr (DYN == PL_DYN_ABA) {
