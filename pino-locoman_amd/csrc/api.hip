@@ -40,6 +40,8 @@ struct pl_ocp {
   bool on_device;
   std::vector<PlNode> nodes;
   std::vector<int> colptr, rowidx, entcol, rowptr, rowent, cplrow, rownode, colnode;
+  std::vector<int> gr_ptr, gc_ptr;    // global CSR / CSC of the whole A (k_check)
+  std::vector<int2> gr_ec, gc_er;     // (entry, global column) / (entry, global row)
   std::vector<PlAdmmNode> anodes;
   std::vector<uint16_t> aprog, fprog;
   std::vector<uint32_t> ttab;
@@ -362,6 +364,42 @@ int build_layout(pl_ocp* o) {
     const PlNode& nd = o->nodes[i];
     for (int r = 0; r < nd.nrow; ++r) o->rownode[nd.row_off + r] = i;
     for (int c = 0; c < nd.nw; ++c) o->colnode[nd.x_off + c] = i;
+  }
+  // global CSR and CSC with flattened (entry, index) pairs: entries of a column in the
+  // order of its own node, then of the previous node (dx_{i+1} part)
+  o->gr_ptr.assign(1, 0);
+  o->gr_ec.clear();
+  for (int i = 0; i <= N; ++i) {
+    const PlNode& nd = o->nodes[i];
+    for (int r = 0; r < nd.nrow; ++r) {
+      for (int q = o->rowptr[nd.rowptr_off + r]; q < o->rowptr[nd.rowptr_off + r + 1]; ++q) {
+        const int e = o->rowent[nd.csr_off + q];
+        const int lc = o->entcol[nd.ent_off + e];
+        const int j = lc < nd.nw ? nd.x_off + lc : o->nodes[i + 1].x_off + (lc - nd.nw);
+        o->gr_ec.push_back(make_int2(nd.ent_off + e, j));
+      }
+      o->gr_ptr.push_back((int)o->gr_ec.size());
+    }
+  }
+  o->gc_ptr.assign(1, 0);
+  o->gc_er.clear();
+  for (int i = 0; i <= N; ++i) {
+    const PlNode& nd = o->nodes[i];
+    for (int lc = 0; lc < nd.nw; ++lc) {
+      if (i < N) {
+        const int* cp = o->colptr.data() + nd.colptr_off;
+        for (int e = cp[lc]; e < cp[lc + 1]; ++e)
+          o->gc_er.push_back(make_int2(nd.ent_off + e, nd.row_off + o->rowidx[nd.ent_off + e]));
+      }
+      if (i > 0 && lc < ndx) {
+        const PlNode& np_ = o->nodes[i - 1];
+        const int* cp = o->colptr.data() + np_.colptr_off;
+        const int c = np_.nw + lc;
+        for (int e = cp[c]; e < cp[c + 1]; ++e)
+          o->gc_er.push_back(make_int2(np_.ent_off + e, np_.row_off + o->rowidx[np_.ent_off + e]));
+      }
+      o->gc_ptr.push_back((int)o->gc_er.size());
+    }
   }
   return 0;
 }
@@ -961,6 +999,10 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= upload(o, &D.cplrow, o->cplrow);
   rc |= upload(o, &D.rownode, o->rownode);
   rc |= upload(o, &D.colnode, o->colnode);
+  rc |= upload(o, &D.gr_ptr, o->gr_ptr);
+  rc |= upload(o, &D.gr_ec, o->gr_ec);
+  rc |= upload(o, &D.gc_ptr, o->gc_ptr);
+  rc |= upload(o, &D.gc_er, o->gc_er);
   rc |= upload(o, &D.anodes, o->anodes);
   rc |= upload(o, &D.aprog, o->aprog);
   rc |= upload(o, &D.fprog, o->fprog);

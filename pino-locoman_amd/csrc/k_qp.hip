@@ -50,10 +50,6 @@ __device__ __forceinline__ double limit_scaling(double v) {
   return v > PL_MAX_SCALING ? PL_MAX_SCALING : v;
 }
 
-__device__ __forceinline__ int gcol(const PlNode* nodes, int i, int lc) {
-  const PlNode& nd = nodes[i];
-  return lc < nd.nw ? nd.x_off + lc : nodes[i + 1].x_off + (lc - nd.nw);
-}
 
 // block reductions over 256 threads
 __device__ double block_max(double v, double* red) {
@@ -67,6 +63,23 @@ __device__ double block_max(double v, double* red) {
   __syncthreads();
   return r;
 }
+// max of K values per thread in one reduction (red: K x RS doubles, RS >= blockDim.x)
+template <int K, int RS>
+__device__ void block_max_k(double (&v)[K], double* red) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) red[k * RS + threadIdx.x] = v[k];
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) red[k * RS + threadIdx.x] = fmax(red[k * RS + threadIdx.x], red[k * RS + threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = red[k * RS];
+  __syncthreads();
+}
 __device__ double block_sum(double v, double* red) {
   red[threadIdx.x] = v;
   __syncthreads();
@@ -77,40 +90,6 @@ __device__ double block_sum(double v, double* red) {
   double r = red[0];
   __syncthreads();
   return r;
-}
-
-// Iterate the entries of global column j: fn(entry index in the problem's A
-// array, global row).
-template <class F>
-__device__ void for_col_entries(const PlDev& d, int N, int j, F fn) {
-  const int i = d.colnode[j];
-  const PlNode* nodes = d.nodes;
-  const int lc = j - nodes[i].x_off;
-  if (i < N) {
-    const PlNode& nd = nodes[i];
-    const int* cp = d.colptr + nd.colptr_off;
-    for (int e = cp[lc]; e < cp[lc + 1]; ++e) fn(nd.ent_off + e, nd.row_off + d.rowidx[nd.ent_off + e]);
-  }
-  if (i > 0 && lc < d.oc->ndx) {
-    const PlNode& np_ = nodes[i - 1];
-    const int* cp = d.colptr + np_.colptr_off;
-    const int c = np_.nw + lc;
-    for (int e = cp[c]; e < cp[c + 1]; ++e) fn(np_.ent_off + e, np_.row_off + d.rowidx[np_.ent_off + e]);
-  }
-}
-
-// Iterate the entries of global row r: fn(entry index, global column).
-template <class F>
-__device__ void for_row_entries(const PlDev& d, int r, F fn) {
-  const int i = d.rownode[r];
-  const PlNode& nd = d.nodes[i];
-  const int lr = r - nd.row_off;
-  const int* rp = d.rowptr + nd.rowptr_off;
-  const int* re = d.rowent + nd.csr_off;
-  for (int s = rp[lr]; s < rp[lr + 1]; ++s) {
-    const int e = re[s];
-    fn(nd.ent_off + e, gcol(d.nodes, i, d.entcol[nd.ent_off + e]));
-  }
 }
 
 }  // namespace
@@ -345,7 +324,10 @@ __global__ __launch_bounds__(256) void k_admm_init(PlDev d, int N, int n, int m,
   double* rhs = d.rhs + (size_t)b * n;
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
     double acc = sigma * xa[j] - qs[j];
-    for_col_entries(d, N, j, [&](int e, int r) { acc += As[e] * (rho[r] * za[r] - ya[r]); });
+    for (int q = d.gc_ptr[j]; q < d.gc_ptr[j + 1]; ++q) {
+      const int2 er = d.gc_er[q];
+      acc += As[er.x] * (rho[er.y] * za[er.y] - ya[er.y]);
+    }
     rhs[j] = acc;
   }
 }
@@ -358,11 +340,13 @@ void launch_admm_init(PlOcpHandle* h) {
 // ---------------------------------------------------------------------------
 // Termination (OSQP 0.6 update_info + check_termination, incl. infeasibility
 // certificates and the x10 "approximate" check at max_iter).
-__global__ __launch_bounds__(256) void k_check(PlDev d, int N, int n, int m, int nnz, PlSettings st, int final_check) {
+constexpr int CHECK_NT = 1024;  // rows / columns of one problem spread over 16 waves
+__global__ __launch_bounds__(CHECK_NT) void k_check(PlDev d, int N, int n, int m, int nnz, PlSettings st,
+                                                     int final_check) {
   const int b = blockIdx.x;
   PlProbInfo* info = d.info + b;
   if (info->done) return;
-  __shared__ double red[256];
+  __shared__ double red[4 * CHECK_NT];
   const double* As = d.As + (size_t)b * nnz;
   const double* za = d.za + (size_t)b * m;
   const double* ya = d.ya + (size_t)b * m;
@@ -375,36 +359,43 @@ __global__ __launch_bounds__(256) void k_check(PlDev d, int N, int n, int m, int
   const double* us = d.us + (size_t)b * m;
   const double* dxs = d.dxs + (size_t)b * n;
   const double* dys = d.dys + (size_t)b * m;
+  const int* __restrict__ gr_ptr = d.gr_ptr;
+  const int2* __restrict__ gr_ec = d.gr_ec;
+  const int* __restrict__ gc_ptr = d.gc_ptr;
+  const int2* __restrict__ gc_er = d.gc_er;
   const double c = d.cs[b], cinv = 1.0 / c;
   // primal: ||E^-1 (A x - z)||, ||E^-1 z||, ||E^-1 A x||
-  double pri = 0.0, nz = 0.0, nax = 0.0;
+  double pv[3] = {0.0, 0.0, 0.0};
   for (int r = threadIdx.x; r < m; r += blockDim.x) {
     double ax = 0.0;
-    for_row_entries(d, r, [&](int e, int j) { ax += As[e] * xa[j]; });
+    for (int s = gr_ptr[r]; s < gr_ptr[r + 1]; ++s) {
+      const int2 ej = gr_ec[s];
+      ax += As[ej.x] * xa[ej.y];
+    }
     const double ei = 1.0 / E[r];
-    pri = fmax(pri, fabs(ei * (ax - za[r])));
-    nz = fmax(nz, fabs(ei * za[r]));
-    nax = fmax(nax, fabs(ei * ax));
+    pv[0] = fmax(pv[0], fabs(ei * (ax - za[r])));
+    pv[1] = fmax(pv[1], fabs(ei * za[r]));
+    pv[2] = fmax(pv[2], fabs(ei * ax));
   }
-  pri = block_max(pri, red);
-  nz = block_max(nz, red);
-  nax = block_max(nax, red);
+  block_max_k<3, CHECK_NT>(pv, red);
+  const double pri = pv[0], nz = pv[1], nax = pv[2];
   // dual: c^-1 ||D^-1 (P x + q + A^T y)||, ||D^-1 q||, ||D^-1 A^T y||, ||D^-1 P x||
-  double dua = 0.0, nq = 0.0, naty = 0.0, npx = 0.0;
+  double dv[4] = {0.0, 0.0, 0.0, 0.0};
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
     double aty = 0.0;
-    for_col_entries(d, N, j, [&](int e, int r) { aty += As[e] * ya[r]; });
+    for (int s = gc_ptr[j]; s < gc_ptr[j + 1]; ++s) {
+      const int2 er = gc_er[s];
+      aty += As[er.x] * ya[er.y];
+    }
     const double di = 1.0 / D[j];
     const double px = Ps[j] * xa[j];
-    dua = fmax(dua, fabs(di * (px + qs[j] + aty)));
-    nq = fmax(nq, fabs(di * qs[j]));
-    naty = fmax(naty, fabs(di * aty));
-    npx = fmax(npx, fabs(di * px));
+    dv[0] = fmax(dv[0], fabs(di * (px + qs[j] + aty)));
+    dv[1] = fmax(dv[1], fabs(di * qs[j]));
+    dv[2] = fmax(dv[2], fabs(di * aty));
+    dv[3] = fmax(dv[3], fabs(di * px));
   }
-  dua = cinv * block_max(dua, red);
-  nq = block_max(nq, red);
-  naty = block_max(naty, red);
-  npx = block_max(npx, red);
+  block_max_k<4, CHECK_NT>(dv, red);
+  const double dua = cinv * dv[0], nq = dv[1], naty = dv[2], npx = dv[3];
   __shared__ int s_status;
   for (int pass = 0; pass < (final_check ? 2 : 1); ++pass) {
     const bool approx = (pass == 1);
@@ -438,14 +429,15 @@ __global__ __launch_bounds__(256) void k_check(PlDev d, int N, int n, int m, int
           double natdy = 0.0;
           for (int j = threadIdx.x; j < n; j += blockDim.x) {
             double s = 0.0;
-            for_col_entries(d, N, j, [&](int e, int r) {
+            for (int q = gc_ptr[j]; q < gc_ptr[j + 1]; ++q) {
+              const int e = gc_er[q].x, r = gc_er[q].y;
               double dy = dys[r];
               const bool uinf = us[r] > PL_OSQP_INFTY * PL_MIN_SCALING, linf = ls[r] < -PL_OSQP_INFTY * PL_MIN_SCALING;
               if (uinf && linf) dy = 0.0;
               else if (uinf) dy = fmin(dy, 0.0);
               else if (linf) dy = fmax(dy, 0.0);
               s += As[e] * dy;
-            });
+            }
             natdy = fmax(natdy, fabs(s / D[j]));
           }
           natdy = block_max(natdy, red);
@@ -466,7 +458,7 @@ __global__ __launch_bounds__(256) void k_check(PlDev d, int N, int n, int m, int
           int bad = 0;
           for (int r = threadIdx.x; r < m; r += blockDim.x) {
             double adx = 0.0;
-            for_row_entries(d, r, [&](int e, int j) { adx += As[e] * dxs[j]; });
+            for (int q = gr_ptr[r]; q < gr_ptr[r + 1]; ++q) adx += As[gr_ec[q].x] * dxs[gr_ec[q].y];
             adx /= E[r];
             if ((us[r] < PL_OSQP_INFTY * PL_MIN_SCALING && adx > eps_dinf * ndx_) ||
                 (ls[r] > -PL_OSQP_INFTY * PL_MIN_SCALING && adx < -eps_dinf * ndx_))
@@ -498,7 +490,7 @@ __global__ __launch_bounds__(256) void k_check(PlDev d, int N, int n, int m, int
 
 void launch_check(PlOcpHandle* h, int it, int final_check) {
   (void)it;
-  hipLaunchKernelGGL(k_check, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz, h->set,
+  hipLaunchKernelGGL(k_check, dim3(h->B), dim3(CHECK_NT), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz, h->set,
                      final_check);
 }
 

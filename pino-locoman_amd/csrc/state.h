@@ -134,6 +134,10 @@ struct PlDev {
   int* cplrow;       // coupling rows (local row ids)
   int* rownode;      // global row -> node
   int* colnode;      // global column -> node
+  int* gr_ptr;       // global CSR of A: row r's (entry, column) pairs at gr_ec[gr_ptr[r] ..)
+  int2* gr_ec;
+  int* gc_ptr;       // global CSC of A: column j's (entry, row) pairs at gc_er[gc_ptr[j] ..)
+  int2* gc_er;
   PlAdmmNode* anodes;    // N + 1 node tables (ADMM and factor programs)
   uint16_t* aprog;       // distinct ADMM programs, concatenated
   uint16_t* fprog;       // distinct factor programs, concatenated
