@@ -130,7 +130,9 @@ __global__ __launch_bounds__(256) void k_ruiz_norms(PlDev d, int N, int n, int m
   double* Dl = As + nent_max;
   double* El = Dl + ncol_max;
   double* cm = El + nrow_max;
-  uint16_t* P = reinterpret_cast<uint16_t*>(cm + chunk_max);
+  // the node program is read in place (L2-resident, shared by the batch): staging it
+  // per (problem, node) block cost more L2 traffic than the A values themselves
+  const uint16_t* __restrict__ P = d.aprog + prog;
   const double* A = d.Araw + (size_t)b * nnz + ent_off;
   const double* Pd = d.P + (size_t)b * n;
   const double* D = d.D + (size_t)b * n;
@@ -143,11 +145,7 @@ __global__ __launch_bounds__(256) void k_ruiz_norms(PlDev d, int N, int n, int m
   for (int k = tid; k < nent; k += 256) As[k] = A[k];
   for (int k = tid; k < ncol; k += 256) Dl[k] = D[x_off + k];  // w_i then dx_{i+1}: contiguous
   for (int k = tid; k < nrow; k += 256) El[k] = E[row_off + k];
-  {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(d.aprog + prog);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(P);
-    for (int k = tid; k < (plen >> 1); k += 256) dst[k] = src[k];
-  }
+  (void)plen;
   __syncthreads();
   // ---- columns
   const int cchn = an[i].cchn;
@@ -296,7 +294,7 @@ void launch_qp_setup(PlOcpHandle* h) {
   hipLaunchKernelGGL(k_ruiz_init, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, h->m);
   const int nent_max = (std::max(h->nent_max, 1) + 1) & ~1, ncol_max = (std::max(h->ncol_max, h->nw_max) + 1) & ~1;
   const int nrow_max = (std::max(h->nrow_max, 1) + 1) & ~1, chunk_max = (std::max(h->chunk_max, 1) + 1) & ~1;
-  const size_t lds = (size_t)(nent_max + ncol_max + nrow_max + chunk_max) * 8 + ((2 * (size_t)h->prog_len_max + 15) & ~(size_t)15);
+  const size_t lds = (size_t)(nent_max + ncol_max + nrow_max + chunk_max) * 8;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)k_ruiz_norms, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
