@@ -1043,6 +1043,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= dalloc(o, &D.S, B * (size_t)h.S_stride);
   rc |= dalloc(o, &D.FS, B * (size_t)h.fs_stride);
   rc |= dalloc(o, &D.work, B * 8);
+  rc |= dalloc(o, &D.chk, B * (size_t)(h.N + 1) * 8);
   rc |= dalloc(o, &D.info, B);
   rc |= dalloc(o, &D.t0, B);
   rc |= dalloc(o, &D.xstate, B * (size_t)h.nx);

@@ -338,16 +338,97 @@ void launch_admm_init(PlOcpHandle* h) {
 // ---------------------------------------------------------------------------
 // Termination (OSQP 0.6 update_info + check_termination, incl. infeasibility
 // certificates and the x10 "approximate" check at max_iter).
-constexpr int CHECK_NT = 1024;  // rows / columns of one problem spread over 16 waves
+// Residual norms per (problem, node): the node's A values, x (w_i and dx_{i+1} are
+// contiguous in x) and y are staged in LDS so the row gathers of A x never leave the
+// workgroup; one 64-thread block per (problem, node), partial maxima to d.chk.
+//   chk[b][i][0..2] = max |E^-1 (A x - z)|, |E^-1 z|, |E^-1 A x|   over node i's rows
+//   chk[b][i][3..6] = max |D^-1 (P x + q + A^T y)|, |D^-1 q|, |D^-1 A^T y|, |D^-1 P x|
+//                     over node i's columns w_i
+// Summation orders are those of the global CSR / CSC (rows in CSR order; a column's
+// own-node entries, then the previous node's), so results do not depend on the split.
+__global__ __launch_bounds__(64) void k_check_part(PlDev d, int N, int n, int m, int nnz, int ndx) {
+  extern __shared__ double lds[];
+  const int b = blockIdx.x / (N + 1), i = blockIdx.x - b * (N + 1);
+  if (d.info[b].done) return;
+  const PlNode nd = d.nodes[i];
+  const int tid = threadIdx.x;
+  const int nent = nd.nent, nrow = nd.nrow, nw = nd.nw, ncol = nd.ncol;
+  // the node's A values are read in place: one block touches ~8 KB of A, L1-resident
+  const double* __restrict__ Al = d.As + (size_t)b * nnz + nd.ent_off;
+  double* xl = lds;                    // ncol (w_i, dx_{i+1})
+  double* yl = xl + ((ncol + nw + 1) & ~1);  // nrow
+  double* red = yl + ((nrow + 1) & ~1);      // 7 x 64
+  const double* As = d.As + (size_t)b * nnz;
+  const double* xa = d.xa + (size_t)b * n;
+  const double* ya = d.ya + (size_t)b * m;
+  for (int c = tid; c < max(ncol, nw); c += 64) xl[c] = xa[nd.x_off + c];
+  for (int r = tid; r < nrow; r += 64) yl[r] = ya[nd.row_off + r];
+  __syncthreads();
+  double v[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  {
+    const double* za = d.za + (size_t)b * m + nd.row_off;
+    const double* E = d.E + (size_t)b * m + nd.row_off;
+    const int* __restrict__ rp = d.gr_ptr + nd.row_off;
+    const int2* __restrict__ ec = d.gr_ec;
+    for (int r = tid; r < nrow; r += 64) {
+      double ax = 0.0;
+      const int q1 = rp[r + 1];
+#pragma unroll 4
+      for (int q = rp[r]; q < q1; ++q) {
+        const int2 ej = ec[q];  // the row's entries and columns belong to node i
+        ax += Al[ej.x - nd.ent_off] * xl[ej.y - nd.x_off];
+      }
+      const double ei = 1.0 / E[r];
+      v[0] = fmax(v[0], fabs(ei * (ax - za[r])));
+      v[1] = fmax(v[1], fabs(ei * za[r]));
+      v[2] = fmax(v[2], fabs(ei * ax));
+    }
+  }
+  {
+    const double* qs = d.qs + (size_t)b * n + nd.x_off;
+    const double* Ps = d.Ps + (size_t)b * n + nd.x_off;
+    const double* D = d.D + (size_t)b * n + nd.x_off;
+    const int* __restrict__ cp = d.gc_ptr + nd.x_off;
+    const int2* __restrict__ er = d.gc_er;
+    for (int lc = tid; lc < nw; lc += 64) {
+      double aty = 0.0;
+      const int q1 = cp[lc + 1];
+#pragma unroll 4
+      for (int q = cp[lc]; q < q1; ++q) {
+        const int2 e = er[q];  // own-node entries first, then node i-1's (dx_i columns)
+        const int le = e.x - nd.ent_off;
+        aty += le >= 0 ? Al[le] * yl[e.y - nd.row_off] : As[e.x] * ya[e.y];
+      }
+      const double di = 1.0 / D[lc];
+      const double px = Ps[lc] * xl[lc];
+      v[3] = fmax(v[3], fabs(di * (px + qs[lc] + aty)));
+      v[4] = fmax(v[4], fabs(di * qs[lc]));
+      v[5] = fmax(v[5], fabs(di * aty));
+      v[6] = fmax(v[6], fabs(di * px));
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) red[k * 64 + tid] = v[k];
+  __syncthreads();
+  for (int s = 32; s > 0; s >>= 1) {
+    if (tid < s)
+#pragma unroll
+      for (int k = 0; k < 7; ++k) red[k * 64 + tid] = fmax(red[k * 64 + tid], red[k * 64 + tid + s]);
+    __syncthreads();
+  }
+  if (tid < 7) d.chk[((size_t)b * (N + 1) + i) * 8 + tid] = red[tid * 64];
+}
+
+// Termination (OSQP 0.6 update_info + check_termination, incl. infeasibility
+// certificates and the x10 "approximate" check at max_iter), from the node partials.
+constexpr int CHECK_NT = 256;
 __global__ __launch_bounds__(CHECK_NT) void k_check(PlDev d, int N, int n, int m, int nnz, PlSettings st,
                                                      int final_check) {
   const int b = blockIdx.x;
   PlProbInfo* info = d.info + b;
   if (info->done) return;
-  __shared__ double red[4 * CHECK_NT];
+  __shared__ double red[7 * CHECK_NT];
   const double* As = d.As + (size_t)b * nnz;
-  const double* za = d.za + (size_t)b * m;
-  const double* ya = d.ya + (size_t)b * m;
   const double* xa = d.xa + (size_t)b * n;
   const double* qs = d.qs + (size_t)b * n;
   const double* Ps = d.Ps + (size_t)b * n;
@@ -362,38 +443,15 @@ __global__ __launch_bounds__(CHECK_NT) void k_check(PlDev d, int N, int n, int m
   const int* __restrict__ gc_ptr = d.gc_ptr;
   const int2* __restrict__ gc_er = d.gc_er;
   const double c = d.cs[b], cinv = 1.0 / c;
-  // primal: ||E^-1 (A x - z)||, ||E^-1 z||, ||E^-1 A x||
-  double pv[3] = {0.0, 0.0, 0.0};
-  for (int r = threadIdx.x; r < m; r += blockDim.x) {
-    double ax = 0.0;
-    for (int s = gr_ptr[r]; s < gr_ptr[r + 1]; ++s) {
-      const int2 ej = gr_ec[s];
-      ax += As[ej.x] * xa[ej.y];
-    }
-    const double ei = 1.0 / E[r];
-    pv[0] = fmax(pv[0], fabs(ei * (ax - za[r])));
-    pv[1] = fmax(pv[1], fabs(ei * za[r]));
-    pv[2] = fmax(pv[2], fabs(ei * ax));
+  double pv[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int i = threadIdx.x; i <= N; i += blockDim.x) {
+    const double* ck = d.chk + ((size_t)b * (N + 1) + i) * 8;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) pv[k] = fmax(pv[k], ck[k]);
   }
-  block_max_k<3, CHECK_NT>(pv, red);
+  block_max_k<7, CHECK_NT>(pv, red);
   const double pri = pv[0], nz = pv[1], nax = pv[2];
-  // dual: c^-1 ||D^-1 (P x + q + A^T y)||, ||D^-1 q||, ||D^-1 A^T y||, ||D^-1 P x||
-  double dv[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int j = threadIdx.x; j < n; j += blockDim.x) {
-    double aty = 0.0;
-    for (int s = gc_ptr[j]; s < gc_ptr[j + 1]; ++s) {
-      const int2 er = gc_er[s];
-      aty += As[er.x] * ya[er.y];
-    }
-    const double di = 1.0 / D[j];
-    const double px = Ps[j] * xa[j];
-    dv[0] = fmax(dv[0], fabs(di * (px + qs[j] + aty)));
-    dv[1] = fmax(dv[1], fabs(di * qs[j]));
-    dv[2] = fmax(dv[2], fabs(di * aty));
-    dv[3] = fmax(dv[3], fabs(di * px));
-  }
-  block_max_k<4, CHECK_NT>(dv, red);
-  const double dua = cinv * dv[0], nq = dv[1], naty = dv[2], npx = dv[3];
+  const double dua = cinv * pv[3], nq = pv[4], naty = pv[5], npx = pv[6];
   __shared__ int s_status;
   for (int pass = 0; pass < (final_check ? 2 : 1); ++pass) {
     const bool approx = (pass == 1);
@@ -488,6 +546,11 @@ __global__ __launch_bounds__(CHECK_NT) void k_check(PlDev d, int N, int n, int m
 
 void launch_check(PlOcpHandle* h, int it, int final_check) {
   (void)it;
+  {
+    const int lds = ((2 * h->ncol_max + 1) & ~1) + ((h->nrow_max + 1) & ~1) + 7 * 64;
+    hipLaunchKernelGGL(k_check_part, dim3(h->B * (h->N + 1)), dim3(64), lds * 8, h->stream, h->d, h->N, h->n, h->m,
+                       h->nnz, h->ndx);
+  }
   hipLaunchKernelGGL(k_check, dim3(h->B), dim3(CHECK_NT), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz, h->set,
                      final_check);
 }

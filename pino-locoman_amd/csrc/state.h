@@ -178,6 +178,7 @@ struct PlDev {
   double* step;      // unscaled QP step dx
   double* S;         // factor blocks (tiled)
   double* work;      // generic reductions scratch
+  double* chk;       // residual-norm partials [B][N+1][8] (k_check_part)
   PlProbInfo* info;
   // MPC (device loop)
   double* t0;        // per-problem gait time offset
