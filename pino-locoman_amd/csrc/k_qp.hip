@@ -357,7 +357,6 @@ __global__ __launch_bounds__(64) void k_check_part(PlDev d, int N, int n, int m,
   const double* __restrict__ Al = d.As + (size_t)b * nnz + nd.ent_off;
   double* xl = lds;                    // ncol (w_i, dx_{i+1})
   double* yl = xl + ((ncol + nw + 1) & ~1);  // nrow
-  double* red = yl + ((nrow + 1) & ~1);      // 7 x 64
   const double* As = d.As + (size_t)b * nnz;
   const double* xa = d.xa + (size_t)b * n;
   const double* ya = d.ya + (size_t)b * m;
@@ -407,16 +406,15 @@ __global__ __launch_bounds__(64) void k_check_part(PlDev d, int N, int n, int m,
       v[6] = fmax(v[6], fabs(di * px));
     }
   }
+  // one wave: butterfly maxima across the 64 lanes (max is order-free, so exact)
 #pragma unroll
-  for (int k = 0; k < 7; ++k) red[k * 64 + tid] = v[k];
-  __syncthreads();
-  for (int s = 32; s > 0; s >>= 1) {
-    if (tid < s)
+  for (int s = 32; s > 0; s >>= 1)
 #pragma unroll
-      for (int k = 0; k < 7; ++k) red[k * 64 + tid] = fmax(red[k * 64 + tid], red[k * 64 + tid + s]);
-    __syncthreads();
-  }
-  if (tid < 7) d.chk[((size_t)b * (N + 1) + i) * 8 + tid] = red[tid * 64];
+    for (int k = 0; k < 7; ++k) v[k] = fmax(v[k], __shfl_xor(v[k], s, 64));
+  double* out = d.chk + ((size_t)b * (N + 1) + i) * 8;
+#pragma unroll
+  for (int k = 0; k < 7; ++k)
+    if (tid == k) out[k] = v[k];
 }
 
 // Termination (OSQP 0.6 update_info + check_termination, incl. infeasibility
@@ -547,7 +545,7 @@ __global__ __launch_bounds__(CHECK_NT) void k_check(PlDev d, int N, int n, int m
 void launch_check(PlOcpHandle* h, int it, int final_check) {
   (void)it;
   {
-    const int lds = ((2 * h->ncol_max + 1) & ~1) + ((h->nrow_max + 1) & ~1) + 7 * 64;
+    const int lds = ((2 * h->ncol_max + 1) & ~1) + ((h->nrow_max + 1) & ~1);
     hipLaunchKernelGGL(k_check_part, dim3(h->B * (h->N + 1)), dim3(64), lds * 8, h->stream, h->d, h->N, h->n, h->m,
                        h->nnz, h->ndx);
   }
