@@ -13,12 +13,20 @@ seeds from the global problem index (weak scaling, no data-path collective); the
 per-problem results are all-gathered over RCCL after the timed region.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+
+With --gpus N > 1 and no torchrun environment, bench.py launches the N ranks itself
+(torch.distributed.run as a child process, before anything touches the GPU) and
+relays rank 0's JSON line.  --dry-run exercises the same rank / shard / gather
+plumbing over gloo on the CPU without solving (tests/test_bench.py).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,14 +44,46 @@ METRIC = "MPC solves/sec (B2G whole_body_rnea N=50) at batch; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 
 
-def admm_bytes_per_problem_iter(sz, node_table):
+TRAFFIC_FILE = os.path.join(HERE, "profiles", "traffic", "admm_traffic.json")
+TRAFFIC_SOURCES = ("pino-locoman_amd/csrc/k_admm.hip", "pino-locoman_amd/csrc/state.h")
+
+
+def admm_bytes_per_problem_iter(sz, node_table, padded=False):
     """Algorithmic HBM bytes of one ADMM iteration of one problem (roofline):
     the two sweeps read every factor block S_i once each, except S_0 and S_N which the
     fused turnaround steps read once per iteration; A is read once, and the vectors
-    x, rhs, bt, q (7n) and z, y, l, u, rho (7m) are read / written once."""
-    blk = node_table[:, 9].astype(float) * 64 * 16  # doubles per factor block (K slots x 64 lanes x 16)
-    s_once = blk[0] + blk[-1]
-    return 8.0 * (2 * sz["S_stride"] - s_once + sz["nnz"] + 7 * sz["n"] + 7 * sz["m"])
+    x, rhs, bt, q (7n) and z, y, l, u, rho (7m) are read / written once.
+
+    A factor block is the stored lower triangle nw (nw + 1) / 2 of S_i; padded=True
+    counts the 4x4 lane-tile slots the kernel actually streams (K x 64 lanes x 16)."""
+    nw = node_table[:, 0].astype(float)
+    blk = node_table[:, 9].astype(float) * 64 * 16 if padded else nw * (nw + 1) / 2
+    return 8.0 * (2 * blk.sum() - blk[0] - blk[-1] + sz["nnz"] + 7 * sz["n"] + 7 * sz["m"])
+
+
+def traffic_source_sha():
+    """sha256 of the k_admm sources: a PMC traffic measurement applies only to the
+    kernel revision it was taken on."""
+    h = hashlib.sha256()
+    for rel in TRAFFIC_SOURCES:
+        with open(os.path.join(HERE, rel), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def measured_traffic(batch, nodes, workload):
+    """HBM bytes per problem-iteration of k_admm from the committed PMC passes
+    (tools/pmc_traffic.py), or None if they were taken on another kernel revision
+    or workload."""
+    try:
+        with open(TRAFFIC_FILE) as fh:
+            tj = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if (tj.get("src_sha") != traffic_source_sha() or tj.get("batch") != batch or tj.get("nodes") != nodes
+            or tj.get("workload") != workload):
+        return None
+    return tj
 
 
 def _baseline_worker(args):
@@ -99,6 +139,46 @@ def cpu_baseline(robot, dynamics, N, n_steps=2):
                       f"oracle (oracle/), one thread per worker; wall = slowest worker's timed solves"}
 
 
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """Run this script as `n` ranks (one process per GPU) via torch.distributed.run in a
+    child process; rank 0 prints the JSON line to the inherited stdout.  Called before
+    any GPU work, so nothing is exec'ed from a process that initialised the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_run(args, world, rank):
+    """Rank / shard / gather plumbing over gloo on the CPU (no GPU, no solve)."""
+    import torch
+    dist = pdist.init("gloo")
+    R = robots.ROBOTS[args.robot]()
+    R.set_gait_sequence("trot", 0.8)
+    B = args.batch
+    first, count = shard(B * world, world, rank)
+    lay, P, X, XS, T0 = build_batch(R, args.dynamics, args.nodes, count, first)
+    t0 = time.perf_counter()
+    elapsed = pdist.max_over_ranks(time.perf_counter() - t0, dist)
+    allp = pdist.gather_rows(torch.from_numpy(np.concatenate([X[:, :lay.nu[0]], XS], 1)), dist)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "solves/s", "n_gpus": world, "steps": 0,
+                          "warmup": 0, "ms_per_step": elapsed * 1e3, "higher_is_better": True, "scaling": "weak",
+                          "dry_run": True, "gathered_rows": int(allp.shape[0]),
+                          "config": {"workload": f"{args.robot} {args.dynamics} N={args.nodes} MPC step",
+                                     "batch_per_gpu": B, "global_batch": B * world}}), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,9 +189,16 @@ def main():
     ap.add_argument("--dynamics", default="whole_body_rnea")
     ap.add_argument("--nodes", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true", help="gloo plumbing only, no GPU")
     args = ap.parse_args()
 
     world, rank, local_rank = pdist.env_ranks()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    if args.dry_run:
+        return dry_run(args, world, rank)
     base = None
     if not args.no_cpu_baseline and world == 1:
         base = cpu_baseline(args.robot, args.dynamics, args.nodes)  # before the GPU is initialised
@@ -160,20 +247,17 @@ def main():
         assert allp.shape[0] == B * world
 
     sz = bo.sizes()
-    bytes_it = admm_bytes_per_problem_iter(sz, bo.node_table())
-    per_launch_bytes = bytes_it * prof["problem_iters"] / max(1, prof["launches"])
+    ntab = bo.node_table()
+    bytes_it = admm_bytes_per_problem_iter(sz, ntab)
+    bytes_it_padded = admm_bytes_per_problem_iter(sz, ntab, padded=True)
+    iters_per_launch = prof["problem_iters"] / max(1, prof["launches"])
+    per_launch_bytes = bytes_it * iters_per_launch
     avg_launch_s = prof["admm_ms"] / max(1, prof["launches"]) / 1e3
     achieved = per_launch_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    traffic = None
-    tfile = os.path.join(HERE, "profiles", "admm_traffic.json")
-    if os.path.exists(tfile):
-        try:
-            with open(tfile) as fh:
-                tj = json.load(fh)
-            if tj.get("batch") == B and tj.get("nodes") == args.nodes:
-                traffic = tj.get("bytes_per_launch")
-        except Exception:  # noqa: BLE001
-            traffic = None
+    workload = f"{args.robot} {args.dynamics} N={args.nodes} MPC step"
+    tj = measured_traffic(B, args.nodes, workload)
+    # PMC bytes per problem-iteration x this run's problem-iterations per launch
+    traffic = tj["bytes_per_problem_iter"] * iters_per_launch if tj else None
 
     if rank == 0:
         total = B * world * args.steps
@@ -190,14 +274,18 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (randomised initial state / gait phase / base velocity target, seed 1234 + problem)",
-            "config": {"workload": f"{args.robot} {args.dynamics} N={args.nodes} MPC step", "batch_per_gpu": B,
+            "config": {"workload": workload, "batch_per_gpu": B,
                        "global_batch": B * world, "nodes": args.nodes, "robot": args.robot,
                        "dynamics": args.dynamics, "solver": "osqp-sqp (1 SQP iteration, max_iter 100)",
                        "parallelism": f"batch-sharded dp{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_admm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "bytes_per_problem_iter": bytes_it, "avg_launch_ms": avg_launch_s * 1e3,
-                         "launches": prof["launches"]},
+                         "algorithmic_bytes_per_launch": per_launch_bytes,
+                         "bytes_per_problem_iter": bytes_it, "bytes_per_problem_iter_padded": bytes_it_padded,
+                         "problem_iters_per_launch": iters_per_launch, "avg_launch_ms": avg_launch_s * 1e3,
+                         "launches": prof["launches"],
+                         "traffic_source": (f"profiles/traffic/admm_traffic.json (k_admm src {tj['src_sha']})"
+                                            if tj else None)},
         }
         if base is not None:
             out["cpu_baseline"] = base

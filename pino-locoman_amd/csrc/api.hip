@@ -1060,8 +1060,11 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   return 0;
 }
 
+static void cas_forget(const pl_ocp* o);
+
 extern "C" void pl_ocp_destroy(pl_ocp* o) {
   if (!o) return;
+  cas_forget(o);  // a bound CasADi handle must not outlive its OCP
   if (o->on_device) {
     hipSetDevice(o->h.device);
     hipStreamSynchronize(o->h.stream);
@@ -1349,6 +1352,10 @@ extern "C" int pl_ocp_profile(pl_ocp* o, int enable) {
   h->prof_admm_ms = 0.0;
   h->prof_admm_launches = 0;
   h->prof_admm_iters = 0;
+  if (enable) {
+    launch_reset_prof(h);
+    PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+  }
   return 0;
 }
 
@@ -1356,6 +1363,14 @@ extern "C" int pl_ocp_profile_read(pl_ocp* o, double* out) {
   REQUIRE_DEVICE(o);
   PlOcpHandle* h = &o->h;
   prof_collect(h);
+  // problem-iterations the ADMM launches actually executed: per-problem counters
+  // (terminated problems skip later launches, so B * niter would over-count)
+  std::vector<PlProbInfo> info(h->B);
+  PL_CHECK_HIP(hipMemcpyAsync(info.data(), h->d.info, h->B * sizeof(PlProbInfo), hipMemcpyDeviceToHost, h->stream));
+  PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+  long long it = 0;
+  for (int b = 0; b < h->B; ++b) it += info[b].iter_prof;
+  h->prof_admm_iters = it;
   out[0] = h->prof_admm_ms;
   out[1] = (double)h->prof_admm_launches;
   out[2] = (double)h->prof_admm_iters;
@@ -1586,6 +1601,10 @@ extern "C" int pl_casadi_bind(pl_ocp* o, int retract_steps) {
 }
 
 extern "C" void pl_casadi_unbind(void) { g_cas.o = nullptr; }
+
+static void cas_forget(const pl_ocp* o) {
+  if (g_cas.o == o) g_cas.o = nullptr;
+}
 
 // ---- shared boilerplate of every external function
 #define PL_CASADI_COMMON(NAME, NIN, NOUT)                                                          \

@@ -787,7 +787,10 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   prefetch_LC(KF0, 0, LCn);
   load_S(0, 0, SR);
   for (int q = 0; q < Q; ++q) step(q);
-  if (lane == 0) info->iter += niter;
+  if (lane == 0) {
+    info->iter += niter;
+    info->iter_prof += niter;  // only problems still iterating reach here (done ones return above)
+  }
   if constexpr (TIMING) {
     if (lane == 0 && d.dbg)
       for (int k = 0; k < 10; ++k) d.dbg[(size_t)b * 16 + k] += (double)tacc[k];
@@ -878,6 +881,5 @@ void launch_admm(PlOcpHandle* h, int niter, int check, int it_base) {
   if (prof) {
     hipEventRecord(h->prof_ev[h->prof_n][1], h->stream);
     h->prof_n++;
-    h->prof_admm_iters += (long long)h->B * niter;
   }
 }

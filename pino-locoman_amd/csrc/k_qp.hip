@@ -587,6 +587,15 @@ __global__ void k_reset_info(PlDev d, int B) {
   I.done = 0;
 }
 
+__global__ void k_reset_prof(PlDev d, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) d.info[b].iter_prof = 0;
+}
+
+void launch_reset_prof(PlOcpHandle* h) {
+  hipLaunchKernelGGL(k_reset_prof, dim3((h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B);
+}
+
 void launch_reset_info(PlOcpHandle* h) {
   hipLaunchKernelGGL(k_reset_info, dim3((h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B);
 }

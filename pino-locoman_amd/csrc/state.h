@@ -119,6 +119,7 @@ struct PlProbInfo {
   double f;          // objective at the returned point
   double viol_max;   // max bound violation at the returned point (ocp.py:412-414)
   double norm_dy, norm_dx;  // scratch for infeasibility checks
+  long long iter_prof;      // ADMM iterations executed since pl_ocp_profile(o, 1) (roofline accounting)
 };
 
 struct PlDev {
@@ -221,7 +222,7 @@ struct PlOcpHandle {
   int prof_n;
   double prof_admm_ms;
   long long prof_admm_launches;
-  long long prof_admm_iters;   // problem-iterations (B * niter) covered by the timed launches
+  long long prof_admm_iters;   // problem-iterations executed by the timed launches (sum of PlProbInfo::iter_prof)
 };
 
 // ---- kernel launchers (defined in the k_*.hip translation units)
@@ -241,6 +242,7 @@ void launch_mpc_prepare(PlOcpHandle* h, int k);
 void launch_mpc_finish(PlOcpHandle* h);
 void launch_reset_info(PlOcpHandle* h);
 void launch_reset_iterates(PlOcpHandle* h);
+void launch_reset_prof(PlOcpHandle* h);
 
 #define PL_CHECK_HIP(expr)                                                        \
   do {                                                                            \

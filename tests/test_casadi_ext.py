@@ -94,3 +94,18 @@ def test_retract_solution_matches_oracle():
         casadi_ext.ExternalFunction("sqp_data")(sol, np.zeros(bo.np))  # no device on this handle
     casadi_ext.unbind()
     bo.close()
+
+
+def test_destroy_unbinds():
+    """Closing a bound OCP clears the process-global binding: a later call reports
+    'no OCP bound' instead of touching freed memory (pl_ocp_destroy -> cas_forget)."""
+    from pinoloco import _lib, casadi_ext
+    from pinoloco.ocp import BatchedOCP
+    R = make_robot("go2")
+    bo = BatchedOCP(R, "whole_body_rnea", 6, batch=1, device=-1)
+    casadi_ext.bind(bo, 2)
+    fr = casadi_ext.ExternalFunction("retract_solution")
+    n, nx = bo.n, R.nq + R.nv
+    bo.close()
+    with pytest.raises(_lib.PinolocoError, match="no OCP bound"):
+        fr(np.zeros(n), np.zeros(nx))
