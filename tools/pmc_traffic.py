@@ -32,7 +32,7 @@ def _rows(d):
     return out
 
 
-def per_launch(d, counter, kernel="k_admm"):
+def per_launch(d, counter, kernel="k_admm<"):  # not k_admm_init
     vals = {}
     for r in _rows(d):
         if r.get("Counter_Name") != counter or kernel not in r.get("Kernel_Name", ""):
