@@ -51,10 +51,11 @@ typedef struct pl_ocp pl_ocp;
 #define PL_JOINT_FREEFLYER 1
 #define PL_JOINT_REVOLUTE 2
 
-/* Dynamics kinds (ocp_factory.py:9-15). centroidal_* stay on the CPU oracle. */
+/* Dynamics kinds (ocp_factory.py:9-15). */
 #define PL_DYN_WHOLE_BODY_RNEA 0
 #define PL_DYN_WHOLE_BODY_ACC 1
 #define PL_DYN_WHOLE_BODY_ABA 2
+#define PL_DYN_CENTROIDAL_VEL 3      /* x = [h (6), q], dx = [dh, dq], u = [v | f] */
 
 typedef struct {
   int njoints;                 /* including the universe joint 0 */
@@ -79,7 +80,7 @@ typedef struct {
   int nodes;                   /* N */
   int tau_nodes;               /* OCP_ARGS["whole_body_rnea"]["tau_nodes"] (ocp_args.py:16) */
   int include_acc;             /* must be 1 (ocp_args.py:17) */
-  int include_base;            /* must be 1 for whole_body_acc (ocp_args.py:11) */
+  int include_base;            /* must be 1 for whole_body_acc / centroidal_vel (ocp_args.py:5-11) */
   int n_feet;                  /* 4: FR, FL, RR, RL (utils/gait_sequence.py:7) */
   int foot_frames[4];
   int ext_force_frame;         /* -1: none */
@@ -159,6 +160,8 @@ int pl_mpc_setup(pl_ocp* o, const double* x_state, const double* t0);
  * x_state <- integrate(x_state, DX[1]).  No host transfers. */
 int pl_mpc_step(pl_ocp* o, int k);
 int pl_mpc_get_state(pl_ocp* o, double* x_state);
+/* Solver stats of the last MPC step's (last) SQP iteration, as pl_ocp_solve reports. */
+int pl_mpc_get_stats(pl_ocp* o, pl_stats* stats);
 /* Copy the first control input row u_0 [batch][nu_0] and x_state into a
  * caller-owned DEVICE buffer (for collectives): layout [batch][nu_0 + nx]. */
 int pl_mpc_export(pl_ocp* o, void* device_dst);
@@ -169,6 +172,43 @@ int pl_ocp_sync(pl_ocp* o);
  *  dynamics/dynamics_whole_body_torque.py:11-40). */
 int pl_state_integrate(const pl_model* m, const double* x, const double* dx, double* out);
 int pl_state_difference(const pl_model* m, const double* x0, const double* x1, double* dx);
+
+/* ---- Dynamics plugin surface (dynamics/*.py factories -> batched point functions).
+ * A pl_dyn handle holds the contact frames (FR, FL, RR, RL feet, optional
+ * external-force frame) and the "base_link" frame of Dynamics.__init__
+ * (dynamics/dynamics.py:13-17).  pl_dyn_eval evaluates `batch` points of one
+ * function: inputs in0..in3 and the output are caller-owned [batch][len] float64
+ * arrays (lengths from pl_dyn_sizes; unused inputs may be NULL).  flags: bit 0 =
+ * the forces include the external-force frame (the factories' ext_force_frame
+ * argument), bit 1 = relative_to_base (get_frame_velocity).  device >= 0 runs one
+ * GPU thread per point; device = -1 evaluates the same code on the host. */
+typedef struct pl_dyn pl_dyn;
+#define PL_FN_RNEA 0           /* rnea_dynamics(q, v, a, forces) -> tau[nv]      dynamics/dynamics.py:33-65 */
+#define PL_FN_ABA 1            /* aba_dynamics(q, v, tau_j, forces) -> a[nv]     dynamics_whole_body_torque.py:73-103 */
+#define PL_FN_FRAME_POS 2      /* get_frame_position(frame)(q) -> [3]            dynamics/dynamics.py:67-75 */
+#define PL_FN_FRAME_VEL 3      /* get_frame_velocity(frame, rel)(q, v) -> [6]    dynamics/dynamics.py:77-118 */
+#define PL_FN_GAPS_WB 4        /* dynamics_gaps(q, v, a, forces) -> [6]          dynamics_whole_body_acc.py:85-126 */
+#define PL_FN_BASE_ACC_WB 5    /* base_acc_dynamics(q, v, a_j, forces) -> [6]    dynamics_whole_body_acc.py:43-83 */
+#define PL_FN_COM_DYN 6        /* com_dynamics(q, forces) -> h_dot[6]            dynamics_centroidal_vel.py:43-71 */
+#define PL_FN_BASE_VEL_CV 7    /* base_vel_dynamics(h, q, v_j) -> v_b[6]         dynamics_centroidal_vel.py:73-89 */
+#define PL_FN_BASE_ACC_CV 8    /* base_acc_dynamics(q, v, a_j, forces) -> a_b[6] dynamics_centroidal_vel.py:91-134 */
+#define PL_FN_GAPS_CV 9        /* dynamics_gaps(h, q, v) -> A v - m h [6]        dynamics_centroidal_vel.py:136-148 */
+#define PL_FN_CRBA 10          /* pinocchio crba(q) -> M[nv][nv]                 run_mpc.py:202 */
+#define PL_FN_NLE 11           /* nonLinearEffects(q, v) -> [nv]                 run_mpc.py:203 */
+#define PL_FN_FRAME_JAC 12     /* computeFrameJacobian(q, frame, LWA) -> [6][nv] run_mpc.py:206-209 */
+#define PL_FN_CMAP 13          /* computeCentroidalMap(q) -> A_G[6][nv]          dynamics_centroidal_vel.py:80 */
+#define PL_FN_COM 14           /* centerOfMass(q) -> [3]                         dynamics_centroidal_vel.py:55 */
+#define PL_FN_INTEGRATE_WB 15  /* state_integrate (x=[q,v], dx) -> x'            dynamics_whole_body_torque.py:11-25 */
+#define PL_FN_DIFFERENCE_WB 16 /* state_difference (x0, x1) -> dx                dynamics_whole_body_torque.py:27-40 */
+#define PL_FN_INTEGRATE_CV 17  /* state_integrate (x=[h,q], dx=[dh,dq]) -> x'    dynamics_centroidal_vel.py:12-26 */
+#define PL_FN_DIFFERENCE_CV 18 /* state_difference (x0, x1) -> dx                dynamics_centroidal_vel.py:28-41 */
+int pl_dyn_create(const pl_model* model, const int* foot_frames, int ext_force_frame, int base_frame, int device,
+                  pl_dyn** out);
+void pl_dyn_destroy(pl_dyn* d);
+/* in_len: [4] input lengths, out_len: output length per point. */
+int pl_dyn_sizes(const pl_dyn* d, int fn, int flags, int* in_len, int* out_len);
+int pl_dyn_eval(pl_dyn* d, int fn, int batch, int frame, int flags, const double* in0, const double* in1,
+                const double* in2, const double* in3, double* out);
 
 /* Timing of the dominant kernel (ADMM sweeps) with HIP events on the handle's
  * stream: pl_ocp_profile(o, 1) clears and starts, pl_ocp_profile_read returns

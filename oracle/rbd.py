@@ -559,3 +559,65 @@ def centroidal_momentum(M: ModelArrays, q, v):
         hl = inertia_mul(M.mass[i], M.lever[i], M.Ic[i], vs[i])
         h = h + act_force(Ro, po - com, hl)
     return h
+
+
+def centroidal_map(M: ModelArrays, q):
+    """computeCentroidalMap: A_G(q) (6 x nv), columns h_G(q, e_k)."""
+    return np.stack([centroidal_momentum(M, q, np.eye(M.nv)[k]) for k in range(M.nv)], -1)
+
+
+def dccrba_v(M: ModelArrays, q, v, h=1e-30):
+    """pinocchio dccrba(q, v) applied to v: d/dt A_G(q(t)) v along q(t) = q (+) t v,
+    by complex step through the Lie-group integrate (dynamics_centroidal_vel.py:110)."""
+    qc = integrate(M, q.astype(complex), 1j * h * v.astype(complex))
+    return (centroidal_map(M, qc) @ v).imag / h
+
+
+def com_dynamics(M: ModelArrays, frames, q, forces, mass, scale=True):
+    """DynamicsCentroidalVel.com_dynamics (dynamics_centroidal_vel.py:43-71):
+    [sum f + (0, 0, -9.81 m), sum (p_e - com) x f_e] (/ m when scale)."""
+    _, oM = forward_kinematics(M, q)
+    com = center_of_mass(M, q)
+    fs = [forces[..., 3 * k:3 * k + 3] for k in range(len(frames))]
+    dp = sum(fs) + np.array([0, 0, -9.81 * mass])
+    dl = 0
+    for k, fid in enumerate(frames):
+        _, pf = frame_placement(M, oM, fid)
+        dl = dl + cross(pf - com, fs[k])
+    out = np.concatenate([dp, dl], -1)
+    return out / mass if scale else out
+
+
+def base_vel_cv(M: ModelArrays, h, q, v_j, mass):
+    """base_vel_dynamics (dynamics_centroidal_vel.py:73-89): A_b^-1 (m h - A_j v_j)."""
+    A = centroidal_map(M, q)
+    return np.linalg.solve(A[:, :6], h * mass - A[:, 6:] @ v_j)
+
+
+def base_acc_cv(M: ModelArrays, frames, q, v, a_j, forces, mass):
+    """base_acc_dynamics (dynamics_centroidal_vel.py:91-134): A_b^-1 (dh - dA v - A_j a_j)."""
+    A = centroidal_map(M, q)
+    dh = com_dynamics(M, frames, q, forces, mass, scale=False)
+    return np.linalg.solve(A[:, :6], dh - dccrba_v(M, q, v) - A[:, 6:] @ a_j)
+
+
+def base_acc_wb(M: ModelArrays, frames, q, v, a_j, forces):
+    """DynamicsWholeBodyAcc.base_acc_dynamics (dynamics_whole_body_acc.py:43-83):
+    M_bb^-1 (-nle_b - M_bj a_j + sum_k J_c,k[:3, :6]^T f_k) with crba, nonLinearEffects
+    and computeFrameJacobian(LOCAL_WORLD_ALIGNED)."""
+    Mq = crba(M, q)
+    nle = rnea(M, q, v, np.zeros(M.nv))
+    tb = sum(frame_jacobian_lwa(M, q, fid)[:3, :6].T @ forces[3 * k:3 * k + 3] for k, fid in enumerate(frames))
+    return np.linalg.solve(Mq[:6, :6], -nle[:6] - Mq[:6, 6:] @ a_j + tb)
+
+
+def ab_inv_ocs2(Ab):
+    """OCS2 closed form of A_b^-1 (DynamicsCentroidalVel._compute_Ab_inv,
+    dynamics_centroidal_vel.py:150-159)."""
+    m = Ab[0, 0]
+    A22i = np.linalg.inv(Ab[3:, 3:])
+    out = np.zeros((6, 6))
+    out[:3, :3] = np.eye(3) / m
+    out[:3, 3:] = -Ab[:3, 3:] @ A22i / m
+    out[3:, 3:] = A22i
+    return out

@@ -16,6 +16,8 @@
 #include <vector>
 
 #include "../../include/pinoloco.h"
+#include "dyn.h"
+#include "handles.h"
 #include "rows.h"
 #include "state.h"
 
@@ -28,12 +30,6 @@ void pl_set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
-struct pl_model {
-  PlModel m;
-  int nframes;
-  std::vector<int> frame_parent;
-  std::vector<double> frame_R, frame_p;
-};
 
 struct pl_ocp {
   PlOcpHandle h;
@@ -144,17 +140,6 @@ extern "C" void pl_model_destroy(pl_model* m) { delete m; }
 // layout
 namespace {
 
-PlFrameRef frame_ref(const pl_model* M, int fid) {
-  PlFrameRef f;
-  memset(&f, 0, sizeof(f));
-  if (fid < 0 || fid >= M->nframes) { f.valid = 0; f.joint = -1; return f; }
-  f.valid = 1;
-  f.joint = M->frame_parent[fid];
-  for (int k = 0; k < 9; ++k) f.R[k] = M->frame_R[9 * fid + k];
-  for (int k = 0; k < 3; ++k) f.p[k] = M->frame_p[3 * fid + k];
-  return f;
-}
-
 void add_block(PlOcpConst& O, int type, int kind, int count, int arg = 0) {
   PlRowBlock& B = O.blk[type][O.nblk[type]++];
   B.kind = kind;
@@ -169,9 +154,18 @@ void build_blocks(PlOcpConst& O, bool has_ext, bool has_arm) {
     O.nblk[type] = 0;
     const bool first = (type == 0);
     const bool tau = (O.dyn == PL_DYN_RNEA) && (type == 1 || (type == 0 && O.tau_nodes > 0));
+    const bool cv = (O.dyn == PL_DYN_CV);
+    // centroidal_vel keeps the state rows at node 0 (ocp.py:137-140, 170-173)
+    const bool state = !first || cv;
     if (first) add_block(O, type, PL_RB_INIT, O.ndx);
-    add_block(O, type, PL_RB_DYNQ, O.nv);
-    add_block(O, type, PL_RB_DYNV, O.nv);
+    if (cv) {  // setup_dynamics_constraints (ocp_centroidal_vel.py:85-107)
+      add_block(O, type, PL_RB_CV_DYNH, 6);
+      add_block(O, type, PL_RB_CV_DYNQ, O.nv);
+      add_block(O, type, PL_RB_CV_GAP, 6);
+    } else {
+      add_block(O, type, PL_RB_DYNQ, O.nv);
+      add_block(O, type, PL_RB_DYNV, O.nv);
+    }
     if (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC) add_block(O, type, PL_RB_RNEA_BASE, 6);
     if (tau) {
       add_block(O, type, PL_RB_TAU_EQ, O.nj);
@@ -181,13 +175,13 @@ void build_blocks(PlOcpConst& O, bool has_ext, bool has_arm) {
       add_block(O, type, PL_RB_FZ, 1, k);
       add_block(O, type, PL_RB_CONE, 1, k);
       add_block(O, type, PL_RB_SWINGF, 3, k);
-      if (!first) {
+      if (state) {
         add_block(O, type, PL_RB_FVXY, 2, k);
         add_block(O, type, PL_RB_FVZ, 1, k);
       }
     }
     if (has_ext) add_block(O, type, PL_RB_EXT, 3);
-    if (!first) {
+    if (state) {
       if (has_arm) add_block(O, type, PL_RB_ARM, 3);
       add_block(O, type, PL_RB_QJ, O.nj);
       add_block(O, type, PL_RB_VJ, O.nj);
@@ -214,11 +208,13 @@ std::vector<std::vector<int>> node_row_deps(const PlModel& M, const PlOcpConst& 
   const int type = pl::node_type(O, i);
   const int nv = O.nv, nj = O.nj, nf = O.nf, ndx = O.ndx;
   const int nw = ndx + nu;
-  auto DQ = [&](int k) { return k; };
-  auto DV = [&](int k) { return nv + k; };
+  const bool cv = (O.dyn == PL_DYN_CV);
+  // dx = [dq, dv] (whole body) or [dh, dq] with v = u[:nv] (centroidal_vel)
+  auto DQ = [&](int k) { return cv ? 6 + k : k; };
   auto U = [&](int k) { return ndx + k; };
+  auto DV = [&](int k) { return cv ? ndx + k : nv + k; };
   auto DXN = [&](int k) { return nw + k; };
-  const int f_off = (O.dyn == PL_DYN_RNEA) ? O.na : (O.dyn == PL_DYN_ACC ? nv : nj);
+  const int f_off = (O.dyn == PL_DYN_RNEA) ? O.na : ((O.dyn == PL_DYN_ACC || cv) ? nv : nj);
   auto F = [&](int k) { return U(f_off + k); };
   std::vector<int> dynset;  // dependency set of the RNEA / ABA outputs
   for (int k = 3; k < nv; ++k) dynset.push_back(DQ(k));
@@ -262,6 +258,17 @@ std::vector<std::vector<int>> node_row_deps(const PlModel& M, const PlOcpConst& 
         case PL_RB_ARM: s = frame_deps(O.arm); break;
         case PL_RB_QJ: s = {DQ(6 + r)}; break;
         case PL_RB_VJ: s = {DV(6 + r)}; break;
+        case PL_RB_CV_DYNH:  // h_dot(q, forces): orientation + joints, every force
+          s = {r, DXN(r)};
+          for (int k = 3; k < nv; ++k) s.push_back(DQ(k));
+          for (int k = 0; k < nf; ++k) s.push_back(F(k));
+          break;
+        case PL_RB_CV_DYNQ: s = {DQ(r), DV(r), DXN(6 + r)}; break;
+        case PL_RB_CV_GAP:  // A(q) v - m h
+          s = {r};
+          for (int k = 3; k < nv; ++k) s.push_back(DQ(k));
+          for (int k = 0; k < nv; ++k) s.push_back(DV(k));
+          break;
       }
       std::sort(s.begin(), s.end());
       s.erase(std::unique(s.begin(), s.end()), s.end());
@@ -648,7 +655,7 @@ int build_admm_prog(pl_ocp* o) {
     h.admm_asr = nmax[dom] <= 16 * 64 ? 16 : PL_ADMM_ASR_MAX;
   }
   if (!factor_supports_ndx(ndx)) {
-    pl_set_error("state dimension ndx = %d is not supported by the factor kernel (36, 48)", ndx);
+    pl_set_error("state dimension ndx = %d is not supported by the factor kernel (24, 36, 48)", ndx);
     return -1;
   }
   if (h.nrow_max > 64 * PL_ADMM_MR || h.nw_max > 64 * PL_ADMM_MV || h.ncpl_max > 64) {
@@ -875,13 +882,17 @@ int upload(pl_ocp* o, T** p, const std::vector<T>& v) {
 
 extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int batch, int device, pl_ocp** out) {
   if (!model || !d || !out || batch <= 0) { pl_set_error("bad arguments"); return -1; }
-  if (d->dynamics < 0 || d->dynamics > 2) { pl_set_error("Unknown dynamics type: %d", d->dynamics); return -1; }
+  if (d->dynamics < 0 || d->dynamics > 3) { pl_set_error("Unknown dynamics type: %d", d->dynamics); return -1; }
   if (d->dynamics == PL_DYN_WHOLE_BODY_RNEA && !d->include_acc) {
     pl_set_error("whole_body_rnea requires include_acc=True on this path");
     return -1;
   }
   if (d->dynamics == PL_DYN_WHOLE_BODY_ACC && !d->include_base) {
     pl_set_error("whole_body_acc requires include_base=True on this path");
+    return -1;
+  }
+  if (d->dynamics == PL_DYN_CENTROIDAL_VEL && !d->include_base) {
+    pl_set_error("centroidal_vel requires include_base=True on this path (OCP_ARGS default, ocp_args.py:5)");
     return -1;
   }
   if (d->nodes < 2 || d->n_feet != 4) { pl_set_error("need nodes >= 2 and 4 feet"); return -1; }
@@ -902,9 +913,10 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   const bool has_arm = d->arm_ee_frame >= 0;
   O.nf = 12 + (has_ext ? 3 : 0);
   O.nee = 4 + (has_ext ? 1 : 0);
-  O.nx = M.nq + M.nv;
-  O.ndx = 2 * M.nv;
-  O.na = (O.dyn == PL_DYN_ABA) ? 0 : M.nv;
+  const bool cv = (O.dyn == PL_DYN_CV);
+  O.nx = cv ? 6 + M.nq : M.nq + M.nv;   // centroidal_vel: x = [h, q] (ocp_centroidal_vel.py:50-52)
+  O.ndx = cv ? 6 + M.nv : 2 * M.nv;
+  O.na = (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC) ? M.nv : 0;
   O.tau_nodes = (O.dyn == PL_DYN_RNEA) ? d->tau_nodes : 0;
   O.mu = d->mu;
   for (int k = 0; k < 4; ++k) O.feet[k] = frame_ref(model, d->foot_frames[k]);
@@ -1299,6 +1311,11 @@ extern "C" int pl_mpc_get_state(pl_ocp* o, double* x_state) {
   return 0;
 }
 
+extern "C" int pl_mpc_get_stats(pl_ocp* o, pl_stats* stats) {
+  REQUIRE_DEVICE(o);
+  return fetch_stats(o, stats);
+}
+
 extern "C" int pl_mpc_export(pl_ocp* o, void* device_dst) {
   REQUIRE_DEVICE(o);
   PlOcpHandle* h = &o->h;
@@ -1511,11 +1528,12 @@ int cas_ready() {
   return 1;
 }
 
-// layout of u_i in the bound OCP: a | forces | tau
+// retract_solution outputs of the bound OCP: inputs ahead of the forces (na), forces
+// (nf), joint torques (nt: u's tau block for rnea, RNEA / u's tau_j for the others)
 void cas_u_split(const pl_ocp* o, int& na, int& nf, int& nt) {
   const PlOcpConst& O = o->h.oc;
   if (O.dyn == PL_DYN_RNEA) { na = O.na; nf = O.nf; nt = O.nj; }
-  else if (O.dyn == PL_DYN_ACC) { na = O.nv; nf = O.nf; nt = 0; }
+  else if (O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CV) { na = O.nv; nf = O.nf; nt = O.nj; }
   else { na = 0; nf = O.nf; nt = O.nj; }
 }
 
@@ -1589,13 +1607,19 @@ extern "C" int pl_casadi_bind(pl_ocp* o, int retract_steps) {
   for (int j = 0; j < h.n; ++j) c.sp_H.push_back(j);
   int na, nf, nt;
   cas_u_split(o, na, nf, nt);
+  if (h.oc.dyn == PL_DYN_CV && retract_steps >= h.N) {
+    pl_set_error("centroidal_vel retract needs node i + 1's velocities: retract_steps < N");
+    c.o = nullptr;
+    return -1;
+  }
   c.sp_q = dense_sp(retract_steps, h.oc.nq);
   c.sp_v = dense_sp(retract_steps, h.oc.nv);
-  c.sp_a = dense_sp(retract_steps, na);
+  c.sp_a = dense_sp(retract_steps, h.oc.nv);  // a: inputs (rnea / acc), ABA (aba), FD + dccrba (cv)
   c.sp_f = dense_sp(retract_steps, nf);
   int ntau = nt;
-  for (int i = 0; i < retract_steps; ++i)
-    if (o->nodes[i].nu - na - nf < ntau) ntau = o->nodes[i].nu - na - nf;
+  if (h.oc.dyn == PL_DYN_RNEA)
+    for (int i = 0; i < retract_steps; ++i)
+      if (o->nodes[i].nu - na - nf < ntau) ntau = o->nodes[i].nu - na - nf;
   c.sp_tau = dense_sp(retract_steps, std::max(ntau, 0));
   return 0;
 }
@@ -1763,28 +1787,65 @@ extern "C" const casadi_int* retract_solution_sparsity_out(casadi_int i) {
     default: return nullptr;
   }
 }
+// compile_solution of each OCP (ocp_whole_body_rnea.py:326-366, ocp_whole_body_acc.py:236-288,
+// ocp_whole_body_aba.py:216-264, ocp_centroidal_vel.py:262-324) on the host, with the
+// library's own point functions (dyn.h): a = ABA (aba), tau = RNEA joints (acc, cv),
+// cv: v from the inputs, a by forward difference with the base part from the
+// centroidal base_acc_dynamics; the step sizes are the bound handle's (problem 0).
 extern "C" int retract_solution(const double** arg, double** res, casadi_int*, double*, int) {
   if (!cas_ready() || !arg[0] || !arg[1]) return 1;
   const pl_ocp* o = g_cas.o;
   const PlModel& M = o->h.model;
-  const int S = g_cas.steps, nq = M.nq, nv = M.nv;
+  const PlOcpConst& O = o->h.oc;
+  const int S = g_cas.steps, nq = M.nq, nv = M.nv, nj = O.nj;
   int na, nf, nt;
   cas_u_split(o, na, nf, nt);
   const int ntau = (int)g_cas.sp_tau[1];
-  std::vector<double> xs(nq + nv);
+  const bool cv = O.dyn == PL_DYN_CV;
+  std::vector<double> xs(O.nx), a(nv), tau(nv);
+  PlFrameRef F0;
+  memset(&F0, 0, sizeof(F0));
+  const double* p = o->h_params.data();
+  if (cv && !(p[O.P.dt_min] > 0.0 && p[O.P.dt_max] > 0.0)) {
+    pl_set_error("retract_solution: the bound centroidal_vel OCP has no step sizes (pl_ocp_set_params)");
+    return 1;
+  }
   for (int i = 0; i < S; ++i) {
     const PlNode& nd = o->nodes[i];
     const double* dx = arg[0] + nd.x_off;
     const double* u = dx + o->h.ndx;
-    pl::VecIn<double> acc{dx, nullptr, 0.0, -1};
-    pl::integrate_q<double>(M, arg[1], acc, xs.data());
-    for (int k = 0; k < nv; ++k) xs[nq + k] = arg[1][nq + k] + dx[nv + k];
+    pl::dyn_eval(M, O, F0, cv ? PL_FN_INTEGRATE_CV : PL_FN_INTEGRATE_WB, 0, arg[1], dx, nullptr, nullptr, xs.data());
+    const double* q = cv ? xs.data() + 6 : xs.data();
+    const double* v = cv ? u : xs.data() + nq;
+    const double* f = u + (O.dyn == PL_DYN_ABA ? nj : na);
+    switch (O.dyn) {
+      case PL_DYN_ABA:
+        pl::dyn_eval(M, O, F0, PL_FN_ABA, 0, q, v, u, f, a.data());
+        break;
+      case PL_DYN_CV: {
+        const double dt = pl::node_dt(O, p, i);
+        const double* un = arg[0] + o->nodes[i + 1].x_off + o->h.ndx;
+        for (int k = 0; k < nv; ++k) a[k] = (un[k] - v[k]) / dt;
+        pl::dyn_eval(M, O, F0, PL_FN_BASE_ACC_CV, 0, q, v, a.data() + 6, f, a.data());
+      } break;
+      default:
+        for (int k = 0; k < nv; ++k) a[k] = u[k];
+    }
+    if (O.dyn == PL_DYN_ACC || cv) pl::dyn_eval(M, O, F0, PL_FN_RNEA, 0, q, v, a.data(), f, tau.data());
     // CasADi dense matrices are column-major: element (row i, col k) at k * S + i
-    if (res[0]) for (int k = 0; k < nq; ++k) res[0][k * S + i] = xs[k];
-    if (res[1]) for (int k = 0; k < nv; ++k) res[1][k * S + i] = xs[nq + k];
-    if (res[2]) for (int k = 0; k < na; ++k) res[2][k * S + i] = u[k];
-    if (res[3]) for (int k = 0; k < nf; ++k) res[3][k * S + i] = u[na + k];
-    if (res[4]) for (int k = 0; k < ntau; ++k) res[4][k * S + i] = u[na + nf + k];
+    if (res[0]) for (int k = 0; k < nq; ++k) res[0][k * S + i] = q[k];
+    if (res[1]) for (int k = 0; k < nv; ++k) res[1][k * S + i] = v[k];
+    if (res[2]) for (int k = 0; k < nv; ++k) res[2][k * S + i] = a[k];
+    if (res[3]) for (int k = 0; k < nf; ++k) res[3][k * S + i] = f[k];
+    if (res[4]) {
+      for (int k = 0; k < ntau; ++k) {
+        double t;
+        if (O.dyn == PL_DYN_RNEA) t = u[na + nf + k];
+        else if (O.dyn == PL_DYN_ABA) t = u[k];
+        else t = tau[6 + k];
+        res[4][k * S + i] = t;
+      }
+    }
   }
   return 0;
 }

@@ -561,12 +561,13 @@ void launch_factor_x(PlOcpHandle* h) {
 
 }  // namespace
 
-// ndx values of the shipped whole-body models: 36 (Go2 / B2), 48 (B2G); the handle
-// refuses others.
-bool factor_supports_ndx(int ndx) { return ndx == 36 || ndx == 48; }
+// ndx values of the shipped models: 36 (Go2 / B2 whole body), 48 (B2G whole body),
+// 24 (Go2 / B2 centroidal_vel: 6 + nv); the handle refuses others.
+bool factor_supports_ndx(int ndx) { return ndx == 24 || ndx == 36 || ndx == 48; }
 
 void launch_factor(PlOcpHandle* h) {
   switch (h->ndx) {
+    case 24: launch_factor_x<24>(h); break;
     case 36: launch_factor_x<36>(h); break;
     case 48: launch_factor_x<48>(h); break;
     default: break;

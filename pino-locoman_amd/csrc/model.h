@@ -49,7 +49,7 @@ struct PlFrameRef {
   double p[3];
 };
 
-enum { PL_DYN_RNEA = 0, PL_DYN_ACC = 1, PL_DYN_ABA = 2 };
+enum { PL_DYN_RNEA = 0, PL_DYN_ACC = 1, PL_DYN_ABA = 2, PL_DYN_CV = 3 };
 
 // Row-block kinds, emitted per node in the reference's subject_to order
 // (optimization/ocp.py:103-190 + setup_dynamics_constraints of each subclass).
@@ -69,6 +69,9 @@ enum {
   PL_RB_ARM,          // v_ee,rel == arm_vel_des                   (ocp.py:180)
   PL_RB_QJ,           // pos_min <= q_j <= pos_max                 (ocp.py:189)
   PL_RB_VJ,           // -vel_max <= v_j <= vel_max                (ocp.py:190)
+  PL_RB_CV_DYNH,      // dh_{i+1} == dh_i + h_dot(q, f) dt         (ocp_centroidal_vel.py:100)
+  PL_RB_CV_DYNQ,      // dq_{i+1} == dq_i + v dt, v = u[:nv]       (ocp_centroidal_vel.py:101)
+  PL_RB_CV_GAP,       // A(q) v - m h == 0                         (ocp_centroidal_vel.py:103-106)
   PL_RB_COUNT
 };
 

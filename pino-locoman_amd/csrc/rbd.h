@@ -475,6 +475,103 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
   }
 }
 
+// ---------------------------------------------------------------- centroidal
+// One pass over the tree for the centroidal model (DynamicsCentroidalVel,
+// dynamics_centroidal_vel.py:43-71, 136-148):
+//   hg   = A(q) v: pinocchio computeCentroidalMap applied to v, i.e. the total spatial
+//          momentum sum_j X_j^* (I_j v_j) about the CoM in world axes (linear first);
+//   hdot = com_dynamics(q, forces) = [sum_e f_e + (0, 0, -9.81 m), sum_e (p_e - com) x f_e] / m
+//          over the contact frames FR, FL, RR, RL (+ the external-force frame).
+// Bodies are pushed to world coordinates as they are visited (as in tree_pass), so
+// only the running sums stay live.  want_h = false skips the velocity recursion.
+template <class S, class QR, class VA, class InF>
+PL_HD void centroidal_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const QR& qrev, const VA& v,
+                           const InF& forces, bool want_h, bool want_hdot, S* hg, S* hdot) {
+  S R0[9];
+  quat_to_R(qb + 3, R0);
+  S p0[3] = {qb[0], qb[1], qb[2]};
+  S mc[3], H[6], pe[PL_MAXFEET + 1][3];
+  for (int k = 0; k < 3; ++k) mc[k] = S(0.0);
+  for (int k = 0; k < 6; ++k) H[k] = S(0.0);
+  for (int e = 0; e < PL_MAXFEET + 1; ++e)
+    for (int k = 0; k < 3; ++k) pe[e][k] = S(0.0);
+  // body j at world pose (oR, op) with local velocity vj: CoM moment, momentum, frames
+  auto visit = [&](int j, const S* oR, const S* op, const S* vj) {
+    S lc[3];
+    matvec(oR, M.lever[j], lc);
+    for (int k = 0; k < 3; ++k) mc[k] += M.mass[j] * (op[k] + lc[k]);
+    if (want_h) {
+      S hl[6], hw[6];
+      inertia_mul(M.mass[j], M.lever[j], M.Ic[j], vj, hl);
+      act_force(oR, op, hl, hw);
+      for (int k = 0; k < 6; ++k) H[k] += hw[k];
+    }
+    if (want_hdot) {
+      for (int e = 0; e < O.nee; ++e) {
+        const PlFrameRef& F = (e < O.nfeet) ? O.feet[e] : O.ext;
+        if (F.joint != j) continue;
+        S t[3];
+        matvec(oR, F.p, t);
+        for (int k = 0; k < 3; ++k) pe[e][k] = op[k] + t[k];
+      }
+    }
+  };
+  S v1[6];
+  for (int k = 0; k < 6; ++k) v1[k] = want_h ? S(v[k]) : S(0.0);
+  visit(1, R0, p0, v1);
+  for (int ch = 0; ch < M.nchains; ++ch) {
+    const int first = M.chain_first[ch];
+    const int L = M.chain_len[ch];
+    S pv[6], oR[9], op[3];
+    for (int k = 0; k < 6; ++k) pv[k] = v1[k];
+    for (int k = 0; k < 9; ++k) oR[k] = R0[k];
+    for (int k = 0; k < 3; ++k) op[k] = p0[k];
+#pragma unroll
+    for (int kk = 0; kk < PL_MAXCL; ++kk) {
+      if (kk >= L) break;
+      const int j = first + kk;
+      S s, c;
+      sincos_s(qrev(M.idx_q[j]), &s, &c);
+      S Rl[9];
+      rev_rot(M, j, s, c, Rl);
+      const double* pl = M.jp[j];
+      S vj[6];
+      if (want_h) {
+        act_inv_motion(Rl, pl, pv, vj);
+        S qd = v[M.idx_v[j]];
+        for (int k = 0; k < 3; ++k) vj[3 + k] += M.axis[j][k] * qd;
+      }
+      S oRj[9], t3[3];
+      matmul3(oR, Rl, oRj);
+      matvec(oR, pl, t3);
+      for (int k = 0; k < 3; ++k) op[k] = op[k] + t3[k];
+      for (int k = 0; k < 9; ++k) oR[k] = oRj[k];
+      visit(j, oR, op, vj);
+      if (want_h)
+        for (int k = 0; k < 6; ++k) pv[k] = vj[k];
+    }
+  }
+  const double m = M.total_mass;
+  S com[3];
+  for (int k = 0; k < 3; ++k) com[k] = mc[k] * (1.0 / m);
+  if (want_h) {  // shift the angular momentum from the world origin to the CoM
+    S cxl[3];
+    cross3(com, H, cxl);
+    for (int k = 0; k < 3; ++k) { hg[k] = H[k]; hg[3 + k] = H[3 + k] - cxl[k]; }
+  }
+  if (want_hdot) {
+    S dp[3] = {S(0.0), S(0.0), S(-9.81 * m)}, dl[3] = {S(0.0), S(0.0), S(0.0)};
+    for (int e = 0; e < O.nee; ++e) {
+      S f[3] = {forces[3 * e], forces[3 * e + 1], forces[3 * e + 2]};
+      S r[3] = {pe[e][0] - com[0], pe[e][1] - com[1], pe[e][2] - com[2]};
+      S t[3];
+      cross3(r, f, t);
+      for (int k = 0; k < 3; ++k) { dp[k] += f[k]; dl[k] += t[k]; }
+    }
+    for (int k = 0; k < 3; ++k) { hdot[k] = dp[k] * (1.0 / m); hdot[3 + k] = dl[k] * (1.0 / m); }
+  }
+}
+
 // ---------------------------------------------------------------- ABA
 // pinocchio::aba(model, data, q, v, [0_6; tau_j], f_ext) (dynamics_whole_body_torque.py:73-103),
 // articulated-body algorithm in local joint frames.  Generic per-body arrays

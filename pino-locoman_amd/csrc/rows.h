@@ -41,7 +41,7 @@ PL_HD double spline_vel_z(double phase, double period, double h_max, double v_lo
 PL_HD int node_type(const PlOcpConst& O, int i) { return i == 0 ? 0 : (i < O.tau_nodes ? 1 : 2); }
 PL_HD int node_nu(const PlOcpConst& O, int i) {
   if (O.dyn == PL_DYN_RNEA) return O.na + O.nf + (i < O.tau_nodes ? O.nj : 0);
-  if (O.dyn == PL_DYN_ACC) return O.nv + O.nf;
+  if (O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CV) return O.nv + O.nf;
   return O.nj + O.nf;
 }
 
@@ -85,37 +85,59 @@ template <class S, int DYN, class Emit>
 PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double* p, const VecIn<S>& dx,
                      const VecIn<S>& u, const VecIn<S>& dxn, Emit& emit, S* kstore, int kstride) {
   const int nv = O.nv, nq = O.nq, nj = O.nj;
+  constexpr bool CV = (DYN == PL_DYN_CV);
   const double* xi = p + O.P.x_init;
   const double dt = node_dt(O, p, i);
   const int type = node_type(O, i);
   // state: q = integrate(x_init.q, dq), v = x_init.v + dv   (ocp_whole_body_rnea.py:173-181);
+  // centroidal_vel: x = [h, q], dx = [dh, dq], v = u[:nv]    (ocp_centroidal_vel.py:109-127);
   // the free-flyer part of q in registers, the rest read through accessors
+  const double* xq = CV ? xi + 6 : xi;
+  const VecIn<S> dq = CV ? sub_in(dx, 6) : dx;
   S qb[7];
-  integrate_ff<S>(xi, dx, qb);
-  const RevQ<S, VecIn<S>> qrev{xi, dx};
-  const VelAcc<S, VecIn<S>> vel{xi + nq, sub_in(dx, nv)};
-  const int f_off = (DYN == PL_DYN_RNEA) ? O.na : (DYN == PL_DYN_ACC ? nv : nj);
+  integrate_ff<S>(xq, dq, qb);
+  const RevQ<S, VecIn<S>> qrev{xq, dq};
+  const auto vel = [&]() {
+    if constexpr (CV) return u;
+    else return VelAcc<S, VecIn<S>>{xi + nq, sub_in(dx, nv)};
+  }();
+  const int f_off = (DYN == PL_DYN_RNEA) ? O.na : ((DYN == PL_DYN_ACC || CV) ? nv : nj);
   const VecIn<S> a = u;                                   // rnea / acc: a = u[0:nv]
   const VecIn<S> forces = sub_in(u, f_off);
   const VecIn<S> tau_j = sub_in(u, DYN == PL_DYN_RNEA ? O.na + O.nf : 0);
-  const bool state_rows = (type != 0);
+  // centroidal_vel keeps the state rows at node 0 (ocp.py:137-140, 170-173)
+  const bool state_rows = CV || (type != 0);
   NodeKin<S> kin;
   kin.store = kstore;
   kin.stride = kstride;
-  constexpr bool want_tau = (DYN != PL_DYN_ABA);
+  constexpr bool want_tau = (DYN == PL_DYN_RNEA || DYN == PL_DYN_ACC);
   // A Jacobian column seeded on dx_{i+1}, or (rnea) on tau_j, has a zero tangent in the
   // tree pass and the ABA: every row that reads them then has a zero derivative, so
   // the pass is skipped (its values are not emitted for such a column's pattern).
-  bool tree = true;
+  // centroidal_vel: h and the forces do not enter the kinematics either; the
+  // centroidal pass reads the forces but not h.
+  bool tree = true, cen = CV;
   if constexpr (!std::is_same<S, double>::value) {
     const bool seed_dxn = dxn.seed >= 0 && dxn.seed < O.ndx;
     const bool seed_tau = DYN == PL_DYN_RNEA && u.seed >= O.na + O.nf && u.seed < O.na + O.nf + nj;
-    tree = !(seed_dxn || seed_tau);
+    const bool seed_h = CV && dx.seed >= 0 && dx.seed < 6;
+    const bool seed_f = CV && u.seed >= nv && u.seed < nv + O.nf;
+    tree = !(seed_dxn || seed_tau || seed_h || seed_f);
+    cen = CV && !(seed_dxn || seed_h);
   }
   if (tree && (want_tau || state_rows)) {
     tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin);
   } else {  // a skipped pass leaves zero (value and tangent) kinematic outputs
     for (int k = 0; k < PL_KIN_STORE_DUAL; ++k) kin.store[k * kstride] = S(0.0);
+    for (int k = 0; k < 3; ++k) kin.arm_vel[k] = S(0.0);
+  }
+  S hg[CV ? 6 : 1], hdot[CV ? 6 : 1];
+  if constexpr (CV) {
+    if (cen) {
+      centroidal_pass<S>(M, O, qb, qrev, vel, forces, true, true, hg, hdot);
+    } else {
+      for (int k = 0; k < 6; ++k) { hg[k] = S(0.0); hdot[k] = S(0.0); }
+    }
   }
   S aba_a[DYN == PL_DYN_ABA ? PL_MAXV : 1];
   if constexpr (DYN == PL_DYN_ABA) {
@@ -195,6 +217,17 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
         break;
       case PL_RB_VJ:
         for (int r = 0; r < nj; ++r) emit(vel[6 + r], -O.vel_max[r], O.vel_max[r]);
+        break;
+      case PL_RB_CV_DYNH:
+        if constexpr (CV)
+          for (int r = 0; r < 6; ++r) emit(dxn[r] - (dx[r] + hdot[r] * dt), 0.0, 0.0);
+        break;
+      case PL_RB_CV_DYNQ:
+        for (int r = 0; r < nv; ++r) emit(dxn[6 + r] - (dx[6 + r] + vel[r] * dt), 0.0, 0.0);
+        break;
+      case PL_RB_CV_GAP:
+        if constexpr (CV)
+          for (int r = 0; r < 6; ++r) emit(hg[r] - M.total_mass * (xi[r] + dx[r]), 0.0, 0.0);
         break;
     }
   }

@@ -1,7 +1,8 @@
 // Tracking targets and objective terms (host+device, doubles).
 //
 // x_des = [q0, base_vel_des, 0], dx_des = difference(x_init, x_des)
-//   (ocp_whole_body_rnea.py:91-94, ocp_whole_body_acc.py:73-76, ocp_whole_body_aba.py:69-72);
+//   (ocp_whole_body_rnea.py:91-94, ocp_whole_body_acc.py:73-76, ocp_whole_body_aba.py:69-72;
+//   centroidal_vel: x_des = [base_vel_des, q0], ocp_centroidal_vel.py:60-63);
 // f_des = 0.8 / 1.2 * m g / n_contacts on front / rear feet, 0 on the end effector,
 // u_des = [0_a, f_des, 0_tau] (ocp_whole_body_rnea.py:96-106 and siblings);
 // objective sum_i |dx_i - dx_des|_Q^2 + |u_i - u_des|_R^2 (+ |tau_0 - tau_prev|_W^2)
@@ -14,6 +15,12 @@ namespace pl {
 
 PL_HD void compute_dx_des(const PlModel& M, const PlOcpConst& O, const double* p, double* dxd) {
   const double* xi = p + O.P.x_init;
+  if (O.dyn == PL_DYN_CV) {
+    // x_des = [base_vel_des, q0], dx_des = [h_des - h, difference(q, q0)] (ocp_centroidal_vel.py:61-63)
+    for (int k = 0; k < 6; ++k) dxd[k] = p[O.P.base_vel_des + k] - xi[k];
+    difference_q(M, xi + 6, O.q0, dxd + 6);
+    return;
+  }
   difference_q(M, xi, O.q0, dxd);
   for (int k = 0; k < O.nv; ++k) {
     double vd = (k < 6) ? p[O.P.base_vel_des + k] : 0.0;
@@ -32,7 +39,7 @@ PL_HD double f_des_comp(const PlModel& M, const PlOcpConst& O, const double* p, 
 
 // Offset of the forces inside u for the dynamics kind.
 PL_HD int u_force_off(const PlOcpConst& O) {
-  return (O.dyn == PL_DYN_RNEA) ? O.na : (O.dyn == PL_DYN_ACC ? O.nv : O.nj);
+  return (O.dyn == PL_DYN_RNEA) ? O.na : ((O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CV) ? O.nv : O.nj);
 }
 
 // u_des[k] (k indexes the padded input of length nu_0).

@@ -66,6 +66,7 @@ EXPORTS = {
     "pl_mpc_setup": (C.c_int, [C.c_void_p, _dp, _dp]),
     "pl_mpc_step": (C.c_int, [C.c_void_p, C.c_int]),
     "pl_mpc_get_state": (C.c_int, [C.c_void_p, _dp]),
+    "pl_mpc_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "pl_mpc_export": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pl_ocp_sync": (C.c_int, [C.c_void_p]),
     "pl_state_integrate": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
@@ -77,6 +78,10 @@ EXPORTS = {
     "pl_debug_get": (C.c_int, [C.c_void_p, C.c_char_p, _dp, C.c_longlong]),
     "pl_debug_nodes": (C.c_int, [C.c_void_p, _ip]),
     "pl_debug_admm": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "pl_dyn_create": (C.c_int, [C.c_void_p, _ip, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    "pl_dyn_destroy": (None, [C.c_void_p]),
+    "pl_dyn_sizes": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _ip, _ip]),
+    "pl_dyn_eval": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp]),
 }
 
 _lib = None

@@ -16,9 +16,10 @@ import time
 import numpy as np
 
 from . import _lib
+from .dynamics import DYNAMICS_CLASSES, Dynamics  # noqa: F401  (Dynamics: plugin base class)
 from .gait import horizon_dts
 
-DYN_CODES = {"whole_body_rnea": 0, "whole_body_acc": 1, "whole_body_aba": 2}
+DYN_CODES = {"whole_body_rnea": 0, "whole_body_acc": 1, "whole_body_aba": 2, "centroidal_vel": 3}
 GAIT_CODES = {"trot": 0, "walk": 1, "stand": 2}
 
 # ocp.py:267-273 plus the OSQP 0.6 library defaults it leaves untouched.
@@ -50,7 +51,14 @@ class Layout:
         self.nx = self.nq + self.nv
         self.ndx = 2 * self.nv
         nv, nj, nf = self.nv, self.nj, self.nf
-        if dynamics == "whole_body_rnea":
+        if dynamics == "centroidal_vel":
+            # x = [h (6), q], dx = [dh, dq], u = [v | f] (ocp_centroidal_vel.py:49-66)
+            self.nx, self.ndx = 6 + self.nq, 6 + nv
+            self.tau_nodes = 0
+            self.na = 0
+            self.nu = [nv + nf] * nodes
+            self.f_idx, self.tau_idx = nv, None
+        elif dynamics == "whole_body_rnea":
             self.tau_nodes = tau_nodes
             self.na = nv
             self.nu = [nv + nf + nj] * tau_nodes + [nv + nf] * (nodes - tau_nodes)
@@ -115,7 +123,10 @@ def default_weights(robot, dynamics, layout):
         Qj += [100] * 6
     Qv = [2000, 2000, 1000, 1000, 1000, 2000] + [1] * nj
     Q = np.array(Qb + Qj + Qv, float)
-    if dynamics == "whole_body_rnea":
+    if dynamics == "centroidal_vel":  # ocp_centroidal_vel.py:23-47
+        Q = np.array([1000] * 6 + Qb + Qj, float)
+        R = np.array([1] * robot.nv + [1e-3] * nf, float)
+    elif dynamics == "whole_body_rnea":
         R = np.array([1e-3] * layout.na + [1e-3] * nf + [1e-4] * nj, float)
     elif dynamics == "whole_body_acc":
         R = np.array([1e-3] * robot.nv + [1e-3] * nf, float)
@@ -271,6 +282,11 @@ class BatchedOCP:
         _lib.check(_lib.lib().pl_mpc_get_state(self.h, _lib.dptr(xs)))
         return xs
 
+    def mpc_stats(self):
+        stats = (_lib.Stats * self.batch)()
+        _lib.check(_lib.lib().pl_mpc_get_stats(self.h, stats))
+        return {k: np.array([getattr(s, k) for s in stats]) for k, _ in _lib.Stats._fields_ if k != "pad"}
+
     def mpc_export(self, device_ptr):
         _lib.check(_lib.lib().pl_mpc_export(self.h, C.c_void_p(device_ptr)))
 
@@ -314,37 +330,10 @@ class ModelCache:
         return cls._cache[key][1]
 
 
-class _StateMap:
-    def __init__(self, fn):
-        self._fn = fn
-
-    def __call__(self, *args):
-        return self._fn(*args)
-
-
-class Dynamics:
-    """Plugin surface of dynamics/dynamics.py: factory methods returning callables.
-
-    ``state_integrate()`` / ``state_difference()`` (dynamics_whole_body_torque.py:11-40)
-    run the library's own Lie-group code on the host (pl_state_integrate)."""
-
-    def __init__(self, robot):
-        self.model = robot.model
-        self.nq, self.nv = robot.nq, robot.nv
-        self.nj = self.nq - 7
-        self._h = ModelCache.get(robot.model)
-
-    def state_integrate(self):
-        return _StateMap(lambda x, dx: self._h.integrate(x, dx))
-
-    def state_difference(self):
-        return _StateMap(lambda x0, x1: self._h.difference(x0, x1))
-
-
 class OCP:
     """Single-problem OCP with the reference's method surface (ocp.py:11-480)."""
 
-    def __init__(self, robot, solver, nodes, dynamics, tau_nodes=3, include_acc=True, include_base=True):
+    def __init__(self, robot, solver, nodes, dynamics, tau_nodes=3, include_acc=True, include_base=True, device=0):
         if solver != "osqp":
             raise ValueError(f"Solver {solver} not supported on the MI355X path (ocp.py:321-322); "
                              "the Fatrop interior-point path is a later row of the build plan")
@@ -360,7 +349,7 @@ class OCP:
         self.nodes = nodes
         self.mass = robot.mass
         self.dynamics = dynamics
-        self.dyn = Dynamics(robot)
+        self.dyn = DYNAMICS_CLASSES[dynamics](robot, device=device)
         self.layout = Layout(robot, dynamics, nodes, tau_nodes)
         L = self.layout
         self.nx, self.ndx_opt, self.nu_opt = L.nx, L.ndx, L.nu
@@ -368,15 +357,18 @@ class OCP:
         self.tau_nodes = L.tau_nodes
         self.na_opt = L.na
         self.include_acc, self.include_base = include_acc, include_base
-        self.x_nom = np.concatenate((robot.q0, [0] * self.nv))
+        if dynamics == "centroidal_vel":
+            self.x_nom = np.concatenate(([0] * 6, robot.q0))  # CoM momentum + joint pos (ocp_centroidal_vel.py:16)
+        else:
+            self.x_nom = np.concatenate((robot.q0, [0] * self.nv))
         self.q_sol, self.v_sol, self.a_sol, self.forces_sol, self.tau_sol = [], [], [], [], []
         self.DX_prev = None
         self.U_prev = None
         self.lam_g = None
         self.solve_time = None
         self.stats = None
-        self._backend = BatchedOCP(robot, dynamics, nodes, batch=1, tau_nodes=tau_nodes, include_acc=include_acc,
-                                   include_base=include_base,
+        self._backend = BatchedOCP(robot, dynamics, nodes, batch=1, device=device, tau_nodes=tau_nodes,
+                                   include_acc=include_acc, include_base=include_base,
                                    gait_type=self.gait_sequence.gait_type if self.gait_sequence else "trot",
                                    gait_period=self.gait_sequence.gait_period if self.gait_sequence else 0.8)
         self.p = {"tau_prev": np.zeros(self.nj), "W_diag": np.zeros(self.nj), "ext_force_des": np.zeros(3),
@@ -402,7 +394,7 @@ class OCP:
         f = self._f_des()
         if self.dynamics == "whole_body_rnea":
             return np.concatenate([np.zeros(self.na_opt), f, np.zeros(self.nj)])
-        if self.dynamics == "whole_body_acc":
+        if self.dynamics in ("whole_body_acc", "centroidal_vel"):
             return np.concatenate([np.zeros(self.nv), f])
         return np.concatenate([np.zeros(self.nj), f])
 
@@ -460,6 +452,8 @@ class OCP:
                 u_prev = self.U_prev[i]
                 if self.dynamics == "whole_body_aba":
                     u = np.concatenate([u_prev[:self.nj], f_des])
+                elif self.dynamics == "centroidal_vel":  # ocp_centroidal_vel.py:152-158
+                    u = np.concatenate([u_prev[:self.nv], f_des])
                 else:
                     u = np.concatenate([u_prev[:self.na_opt], f_des])
                     if self.dynamics == "whole_body_rnea" and i < self.tau_nodes:
@@ -488,7 +482,8 @@ class OCP:
         return x
 
     def retract_stacked_sol(self, sol_x, retract_all=True):
-        """ocp_whole_body_rnea.py:293-324."""
+        """ocp_whole_body_rnea.py:293-324 (ocp_whole_body_acc.py:195-234,
+        ocp_whole_body_aba.py:177-214: a from aba_dynamics at the node)."""
         L = self.layout
         x_init = self.p["x_init"]
         integ = self.dyn.state_integrate()
@@ -502,8 +497,11 @@ class OCP:
                 self.v_sol.append(xs[self.nq:])
                 u = U[i]
                 if self.dynamics == "whole_body_aba":
-                    self.tau_sol.append(u[:self.nj])
-                    self.forces_sol.append(u[self.f_idx:])
+                    tau_j, forces = u[:self.nj], u[self.f_idx:]
+                    self.tau_sol.append(tau_j)
+                    self.forces_sol.append(forces)
+                    ext = self.ext_force_frame
+                    self.a_sol.append(self.dyn.aba_dynamics(ext)(xs[:self.nq], xs[self.nq:], tau_j, forces))
                 else:
                     self.a_sol.append(u[:self.na_opt])
                     self.forces_sol.append(u[self.f_idx:self.tau_idx] if self.tau_idx else u[self.f_idx:])
@@ -533,17 +531,59 @@ class OCPWholeBodyABA(OCP):
         super().__init__(robot, solver, nodes, "whole_body_aba")
 
 
-class _CentroidalOnCPU:
+class OCPCentroidalVel(OCP):
+    """ocp_centroidal_vel.py: x = [h, q], dx = [dh, dq], u = [v | forces]."""
+
+    def __init__(self, robot, solver, nodes, include_base=False):
+        if not include_base:
+            raise ValueError("centroidal_vel with include_base=False (base velocity from A_b^-1, "
+                             "ocp_centroidal_vel.py:118-127) is not on the MI355X path; OCP_ARGS uses True")
+        super().__init__(robot, solver, nodes, "centroidal_vel", include_base=include_base)
+        self.nv_opt = self.nv
+
+    def retract_stacked_sol(self, sol_x, retract_all=True):
+        """ocp_centroidal_vel.py:195-260: q, h from the state; v from the inputs; a by a
+        forward difference of the input velocities, its base part replaced by
+        base_acc_dynamics (pinocchio dccrba).  The reference's slice of the node after
+        the last input is empty there (an error); the last node reuses the previous
+        node's difference."""
+        L = self.layout
+        x_init = self.p["x_init"]
+        integ = self.dyn.state_integrate()
+        DX, U = L.split(np.asarray(sol_x, float))
+        self.DX_prev = [np.array(d) for d in DX]
+        self.U_prev = [np.array(u) for u in U]
+        dts = self.dts
+        base_acc = self.dyn.base_acc_dynamics(self.ext_force_frame)
+        for i in range(self.nodes):
+            if not (i == 0 or retract_all):
+                continue
+            xs = integ(x_init, DX[i])
+            q = xs[6:]
+            u = U[i]
+            v, forces = u[:self.nv], u[self.f_idx:]
+            k = i if i + 1 < self.nodes else i - 1
+            a = (U[k + 1][:self.nv] - U[k][:self.nv]) / dts[k]
+            a_b = base_acc(q, v, a[6:], forces)
+            self.q_sol.append(q)
+            self.v_sol.append(v)
+            self.a_sol.append(np.concatenate([a_b, a[6:]]))
+            self.forces_sol.append(forces)
+        if retract_all:
+            self.q_sol.append(integ(x_init, DX[-1])[6:])
+
+
+class _CentroidalAcc:
     def __init__(self, *args, **kwargs):
-        raise NotImplementedError("centroidal_vel / centroidal_acc are not on the MI355X path in this release "
-                                  "(SURVEY.md section 8f, row 3); the CPU oracle restates centroidal_vel for parity")
+        raise NotImplementedError("centroidal_acc (ocp_centroidal_acc.py) is not on the MI355X path: no BASELINE "
+                                  "config uses it (SURVEY.md section 8f, row 3)")
 
 
 def make_ocp(dynamics, default_args, **kwargs):
     """ocp_factory.py:8-27."""
     ocp_classes = {
-        "centroidal_vel": _CentroidalOnCPU,
-        "centroidal_acc": _CentroidalOnCPU,
+        "centroidal_vel": OCPCentroidalVel,
+        "centroidal_acc": _CentroidalAcc,
         "whole_body_acc": OCPWholeBodyAcc,
         "whole_body_aba": OCPWholeBodyABA,
         "whole_body_rnea": OCPWholeBodyRNEA,

@@ -22,8 +22,9 @@ GAIT_PERIOD = 0.8
 GRAV = 9.81
 
 
-def random_state(robot, gidx):
-    """(x_state, t0, vx) of global problem ``gidx``."""
+def random_state(robot, gidx, dynamics="whole_body_rnea"):
+    """(x_state, t0, vx) of global problem ``gidx``.  x = [q, v]; for centroidal_vel
+    x = [h, q] with the scaled momentum h = [v_base, 0.1 w_base] of the same draw."""
     rng = np.random.default_rng(1234 + gidx)
     q = robot.q0.copy()
     q[:3] += rng.normal(0.0, 0.01, 3)
@@ -35,6 +36,8 @@ def random_state(robot, gidx):
     v = rng.normal(0.0, 0.1, robot.nv)
     t0 = rng.uniform(0.0, GAIT_PERIOD)
     vx = rng.uniform(0.0, 0.3)
+    if dynamics == "centroidal_vel":
+        return np.concatenate([v[:3], 0.1 * v[3:6], q]), t0, vx
     return np.concatenate([q, v]), t0, vx
 
 
@@ -49,7 +52,7 @@ def problem_values(robot, dynamics, N, gidx, lay=None, k=0):
     """Parameter values (Layout.pack keys) of problem ``gidx`` at MPC step ``k``
     (gait time t0 + k * dt_min), and its initial state."""
     lay = lay or Layout(robot, dynamics, N)
-    xs, t0, vx = random_state(robot, gidx)
+    xs, t0, vx = random_state(robot, gidx, dynamics)
     Q, Rw, W = default_weights(robot, dynamics, lay)
     contact, swing = robot.gait_sequence.get_gait_schedule(t0 + k * DT_MIN, horizon_dts(DT_MIN, DT_MAX, N), N)
     vals = dict(x_init=xs, dt_min=DT_MIN, dt_max=DT_MAX, n_contacts=robot.gait_sequence.n_contacts,
@@ -71,7 +74,7 @@ def u_des(robot, lay, n_contacts):
     if lay.dynamics == "whole_body_aba":
         return np.concatenate([np.zeros(robot.nj), f])
     tail = [np.zeros(robot.nj)] if lay.dynamics == "whole_body_rnea" else []
-    return np.concatenate([np.zeros(lay.na), f] + tail)
+    return np.concatenate([np.zeros(lay.f_idx), f] + tail)
 
 
 def initial_guess(robot, lay, n_contacts):

@@ -20,7 +20,8 @@ from oracle.ocp import OracleOCP
 
 HEADER = os.path.join(ROOT, "include", "pinoloco.h")
 CONFIGS = [("go2", "whole_body_rnea", 20, 1392, 2032, 318), ("b2", "whole_body_aba", 40, 2436, 3680, None),
-           ("b2g", "whole_body_acc", 50, 4398, 6397, None), ("b2g", "whole_body_rnea", 50, 4452, 6505, 609)]
+           ("b2g", "whole_body_acc", 50, 4398, 6397, None), ("b2g", "whole_body_rnea", 50, 4452, 6505, 609),
+           ("go2", "centroidal_vel", 20, 1104, 1744, None)]
 
 
 def header_functions():
@@ -149,7 +150,7 @@ def test_host_state_maps_match_oracle(rname):
 
 
 @pytest.mark.parametrize("rname,dyn,N", [("go2", "whole_body_rnea", 20), ("b2", "whole_body_aba", 40),
-                                         ("b2g", "whole_body_acc", 50)])
+                                         ("b2g", "whole_body_acc", 50), ("go2", "centroidal_vel", 20)])
 def test_layout_pack_matches_oracle(rname, dyn, N):
     from pinoloco.ocp import Layout
     from pinoloco.synthetic import problem_values, initial_guess

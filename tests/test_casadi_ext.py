@@ -109,3 +109,39 @@ def test_destroy_unbinds():
     bo.close()
     with pytest.raises(_lib.PinolocoError, match="no OCP bound"):
         fr(np.zeros(n), np.zeros(nx))
+
+
+@pytest.mark.parametrize("dyn", ["whole_body_aba", "whole_body_acc"])
+def test_retract_solution_dynamics_outputs(dyn):
+    """retract_solution fills a (ABA, ocp_whole_body_aba.py:239) and tau (RNEA joint rows,
+    ocp_whole_body_acc.py:262) from the library's point functions, against the oracle."""
+    from oracle import rbd
+    from oracle.ocp import OracleOCP
+    from pinoloco import casadi_ext
+    from pinoloco.ocp import BatchedOCP
+    R = make_robot("b2g")
+    N = 6
+    bo = BatchedOCP(R, dyn, N, batch=1, device=-1)
+    casadi_ext.bind(bo, 3)
+    rng = np.random.default_rng(5)
+    o = OracleOCP(R, dyn, N)
+    sol = rng.normal(size=bo.n) * 0.1
+    x_init = np.concatenate([R.q0, rng.normal(size=R.nv) * 0.1])
+    q, v, a, f, tau = casadi_ext.ExternalFunction("retract_solution")(sol, x_init)
+    M = rbd.ModelArrays(R.model)
+    frames = list(R.foot_frames) + [R.ext_force_frame]
+    DX, U = o.split(sol)
+    assert a.shape == (3, R.nv) and tau.shape == (3, R.nj)
+    for i in range(3):
+        xs = o.integrate_state(x_init, DX[i])
+        qi, vi = xs[:R.nq], xs[R.nq:]
+        if dyn == "whole_body_aba":
+            want_a = rbd.aba_dynamics(M, frames, qi, vi, U[i][:R.nj], U[i][R.nj:])
+            assert np.abs(a[i] - want_a).max() < 1e-10 * max(1, np.abs(want_a).max())
+            assert np.array_equal(tau[i], U[i][:R.nj])
+        else:
+            assert np.array_equal(a[i], U[i][:R.nv])
+            want_t = rbd.rnea_dynamics(M, frames, qi, vi, U[i][:R.nv], U[i][R.nv:])[6:]
+            assert np.abs(tau[i] - want_t).max() < 1e-12 * max(1, np.abs(want_t).max())
+    casadi_ext.unbind()
+    bo.close()

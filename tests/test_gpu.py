@@ -21,19 +21,32 @@ from conftest import golden, make_robot
 
 pytestmark = pytest.mark.gpu
 
-CONFIGS = [("go2_rnea_n20", "go2", "whole_body_rnea", 20), ("b2_aba_n40", "b2", "whole_body_aba", 40),
-           ("b2g_acc_n50", "b2g", "whole_body_acc", 50), ("b2g_rnea_n50", "b2g", "whole_body_rnea", 50)]
+CONFIGS = [("go2_rnea_n20", "go2", "whole_body_rnea", 20), ("go2_cv_n20", "go2", "centroidal_vel", 20),
+           ("b2_aba_n40", "b2", "whole_body_aba", 40), ("b2g_acc_n50", "b2g", "whole_body_acc", 50),
+           ("b2g_rnea_n50", "b2g", "whole_body_rnea", 50)]
+# edge-case fixtures (tests/golden/make_golden.py): gaits, quaternion branch, OSQP
+# termination at 25/50/75/100, infeasible QPs, line-search branches 2 and 3
+EDGE = [(f"go2_rnea_n20_{k}", "go2", "whole_body_rnea", 20) for k in ("walk", "stand", "eps2", "infeas", "eps5", "eps6")]
 
 
 def _rel(a, b):
     return np.abs(np.asarray(a) - np.asarray(b)).max() / max(1e-300, np.abs(np.asarray(b)).max())
 
 
+def _settings(G):
+    """OSQP settings and gait the fixture was generated with."""
+    eps = G["osqp_eps"] if "osqp_eps" in G else (1e-3, 1e-3)
+    mi = int(G["osqp_max_iter"]) if "osqp_max_iter" in G else 100
+    gait = str(G["gait"]) if "gait" in G else "trot"
+    return {"eps_abs": float(eps[0]), "eps_rel": float(eps[1]), "max_iter": mi}, gait
+
+
 def _batched(rname, dyn, N, G, B=None):
     from pinoloco.ocp import BatchedOCP
-    R = make_robot(rname)
+    settings, gait = _settings(G)
+    R = make_robot(rname, gait)
     B = B or G["P"].shape[0]
-    bo = BatchedOCP(R, dyn, N, batch=B, device=0)
+    bo = BatchedOCP(R, dyn, N, batch=B, device=0, osqp_settings=settings, gait_type=gait)
     bo.set_params(G["P"][:B])
     bo.set_x(G["X"][:B])
     bo.init_solver()
@@ -52,6 +65,8 @@ def test_eval_sqp_data_matches_golden(name, rname, dyn, N):
         assert np.array_equal(lbg[b], G["lbg"][b]) and np.array_equal(ubg[b], G["ubg"][b])
         assert _rel(grad[b], G["grad"][b]) < 1e-12
         assert f[b] == pytest.approx(float(G["f"][b]), rel=1e-12)
+        if f"J_data_{b}" not in G:
+            continue  # Jacobians are stored for the first problems only
         Jg = sp.csr_matrix((G[f"J_data_{b}"], G[f"J_indices_{b}"], G[f"J_indptr_{b}"]), shape=(bo.m, bo.n))
         ref = np.asarray(Jg[rows, cols]).ravel()
         assert _rel(J[b], ref) < 1e-12
@@ -60,41 +75,72 @@ def test_eval_sqp_data_matches_golden(name, rname, dyn, N):
     bo.close()
 
 
-@pytest.mark.parametrize("name,rname,dyn,N", CONFIGS)
+@pytest.mark.parametrize("name,rname,dyn,N", CONFIGS + EDGE)
 def test_sqp_step_matches_golden(name, rname, dyn, N):
+    """One SQP iteration per problem: solver outcome exact, step <= 1e-8; the max
+    violation at the returned point <= 1e-10 against the oracle's metric at the same
+    point (and <= 1e-6 against the golden value, which sits at the oracle's own x)."""
+    from oracle.ocp import OracleOCP
     G = golden(f"sqp_{name}.npz")
     R, bo = _batched(rname, dyn, N, G)
     st = bo.solve()
     dx = bo.get_step()
     xn = bo.get_x()
+    o = OracleOCP(R, dyn, N)
     for b in range(G["P"].shape[0]):
-        assert st["status"][b] == G["status"][b]
-        assert st["admm_iters"][b] == G["iters"][b]
-        assert st["ls_accepted"][b] == G["accepted"][b]
-        assert st["ls_branch"][b] == G["branch"][b]
-        assert st["ls_trials"][b] == G["trials"][b]
-        assert st["ls_alpha"][b] == G["alpha"][b]
-        assert _rel(dx[b], G["dx"][b]) < 1e-8
-        assert _rel(xn[b], G["x_new"][b]) < 1e-8
-        assert st["viol_max"][b] == pytest.approx(float(G["viol_max"][b]), rel=1e-6)
+        assert st["status"][b] == G["status"][b], b
+        assert st["admm_iters"][b] == G["iters"][b], b
+        assert st["ls_accepted"][b] == G["accepted"][b], b
+        assert st["ls_branch"][b] == G["branch"][b], b
+        assert st["ls_trials"][b] == G["trials"][b], b
+        assert st["ls_alpha"][b] == G["alpha"][b], b
+        if np.all(np.isnan(G["dx"][b])):  # infeasible QP: NaN step, x unchanged (ocp.py:478-480)
+            assert np.all(np.isnan(dx[b])) and np.array_equal(xn[b], G["X"][b])
+        else:
+            assert _rel(dx[b], G["dx"][b]) < 1e-8, b
+        assert _rel(xn[b], G["x_new"][b]) < 1e-8, b
+        g, l, u = o.eval_g(xn[b], G["P"][b])
+        assert st["viol_max"][b] == pytest.approx(o.violation_max(g, l, u), rel=1e-10, abs=1e-14), b
+        assert st["viol_max"][b] == pytest.approx(float(G["viol_max"][b]), rel=1e-6, abs=1e-12), b
     bo.close()
 
 
-def test_device_mpc_loop_matches_oracle_loop():
+def test_fixture_coverage():
+    """The golden set exercises the reference's branches: line-search branches 1/2/3
+    and the rejection path (ocp.py:455-480), OSQP termination at 25/50/75/100 and an
+    infeasible QP, trot/walk/stand gaits (gait_sequence.py:53-75), the quaternion
+    trace <= 0 branch, and >= 8 problems for each BASELINE config."""
+    branches, iters, status, gaits, trace, rejected = set(), set(), set(), set(), 0, 0
+    for name, _, _, _ in CONFIGS + EDGE:
+        G = golden(f"sqp_{name}.npz")
+        branches |= set(G["branch"].tolist())
+        iters |= set(G["iters"].tolist())
+        status |= set(G["status"].tolist())
+        gaits.add(str(G["gait"]))
+        trace += int(G["quat_trace_le0"].sum())
+        rejected += int((G["accepted"] == 0).sum())
+        if name in [c[0] for c in CONFIGS]:
+            assert G["P"].shape[0] >= 8, name
+    assert {1, 2, 3} <= branches and rejected > 0
+    assert {25, 50, 75, 100} <= iters and -3 in status
+    assert gaits == {"trot", "walk", "stand"} and trace > 0
+
+
+@pytest.mark.parametrize("name,rname,dyn,N", [CONFIGS[0], CONFIGS[1], EDGE[0], EDGE[1], EDGE[4]])
+def test_device_mpc_loop_matches_oracle_loop(name, rname, dyn, N):
     """run_mpc.py:127-143 executed on the device (gait, x_init, warm start, solve,
-    x <- integrate(x, DX[1])) vs the oracle's closed loop in the golden file."""
-    from pinoloco.ocp import BatchedOCP
-    G = golden("sqp_go2_rnea_n20.npz")
-    R = make_robot("go2")
-    bo = BatchedOCP(R, "whole_body_rnea", 20, batch=1, device=0)
-    bo.set_params(G["P"][:1])
-    bo.set_x(G["X"][:1])
-    bo.init_solver()
+    x <- integrate(x, DX[1])) vs the oracle's closed loop in the golden file: states
+    <= 1e-7 and each step's solver outcome (status, ADMM iterations, branch, trials)."""
+    G = golden(f"sqp_{name}.npz")
+    R, bo = _batched(rname, dyn, N, G, B=1)
     bo.mpc_setup(G["XS"][:1], G["T0"][:1])
     for k, want in enumerate(G["loop_states"]):
         bo.mpc_step(k)
         got = bo.mpc_state()[0]
         assert _rel(got, want) < 1e-7, k
+        st = bo.mpc_stats()
+        assert [st["status"][0], st["admm_iters"][0], st["ls_branch"][0], st["ls_trials"][0]] == \
+            G["loop_stats"][k].tolist(), k
     bo.close()
 
 
@@ -128,6 +174,63 @@ def test_make_ocp_surface_matches_oracle():
         assert len(ocp.q_sol) == k + 1 and ocp.get_tau_sol(1).shape == (R.nj,)
 
 
+def test_make_ocp_centroidal_vel_surface_matches_oracle():
+    """make_ocp("centroidal_vel") (ocp_centroidal_vel.py) in the run_mpc.py:115-143 loop on
+    the GPU against the oracle's closed loop; retract fills q / v / a (forward
+    difference + centroidal base_acc_dynamics) / forces."""
+    from oracle import rbd
+    from pinoloco.ocp import OCP_ARGS, make_ocp
+    from pinoloco.synthetic import DT_MAX, DT_MIN, SWING_HEIGHT, SWING_VEL_LIMITS, random_state
+    G = golden("sqp_go2_cv_n20.npz")
+    R = make_robot("go2")
+    xs, t0, vx = random_state(R, 0, "centroidal_vel")
+    ocp = make_ocp("centroidal_vel", OCP_ARGS["centroidal_vel"], robot=R, nodes=20, solver="osqp")
+    ocp.set_time_params(DT_MIN, DT_MAX)
+    ocp.set_swing_params(SWING_HEIGHT, list(SWING_VEL_LIMITS))
+    ocp.set_tracking_targets([vx, 0, 0, 0, 0, 0], [0, 0, 0], [0, 0, 0])
+    x_init = xs.copy()
+    ocp.update_initial_state(x_init)
+    ocp.update_gait_sequence(t0)
+    ocp.init_solver()
+    for k, want in enumerate(G["loop_states"]):
+        ocp.update_initial_state(x_init)
+        ocp.update_gait_sequence(t0 + k * DT_MIN)
+        ocp.warm_start()
+        ocp.solve(retract_all=False)
+        x_init = ocp.dyn.state_integrate()(x_init, ocp.DX_prev[1])
+        assert _rel(x_init, want) < 1e-7, k
+        assert _rel(ocp.U_prev[0], G["loop_u0"][k]) < 1e-6, k
+    # retract of the last solve (node 0): a = [base_acc_cv(q, v, a_j, f), (v_1 - v_0) / dt_0]
+    M = rbd.ModelArrays(R.model)
+    q0, v0, f0 = ocp.q_sol[-1], ocp.v_sol[-1], ocp.forces_sol[-1]
+    a_j = (ocp.U_prev[1][:R.nv] - ocp.U_prev[0][:R.nv])[6:] / ocp.dts[0]
+    a_b = rbd.base_acc_cv(M, list(R.foot_frames), q0, v0, a_j, f0, R.mass)
+    assert _rel(ocp.a_sol[-1], np.concatenate([a_b, a_j])) < 1e-10
+
+
+def test_make_ocp_aba_retract_fills_acceleration():
+    """whole_body_aba retract (ocp_whole_body_aba.py:177-214): a_sol = ABA at each node."""
+    from oracle import rbd
+    from pinoloco.ocp import OCP_ARGS, make_ocp
+    from pinoloco.synthetic import DT_MAX, DT_MIN, SWING_HEIGHT, SWING_VEL_LIMITS, random_state
+    R = make_robot("b2")
+    xs, t0, vx = random_state(R, 3)
+    ocp = make_ocp("whole_body_aba", OCP_ARGS["whole_body_aba"], robot=R, nodes=12, solver="osqp")
+    ocp.set_time_params(DT_MIN, DT_MAX)
+    ocp.set_swing_params(SWING_HEIGHT, list(SWING_VEL_LIMITS))
+    ocp.set_tracking_targets([vx, 0, 0, 0, 0, 0], [0, 0, 0], [0, 0, 0])
+    ocp.update_initial_state(xs)
+    ocp.update_gait_sequence(t0)
+    ocp.init_solver()
+    ocp.solve(retract_all=True)
+    M = rbd.ModelArrays(R.model)
+    frames = list(R.foot_frames) + ([R.ext_force_frame] if R.ext_force_frame is not None else [])
+    assert len(ocp.a_sol) == 12 and len(ocp.q_sol) == 13
+    for i in range(12):
+        want = rbd.aba_dynamics(M, frames, ocp.q_sol[i], ocp.v_sol[i], ocp.tau_sol[i], ocp.forces_sol[i])
+        assert _rel(ocp.a_sol[i], want) < 1e-10, i
+
+
 def test_batch_invariance_and_repeatability():
     """Problem b of a batch gives bit-identical results alone, and a second run of
     the same inputs is bit-identical (one workgroup per problem, fixed reduction order)."""
@@ -155,17 +258,18 @@ def test_batch_invariance_and_repeatability():
     bo.close()
 
 
-def test_full_size_properties():
-    """Config 5 at batch 256 (size-independent properties of every problem):
-    finite results, OSQP status in {solved, inaccurate, max iter}, the step obeys
-    dist(J dx, [l - g, u - g]) <= pri_res (OSQP's z lies in [l, u]), and the new
+@pytest.mark.parametrize("rname,dyn,N,B", [("b2", "whole_body_aba", 40, 256), ("b2g", "whole_body_acc", 50, 1024),
+                                           ("b2g", "whole_body_rnea", 50, 1024), ("go2", "centroidal_vel", 20, 256)])
+def test_full_size_properties(rname, dyn, N, B):
+    """BASELINE configs 3-5 at their batch sizes (size-independent properties of every
+    problem): finite results, OSQP status in {solved, inaccurate, max iter}, the step
+    obeys dist(J dx, [l - g, u - g]) <= pri_res (OSQP's z lies in [l, u]), and the new
     iterate is x + alpha dx."""
     from pinoloco.ocp import BatchedOCP
     from pinoloco.synthetic import build_batch
-    R = make_robot("b2g")
-    B = 256
-    lay, P, X, XS, T0 = build_batch(R, "whole_body_rnea", 50, B, 1000)
-    bo = BatchedOCP(R, "whole_body_rnea", 50, batch=B, device=0)
+    R = make_robot(rname)
+    lay, P, X, XS, T0 = build_batch(R, dyn, N, B, 1000)
+    bo = BatchedOCP(R, dyn, N, batch=B, device=0)
     bo.set_params(P)
     bo.set_x(X)
     bo.init_solver()
@@ -176,7 +280,7 @@ def test_full_size_properties():
     rows, cols = bo.pattern()
     assert np.all(np.isfinite(xn)) and np.all(np.isfinite(dx))
     assert set(np.unique(st["status"])) <= {1, 2, -2}
-    for b in range(0, B, 17):
+    for b in range(0, B, max(17, B // 16)):
         A = sp.csr_matrix((J[b], (rows, cols)), shape=(bo.m, bo.n))
         Adx = A @ dx[b]
         lo, hi = lbg[b] - g[b], ubg[b] - g[b]

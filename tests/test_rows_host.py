@@ -48,6 +48,7 @@ def _consts(bo):
     ("b2", "whole_body_aba", 40, [0, 1, 2, 3, 20, 39]),
     ("b2g", "whole_body_acc", 50, [0, 1, 25, 49]),
     ("b2g", "whole_body_rnea", 50, [0, 2, 3, 26, 49]),
+    ("go2", "centroidal_vel", 20, None),
 ])
 def test_node_rows_and_dual_jacobian(harness, rname, dyn, N, nodes_checked):
     from pinoloco.ocp import BatchedOCP
