@@ -86,57 +86,44 @@ def measured_traffic(batch, nodes, workload):
     return tj
 
 
-def _baseline_worker(args):
-    """One worker of the CPU baseline: problem `b`, `n_steps` MPC steps, one thread."""
-    robot, dynamics, N, b, n_steps = args
-    from threadpoolctl import threadpool_limits
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(robot, dynamics, N, per_core=4, n_steps=2):
+    """The compiled C++ restatement of the reference's CPU path (oracle/cpu/sqp_cpu.cpp:
+    rows + dual Jacobians, OSQP 0.6 with the QDLDL LDL^T on the quasi-definite KKT,
+    line search, MPC loop; -O3 -march=x86-64-v3, OpenMP over problems) on the host's
+    CPU share, same workload and seeds as the GPU run.  Sample: per_core problems per
+    thread x n_steps MPC steps, plus the single-thread latency of one problem.
+    Runs before the GPU is initialised."""
     sys.path.insert(0, HERE)
-    from oracle.ocp import OracleOCP  # noqa: E402  (checker / baseline only)
-    from pinoloco.synthetic import problem_values
-    R = robots.ROBOTS[robot]()
-    R.set_gait_sequence("trot", 0.8)
-    with threadpool_limits(1):
-        lay, P, X, XS, T0 = build_batch(R, dynamics, N, 1, b)
-        xs, x = XS[0].copy(), X[0].copy()
-        o = OracleOCP(R, dynamics, N)
-        elapsed, solves = 0.0, 0
-        for k in range(n_steps):
-            vals, _, _ = problem_values(R, dynamics, N, b, lay, k)
-            vals["x_init"] = xs
-            p = lay.pack(vals)
-            if k == 0:
-                o.init_solver(x, p)  # OSQP setup: excluded like pl_ocp_init_solver
-            t = time.perf_counter()
-            if k > 0:
-                x = o.warm_start(x, p)
-            x, _, _ = o.sqp_step(x, p)
-            DX, _ = o.split(x)
-            xs = o.integrate_state(xs, DX[1])
-            elapsed += time.perf_counter() - t
-            solves += 1
-    return elapsed, solves
-
-
-def cpu_baseline(robot, dynamics, N, n_steps=2):
-    """Oracle (numpy restatement of the reference path, oracle/) timed on the host's
-    CPU share: one single-threaded worker per core, one problem each, the same closed
-    loop as the device (gait at t0 + k dt_min, warm start, one SQP iteration,
-    x <- integrate(x, DX[1])).  Runs before the GPU is initialised (fork pool).
-    value = solves of all workers / the wall time of the pool's timed work."""
-    import multiprocessing as mp
+    from oracle.cpu_baseline import CpuOCP  # noqa: E402  (baseline leg only)
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         avail = os.cpu_count() or 1
-    cores = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)), 16))
-    ctx = mp.get_context("fork")
-    with ctx.Pool(cores) as pool:
-        res = pool.map(_baseline_worker, [(robot, dynamics, N, b, n_steps) for b in range(cores)])
-    solves = sum(r[1] for r in res)
-    wall = max(r[0] for r in res)  # timed regions run concurrently, one per core
-    return {"value": solves / wall, "unit": "solves/s", "cores": cores, "kind": "port",
-            "sample": f"{cores} problems x {n_steps} MPC steps of the same workload (one problem per core), numpy "
-                      f"oracle (oracle/), one thread per worker; wall = slowest worker's timed solves"}
+    env = os.environ.get("OMP_NUM_THREADS")
+    threads = max(1, min(avail, int(env))) if env else avail  # the box's CPU share is exported as OMP_NUM_THREADS
+    R = robots.ROBOTS[robot]()
+    R.set_gait_sequence("trot", 0.8)
+    B = per_core * threads
+    lay, P, X, XS, T0 = build_batch(R, dynamics, N, B, 0)
+    c = CpuOCP(R, dynamics, N, gait_type="trot", gait_period=0.8)
+    wall, _, _ = c.mpc(P, X, XS, T0, n_steps, threads=threads)
+    w1, _, _ = c.mpc(P[:1], X[:1], XS[:1], T0[:1], n_steps, threads=1)
+    return {"value": B * n_steps / wall, "unit": "solves/s", "cores": threads, "kind": "port",
+            "sample": f"{B} problems x {n_steps} MPC steps of the same workload (seeds 0..{B - 1}) on {threads} OpenMP "
+                      f"threads; compiled C++ restatement of the reference CPU path (oracle/cpu/sqp_cpu.cpp: OSQP 0.6 "
+                      f"+ QDLDL LDL^T, Armijo/filter line search), g++ -O3 -march=x86-64-v3",
+            "single_core_ms_per_solve": w1 / n_steps * 1e3, "cpu_model": _cpu_model(), "host_cpus_visible": avail}
 
 
 def _free_port():

@@ -1,0 +1,132 @@
+"""CPU BASELINE (test infrastructure): ctypes driver of oracle/cpu/sqp_cpu.cpp.
+
+A compiled C++ restatement of the reference's CPU solve path (OSQP 0.6 with the
+QDLDL LDL^T on the quasi-definite KKT, the Armijo / filter line search, the MPC
+loop of run_mpc.py:127-143), run with OpenMP over independent problems.  bench.py
+times it on the GPU box's host cores beside the GPU run (``cpu_baseline``);
+tests/test_cpu_baseline.py checks it against the numpy oracle's golden vectors.
+Only tests/, bench.py's cpu_baseline leg and __graft_entry__ use this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.normpath(os.path.join(HERE, ".."))
+SRC = os.path.join(HERE, "cpu", "sqp_cpu.cpp")
+LIB = os.path.join(HERE, "_build", "libsqp_cpu.so")
+CSRC = os.path.join(ROOT, "pino-locoman_amd", "csrc")
+# x86-64-v3 (AVX2 + FMA): built in the development container, run on the GPU box's host
+CXXFLAGS = ["-std=c++17", "-O3", "-march=x86-64-v3", "-fopenmp", "-fPIC", "-shared", "-Wno-unknown-pragmas",
+            "-Wno-maybe-uninitialized", "-Wno-uninitialized"]
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+_lib = None
+
+
+def _inputs():
+    hdrs = ("ad.h", "model.h", "rbd.h", "rows.h", "targets.h")
+    return [SRC, os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in hdrs]
+
+
+def build(force=False):
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(p) for p in _inputs()):
+        return LIB
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    cmd = ["g++"] + CXXFLAGS + ["-I", CSRC, SRC, "-o", LIB + ".tmp"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"CPU baseline build failed:\n{r.stderr[-4000:]}")
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        L.cpu_create.restype = C.c_void_p
+        L.cpu_create.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _ip, _ip, _ip, _ip,
+                                 _ip, _ip, _dp, C.c_int, C.c_double]
+        L.cpu_destroy.argtypes = [C.c_void_p]
+        L.cpu_factor_nnz.restype = C.c_longlong
+        L.cpu_factor_nnz.argtypes = [C.c_void_p]
+        L.cpu_mpc_batch.restype = C.c_double
+        L.cpu_mpc_batch.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp, C.c_int, C.c_int, _dp, _ip]
+        L.cpu_sqp_step.argtypes = [C.c_void_p, _dp, _dp, _dp, _ip, _dp]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(_dp)
+
+
+def _i(a):
+    return a.ctypes.data_as(_ip)
+
+
+class CpuOCP:
+    """One (robot, dynamics, N) OCP on the CPU baseline; structure from the product's
+    host-only handle (layout and Jacobian pattern, pl_ocp_pattern / pl_debug_consts)."""
+
+    def __init__(self, robot, dynamics, nodes, osqp_settings=None, gait_type="trot", gait_period=0.8):
+        from pinoloco import _lib as plib
+        from pinoloco.ocp import GAIT_CODES, OSQP_SETTINGS, BatchedOCP
+        s = dict(OSQP_SETTINGS)
+        s.update(osqp_settings or {})
+        bo = BatchedOCP(robot, dynamics, nodes, batch=1, device=-1, osqp_settings=s, gait_type=gait_type,
+                        gait_period=gait_period)
+        sizes = (C.c_int * 2)()
+        plib.check(plib.lib().pl_debug_consts(bo.h, None, None, sizes))
+        mb, ob = C.create_string_buffer(sizes[0]), C.create_string_buffer(sizes[1])
+        plib.check(plib.lib().pl_debug_consts(bo.h, mb, ob, None))
+        rows, cols = bo.pattern()
+        nt = bo.node_table()
+        self.n, self.m, self.np, self.N = bo.n, bo.m, bo.np, nodes
+        self.nx = bo.layout.nx
+        arrs = [np.ascontiguousarray(nt[:, k], dtype=np.int32) for k in (2, 3, 4, 0)]  # x_off, row_off, nrow, nw
+        st = np.array([s["rho"], s["sigma"], s["alpha"], s["eps_abs"], s["eps_rel"], s["eps_prim_inf"],
+                       s["eps_dual_inf"], s["max_iter"], s["check_termination"], s["scaling"]], dtype=np.float64)
+        self._keep = (mb, ob, arrs, rows, cols, st)
+        self.h = lib().cpu_create(mb, ob, nodes, bo.n, bo.m, bo.nnz, *[_i(a) for a in arrs], _i(rows), _i(cols),
+                                  _d(st), GAIT_CODES[gait_type], float(gait_period))
+        bo.close()
+
+    def factor_nnz(self):
+        return int(lib().cpu_factor_nnz(self.h))
+
+    def sqp_step(self, x, p):
+        """One SQP iteration from a cold OSQP (like OracleOCP.init_solver + sqp_step)."""
+        x = np.ascontiguousarray(np.array(x, dtype=np.float64))
+        p = np.ascontiguousarray(np.asarray(p, dtype=np.float64))
+        dx = np.zeros(self.n)
+        stats = np.zeros(4, dtype=np.int32)
+        alpha = C.c_double()
+        lib().cpu_sqp_step(self.h, _d(p), _d(x), _d(dx), _i(stats), C.byref(alpha))
+        return x, dx, dict(status=int(stats[0]), iter=int(stats[1]), branch=int(stats[2]), trials=int(stats[3]),
+                           alpha=alpha.value)
+
+    def mpc(self, P, X, XS, T0, steps, threads=0):
+        """`steps` MPC steps of every problem; returns (wall seconds, final states, stats)."""
+        B = P.shape[0]
+        P, X, XS = (np.ascontiguousarray(a, dtype=np.float64) for a in (P, X, XS))
+        T0 = np.ascontiguousarray(T0, dtype=np.float64)
+        xs = np.zeros((B, self.nx))
+        stats = np.zeros((B, steps, 4), dtype=np.int32)
+        wall = lib().cpu_mpc_batch(self.h, B, _d(P), _d(X), _d(XS), _d(T0), steps, threads, _d(xs), _i(stats))
+        return wall, xs, stats
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and _lib is not None:
+                _lib.cpu_destroy(self.h)
+        except Exception:  # noqa: BLE001
+            pass

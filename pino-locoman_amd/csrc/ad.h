@@ -8,10 +8,13 @@
 // Taylor switches, quaternion branch) follow the primal exactly as CasADi's
 // if_else does.
 #pragma once
-#include <hip/hip_runtime.h>
 #include <math.h>
-
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
 #define PL_HD __host__ __device__ __forceinline__
+#else  // plain C++ build of the same math (the CPU baseline in oracle/cpu, g++ -O3)
+#define PL_HD inline __attribute__((always_inline))
+#endif
 
 struct Dual {
   double v, d;

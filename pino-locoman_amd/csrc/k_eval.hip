@@ -333,35 +333,6 @@ void launch_line_search(PlOcpHandle* h) {
 
 // ---------------------------------------------------------------------------
 // Device-side MPC loop glue (run_mpc.py:127-143).
-// Gait schedule (utils/gait_sequence.py:26-77) for one problem.
-__device__ void gait_schedule(const PlOcpConst& O, int gait_type, double period, double swing_period, double t_cur,
-                              const double* p, double* contact, double* swing) {
-  const int N = O.N;
-  double t = t_cur;
-  for (int i = 0; i < N; ++i) {
-    if (i > 0) t += pl::node_dt(O, p, i - 1);
-    for (int f = 0; f < 4; ++f) {
-      contact[4 * i + f] = 1.0;
-      swing[4 * i + f] = 0.0;
-    }
-    if (gait_type == 2) continue;
-    double gp = fmod(t, period) / period;
-    double sp = fmod(t, swing_period) / swing_period;
-    int f0 = -1, f1 = -1;
-    if (gait_type == 0) {
-      if (gp < 0.5) { f0 = 0; f1 = 3; } else { f0 = 1; f1 = 2; }
-    } else {
-      f0 = gp < 0.25 ? 1 : gp < 0.5 ? 2 : gp < 0.75 ? 0 : 3;
-    }
-    contact[4 * i + f0] = 0.0;
-    swing[4 * i + f0] = sp;
-    if (f1 >= 0) {
-      contact[4 * i + f1] = 0.0;
-      swing[4 * i + f1] = sp;
-    }
-  }
-}
-
 // MPC step k, before the solve: parameters (x_init, gait schedule at
 // t0 + k dt_min) and warm start (forces <- f_des masked by the new schedule;
 // ocp_whole_body_rnea.py:207-235).  k == 0 keeps the initial guess.
@@ -374,7 +345,7 @@ __global__ __launch_bounds__(64) void k_mpc_prepare(PlDev d, int k, int N, int n
   for (int j = threadIdx.x; j < nx; j += blockDim.x) p[O.P.x_init + j] = d.xstate[(size_t)b * nx + j];
   if (threadIdx.x == 0) {
     double t = d.t0[b] + k * p[O.P.dt_min];
-    gait_schedule(O, gait_type, period, swing_period, t, p, p + O.P.contact, p + O.P.swing);
+    pl::gait_schedule(O, gait_type, period, swing_period, t, p, p + O.P.contact, p + O.P.swing);
   }
   __syncthreads();
   if (k == 0) return;

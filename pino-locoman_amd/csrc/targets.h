@@ -49,4 +49,33 @@ PL_HD double u_des(const PlModel& M, const PlOcpConst& O, const double* p, int k
   return 0.0;
 }
 
+// Gait schedule (utils/gait_sequence.py:26-77) for one problem.
+PL_HD void gait_schedule(const PlOcpConst& O, int gait_type, double period, double swing_period, double t_cur,
+                              const double* p, double* contact, double* swing) {
+  const int N = O.N;
+  double t = t_cur;
+  for (int i = 0; i < N; ++i) {
+    if (i > 0) t += pl::node_dt(O, p, i - 1);
+    for (int f = 0; f < 4; ++f) {
+      contact[4 * i + f] = 1.0;
+      swing[4 * i + f] = 0.0;
+    }
+    if (gait_type == 2) continue;
+    double gp = fmod(t, period) / period;
+    double sp = fmod(t, swing_period) / swing_period;
+    int f0 = -1, f1 = -1;
+    if (gait_type == 0) {
+      if (gp < 0.5) { f0 = 0; f1 = 3; } else { f0 = 1; f1 = 2; }
+    } else {
+      f0 = gp < 0.25 ? 1 : gp < 0.5 ? 2 : gp < 0.75 ? 0 : 3;
+    }
+    contact[4 * i + f0] = 0.0;
+    swing[4 * i + f0] = sp;
+    if (f1 >= 0) {
+      contact[4 * i + f1] = 0.0;
+      swing[4 * i + f1] = sp;
+    }
+  }
+}
+
 }  // namespace pl

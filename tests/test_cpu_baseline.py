@@ -1,0 +1,57 @@
+"""The compiled CPU baseline (oracle/cpu/sqp_cpu.cpp: OSQP 0.6 with the QDLDL
+LDL^T, line search, MPC loop) against the oracle's golden vectors: the SQP outcome
+(status, ADMM iterations, line-search branch, trials, alpha) exact and the QP step
+<= 1e-9 relative (both solve the quasi-definite KKT directly; measured ~1e-11),
+and the closed MPC loop <= 1e-8.  It is the timed `cpu_baseline` of bench.py, so
+it must solve the same problems as the reference path restated by the oracle."""
+import numpy as np
+import pytest
+
+from conftest import golden, make_robot
+
+
+def _cpu(name, rname, dyn, N):
+    from oracle.cpu_baseline import CpuOCP
+    G = golden(f"sqp_{name}.npz")
+    eps = G["osqp_eps"]
+    s = {"eps_abs": float(eps[0]), "eps_rel": float(eps[1]), "max_iter": int(G["osqp_max_iter"])}
+    R = make_robot(rname, str(G["gait"]))
+    return G, CpuOCP(R, dyn, N, osqp_settings=s, gait_type=str(G["gait"]))
+
+
+@pytest.mark.parametrize("name,rname,dyn,N,probs", [
+    ("go2_rnea_n20", "go2", "whole_body_rnea", 20, [0, 1, 4]),
+    ("go2_cv_n20", "go2", "centroidal_vel", 20, [0, 2]),
+    ("b2_aba_n40", "b2", "whole_body_aba", 40, [0]),
+    ("b2g_acc_n50", "b2g", "whole_body_acc", 50, [0]),
+    ("b2g_rnea_n50", "b2g", "whole_body_rnea", 50, [0]),
+    ("go2_rnea_n20_eps2", "go2", "whole_body_rnea", 20, [1, 3, 4]),
+    ("go2_rnea_n20_eps5", "go2", "whole_body_rnea", 20, [0]),
+    ("go2_rnea_n20_eps6", "go2", "whole_body_rnea", 20, [0]),
+    ("go2_rnea_n20_infeas", "go2", "whole_body_rnea", 20, [0, 1]),
+])
+def test_cpu_sqp_step_matches_golden(name, rname, dyn, N, probs):
+    G, c = _cpu(name, rname, dyn, N)
+    for b in probs:
+        xn, dx, st = c.sqp_step(G["X"][b], G["P"][b])
+        assert (st["status"], st["iter"], st["branch"], st["trials"]) == \
+            (G["status"][b], G["iters"][b], G["branch"][b], G["trials"][b]), b
+        assert st["alpha"] == G["alpha"][b]
+        if np.all(np.isnan(G["dx"][b])):
+            assert np.all(np.isnan(dx)) and np.array_equal(xn, G["X"][b])
+        else:
+            assert np.abs(dx - G["dx"][b]).max() <= 1e-9 * np.abs(G["dx"][b]).max()
+        assert np.abs(xn - G["x_new"][b]).max() <= 1e-9 * np.abs(G["x_new"][b]).max()
+
+
+@pytest.mark.parametrize("name,rname,dyn,N", [("go2_rnea_n20", "go2", "whole_body_rnea", 20),
+                                              ("go2_cv_n20", "go2", "centroidal_vel", 20),
+                                              ("go2_rnea_n20_walk", "go2", "whole_body_rnea", 20)])
+def test_cpu_mpc_loop_matches_golden(name, rname, dyn, N):
+    G, c = _cpu(name, rname, dyn, N)
+    K = len(G["loop_states"])
+    wall, xs, stats = c.mpc(G["P"][:1], G["X"][:1], G["XS"][:1], G["T0"][:1], K, threads=1)
+    want = G["loop_states"][-1]
+    assert np.abs(xs[0] - want).max() <= 1e-8 * np.abs(want).max()
+    assert np.array_equal(stats[0], G["loop_stats"])
+    assert wall > 0
