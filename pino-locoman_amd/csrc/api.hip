@@ -977,6 +977,10 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   h.set.check_termination = d->check_termination;
   h.set.warm_start = d->warm_start;
   h.sqp_iters = 1;
+  // ADMM sweep kernel: one wave per problem (k_admm); PL_ADMM_WAVES=2 selects the
+  // two-waves-per-problem variant (k_admm2.hip; measured slower)
+  h.admm_waves = (getenv("PL_ADMM_WAVES") && atoi(getenv("PL_ADMM_WAVES")) == 2) ? 2 : 1;
+  if (h.admm_waves == 2 && !admm2_supported(&h)) h.admm_waves = 1;
   h.gait_type = d->gait_type;
   h.gait_period = d->gait_period;
   h.swing_period = d->gait_type == 0 ? 0.5 * d->gait_period : (d->gait_type == 1 ? 0.25 * d->gait_period : d->gait_period);

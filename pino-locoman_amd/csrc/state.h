@@ -202,6 +202,7 @@ struct PlOcpHandle {
   int admm_asr;                     // A values per lane staged through registers (x 64 lanes)
   int admm_fwd_asb;                 // coupling rows too dense for registers: forward steps stage A in LDS
   int sqp_iters;                    // SQP iterations per solve (reference: 1, ocp.py:382-383)
+  int admm_waves;                   // ADMM sweep kernel: 2 = k_admm2 (two waves per problem), 1 = k_admm
   long long fs_stride;              // factor scratch per problem (doubles)
   int nfgroup;                      // k_fnode launches: consecutive nodes with one program
   int fg_i0[PL_FAC_MAXGROUPS], fg_n[PL_FAC_MAXGROUPS], fg_lds[PL_FAC_MAXGROUPS], fg_um[PL_FAC_MAXGROUPS];
@@ -235,6 +236,8 @@ void launch_factor(PlOcpHandle* h);
 bool factor_supports_ndx(int ndx);
 void launch_admm_init(PlOcpHandle* h);
 void launch_admm(PlOcpHandle* h, int niter, int check, int it_base);
+bool admm2_supported(const PlOcpHandle* h);
+void launch_admm2(PlOcpHandle* h, int niter, int check);
 void launch_check(PlOcpHandle* h, int it, int final_check);
 void launch_unscale(PlOcpHandle* h);
 void launch_line_search(PlOcpHandle* h);
