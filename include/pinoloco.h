@@ -140,6 +140,37 @@ int pl_ocp_solve(pl_ocp* o, pl_stats* stats, double* phase_ms);
  * `for _ in range(1)`, optimization/ocp.py:382-383). */
 int pl_ocp_set_sqp_iters(pl_ocp* o, int sqp_iters);
 
+/* Interior-point solve: the reference's Fatrop branch (ocp.py:248-263 settings,
+ * :360-373 solve; run_mpc.py:34-37 selects it), restated as an IPOPT-style
+ * primal-dual barrier method with a filter line search (oracle/ip_ref.py documents
+ * the algorithm).  pl_ocp_set_solver(o, PL_SOLVER_IP) switches pl_ocp_solve and
+ * pl_mpc_step to it; pl_stats then holds status (1 converged, -1 max_iter, -2 line
+ * search failed, -3 non-finite), admm_iters = IP iterations, ls_trials (total),
+ * ls_alpha (last step), viol_max, pri_res = scaled NLP error, dua_res = mu, f. */
+#define PL_SOLVER_OSQP 0
+#define PL_SOLVER_IP 1
+typedef struct {
+  double tol;          /* 1e-3  (ocp.py:257) */
+  double mu_init;      /* 1e-4  (ocp.py:258) */
+  double bound_push;   /* 1e-7  (ocp.py:261) */
+  double bound_frac;   /* 1e-2 */
+  double delta_w;      /* 1e-8  primal regularisation of the Newton system */
+  double delta_c;      /* 1e-4  dual regularisation (equality rows weighted 1 / delta_c) */
+  int max_iter;        /* 10    (ocp.py:256), at most 32 */
+  int ls_max;          /* 12    line-search trials */
+  int n_refine;        /* 2     iterative-refinement solves of each Newton system */
+  int pad;
+} pl_ip_settings;
+typedef struct {
+  int status, iter, ls_trials, nfilter;
+  double err, mu, alpha, alpha_z, f, viol_max;
+  double alphas[32];   /* accepted step of each iteration (0: failed line search) */
+} pl_ip_stats;
+int pl_ocp_set_solver(pl_ocp* o, int solver);
+int pl_ocp_set_ip_settings(pl_ocp* o, const pl_ip_settings* s);
+int pl_ocp_ip_stats(pl_ocp* o, pl_ip_stats* stats);   /* [batch] */
+int pl_ocp_get_lam(pl_ocp* o, double* lam);           /* [batch][m]: lam_g (ocp.py:373) */
+
 /* CasADi external-function ABI (include/pinoloco_casadi.h): bind the OCP whose
  * shapes / sparsity the exported sqp_data, f_data, g_data, hess_data and
  * retract_solution describe (replaces the generated code of ocp.py:299-302 and

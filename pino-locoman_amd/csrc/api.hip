@@ -977,6 +977,10 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   h.set.check_termination = d->check_termination;
   h.set.warm_start = d->warm_start;
   h.sqp_iters = 1;
+  h.solver = PL_SOLVER_OSQP;
+  // Fatrop settings of the reference (ocp.py:254-262) + the restatement's constants
+  // (oracle/ip_ref.py IP_SETTINGS)
+  h.ip = PlIpSettings{1e-3, 1e-4, 1e-7, 1e-2, 1e-8, 1e-4, 10, 12, 2, 0};
   // ADMM sweep kernel: one wave per problem (k_admm); PL_ADMM_WAVES=2 selects the
   // two-waves-per-problem variant (k_admm2.hip; measured slower)
   h.admm_waves = (getenv("PL_ADMM_WAVES") && atoi(getenv("PL_ADMM_WAVES")) == 2) ? 2 : 1;
@@ -1245,8 +1249,88 @@ extern "C" int pl_ocp_set_sqp_iters(pl_ocp* o, int sqp_iters) {
   return 0;
 }
 
+// Solver selection (ocp.py:248 / :265 dispatch on the solver string).  The interior
+// point's per-problem state (slacks and multipliers, 7 x m doubles per problem) is
+// allocated on first selection.
+extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
+  REQUIRE_DEVICE(o);
+  if (solver != PL_SOLVER_OSQP && solver != PL_SOLVER_IP) {
+    pl_set_error("Solver %d not supported (PL_SOLVER_OSQP = 0, PL_SOLVER_IP = 1)", solver);
+    return -1;
+  }
+  PlOcpHandle* h = &o->h;
+  if (solver == PL_SOLVER_IP && !h->d.ipinfo) {
+    const size_t Bm = (size_t)h->B * h->m;
+    if (dalloc(o, &h->d.ip_s, Bm) || dalloc(o, &h->d.ip_lam, Bm) || dalloc(o, &h->d.ip_zl, Bm) ||
+        dalloc(o, &h->d.ip_zu, Bm) || dalloc(o, &h->d.ip_rh, Bm) || dalloc(o, &h->d.ip_dl, Bm) ||
+        dalloc(o, &h->d.ip_ds, Bm) || dalloc(o, &h->d.ip_jdx, Bm) || dalloc(o, &h->d.ip_dx, (size_t)h->B * h->n) ||
+        dalloc(o, &h->d.ipinfo, (size_t)h->B))
+      return -2;
+  }
+  h->solver = solver;
+  return 0;
+}
+
+extern "C" int pl_ocp_set_ip_settings(pl_ocp* o, const pl_ip_settings* s) {
+  if (!o || !s) { pl_set_error("null argument"); return -1; }
+  if (s->max_iter < 0 || s->max_iter > PL_IP_MAXFILT) {
+    pl_set_error("ip max_iter %d outside [0, %d]", s->max_iter, PL_IP_MAXFILT);
+    return -1;
+  }
+  if (s->ls_max < 1 || s->ls_max > 60 || !(s->tol > 0) || !(s->mu_init > 0) || !(s->bound_push > 0) ||
+      !(s->bound_frac > 0) || !(s->delta_w >= 0) || !(s->delta_c > 0) || s->n_refine < 0 || s->n_refine > 8) {
+    pl_set_error("invalid interior-point settings");
+    return -1;
+  }
+  o->h.ip = PlIpSettings{s->tol, s->mu_init, s->bound_push, s->bound_frac, s->delta_w, s->delta_c, s->max_iter,
+                         s->ls_max, s->n_refine, 0};
+  return 0;
+}
+
+extern "C" int pl_ocp_get_lam(pl_ocp* o, double* lam) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  if (!h->d.ip_lam) { pl_set_error("no interior-point state (pl_ocp_set_solver(o, PL_SOLVER_IP) first)"); return -1; }
+  PL_CHECK_HIP(hipMemcpyAsync(lam, h->d.ip_lam, (size_t)h->B * h->m * 8, hipMemcpyDeviceToHost, h->stream));
+  PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int pl_ocp_ip_stats(pl_ocp* o, pl_ip_stats* out) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  if (!h->d.ipinfo) { pl_set_error("no interior-point state (pl_ocp_set_solver(o, PL_SOLVER_IP) first)"); return -1; }
+  std::vector<PlIpInfo> info(h->B);
+  PL_CHECK_HIP(hipMemcpyAsync(info.data(), h->d.ipinfo, h->B * sizeof(PlIpInfo), hipMemcpyDeviceToHost, h->stream));
+  PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+  for (int b = 0; b < h->B; ++b) {
+    pl_ip_stats& s = out[b];
+    memset(&s, 0, sizeof(s));
+    s.status = info[b].status;
+    s.iter = info[b].iter;
+    s.ls_trials = info[b].trials;
+    s.nfilter = info[b].nfilt;
+    s.err = info[b].err;
+    s.mu = info[b].mu;
+    s.alpha = info[b].alpha;
+    s.alpha_z = info[b].alpha_z;
+    s.f = info[b].f;
+    s.viol_max = info[b].viol_max;
+    for (int q = 0; q < PL_IP_MAXFILT; ++q) s.alphas[q] = info[b].alphas[q];
+  }
+  return 0;
+}
+
 extern "C" int pl_ocp_solve(pl_ocp* o, pl_stats* stats, double* phase_ms) {
   REQUIRE_DEVICE(o);
+  if (o->h.solver == PL_SOLVER_IP) {
+    enqueue_ip(&o->h);
+    PL_CHECK_HIP(hipGetLastError());
+    PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
+    if (phase_ms)
+      for (int k = 0; k < 4; ++k) phase_ms[k] = 0.0;
+    return fetch_stats(o, stats);
+  }
   for (int k = 0; k < o->h.sqp_iters; ++k) enqueue_solve(o, phase_ms != nullptr);
   PL_CHECK_HIP(hipGetLastError());
   PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
@@ -1301,7 +1385,9 @@ extern "C" int pl_mpc_step(pl_ocp* o, int k) {
   REQUIRE_DEVICE(o);
   if (o->h.profile && o->h.prof_n > 48) prof_collect(&o->h);
   launch_mpc_prepare(&o->h, k);
-  for (int it = 0; it < o->h.sqp_iters; ++it) enqueue_solve(o, false);
+  if (o->h.solver == PL_SOLVER_IP) enqueue_ip(&o->h);
+  else
+    for (int it = 0; it < o->h.sqp_iters; ++it) enqueue_solve(o, false);
   launch_mpc_finish(&o->h);
   PL_CHECK_HIP(hipGetLastError());
   return 0;
@@ -1422,7 +1508,12 @@ extern "C" int pl_debug_get(pl_ocp* o, const char* name, double* out, long long 
       {"admm_t", h->d.dbg, h->d.dbg ? B * 32 : 0}, {"Ps", h->d.Ps, B * h->n},   {"P", h->d.P, B * h->n},         {"xa", h->d.xa, B * h->n},
       {"za", h->d.za, B * h->m},   {"ya", h->d.ya, B * h->m},       {"S", h->d.S, B * (size_t)h->S_stride},
       {"rhs", h->d.rhs, B * h->n}, {"step", h->d.step, B * h->n},   {"grad", h->d.grad, B * h->n},
-      {"g", h->d.g, B * h->m},     {"xstate", h->d.xstate, B * h->nx}};
+      {"g", h->d.g, B * h->m},     {"xstate", h->d.xstate, B * h->nx},
+      {"ip_s", h->d.ip_s, h->d.ip_s ? B * h->m : 0},     {"ip_lam", h->d.ip_lam, h->d.ip_lam ? B * h->m : 0},
+      {"ip_zl", h->d.ip_zl, h->d.ip_zl ? B * h->m : 0},  {"ip_zu", h->d.ip_zu, h->d.ip_zu ? B * h->m : 0},
+      {"ip_rh", h->d.ip_rh, h->d.ip_rh ? B * h->m : 0},  {"ip_dl", h->d.ip_dl, h->d.ip_dl ? B * h->m : 0},
+      {"ip_ds", h->d.ip_ds, h->d.ip_ds ? B * h->m : 0},  {"ip_dx", h->d.ip_dx, h->d.ip_dx ? B * h->n : 0},
+      {"ip_jdx", h->d.ip_jdx, h->d.ip_jdx ? B * h->m : 0}};
   for (auto& it : items) {
     if (strcmp(it.n, name) == 0) {
       if ((size_t)count < it.len) { pl_set_error("buffer too small for %s (%zu)", name, it.len); return -1; }

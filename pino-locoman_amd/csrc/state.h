@@ -122,6 +122,21 @@ struct PlProbInfo {
   long long iter_prof;      // ADMM iterations executed since pl_ocp_profile(o, 1) (roofline accounting)
 };
 
+// Interior-point solve (k_ip.hip, the Fatrop branch of the reference, ocp.py:248-263,
+// 360-373): settings and per-problem state.  The filter holds at most one entry per
+// iteration, so max_iter <= PL_IP_MAXFILT.
+#define PL_IP_MAXFILT 32
+struct PlIpSettings {
+  double tol, mu_init, bound_push, bound_frac, delta_w, delta_c;
+  int max_iter, ls_max, n_refine, pad;
+};
+struct PlIpInfo {
+  double mu, theta_max, theta_min, err, f, alpha, alpha_z, viol_max;
+  int iter, status, nfilt, trials, active, pad;
+  double filt[2 * PL_IP_MAXFILT];  // (theta, phi) pairs
+  double alphas[PL_IP_MAXFILT];    // accepted step of each iteration
+};
+
 struct PlDev {
   // shared structure
   PlModel* model;
@@ -185,6 +200,17 @@ struct PlDev {
   double* t0;        // per-problem gait time offset
   double* xstate;    // per-problem current state x_init (nx)
   double* dbg;       // optional kernel timing [B][16] (PL_ADMM_TIMING=1 at handle creation)
+  // interior point [B][m] (allocated by pl_ocp_set_solver(o, PL_SOLVER_IP))
+  double* ip_s;      // slacks of the inequality rows
+  double* ip_lam;    // constraint multipliers (lam_g)
+  double* ip_zl;     // lower / upper bound multipliers of the slacks
+  double* ip_zu;
+  double* ip_rh;     // r^ of the reduced Newton system
+  double* ip_dl;     // Newton direction: multipliers, slacks
+  double* ip_ds;
+  double* ip_dx;     // Newton step dx [B][n] and J dx [B][m], accumulated over the refinement solves
+  double* ip_jdx;
+  PlIpInfo* ipinfo;  // [B]
 };
 
 struct PlOcpHandle {
@@ -203,6 +229,8 @@ struct PlOcpHandle {
   int admm_fwd_asb;                 // coupling rows too dense for registers: forward steps stage A in LDS
   int sqp_iters;                    // SQP iterations per solve (reference: 1, ocp.py:382-383)
   int admm_waves;                   // ADMM sweep kernel: 2 = k_admm2 (two waves per problem), 1 = k_admm
+  int solver;                       // PL_SOLVER_OSQP (SQP + OSQP ADMM) or PL_SOLVER_IP (interior point)
+  PlIpSettings ip;
   long long fs_stride;              // factor scratch per problem (doubles)
   int nfgroup;                      // k_fnode launches: consecutive nodes with one program
   int fg_i0[PL_FAC_MAXGROUPS], fg_n[PL_FAC_MAXGROUPS], fg_lds[PL_FAC_MAXGROUPS], fg_um[PL_FAC_MAXGROUPS];
@@ -246,6 +274,7 @@ void launch_mpc_finish(PlOcpHandle* h);
 void launch_reset_info(PlOcpHandle* h);
 void launch_reset_iterates(PlOcpHandle* h);
 void launch_reset_prof(PlOcpHandle* h);
+void enqueue_ip(PlOcpHandle* h);
 
 #define PL_CHECK_HIP(expr)                                                        \
   do {                                                                            \

@@ -42,6 +42,18 @@ class Stats(C.Structure):
                 ("pri_res", C.c_double), ("dua_res", C.c_double), ("f", C.c_double)]
 
 
+class IpSettings(C.Structure):
+    _fields_ = [("tol", C.c_double), ("mu_init", C.c_double), ("bound_push", C.c_double), ("bound_frac", C.c_double),
+                ("delta_w", C.c_double), ("delta_c", C.c_double), ("max_iter", C.c_int), ("ls_max", C.c_int),
+                ("n_refine", C.c_int), ("pad", C.c_int)]
+
+
+class IpStats(C.Structure):
+    _fields_ = [("status", C.c_int), ("iter", C.c_int), ("ls_trials", C.c_int), ("nfilter", C.c_int),
+                ("err", C.c_double), ("mu", C.c_double), ("alpha", C.c_double), ("alpha_z", C.c_double),
+                ("f", C.c_double), ("viol_max", C.c_double), ("alphas", C.c_double * 32)]
+
+
 EXPORTS = {
     "pl_last_error": (C.c_char_p, []),
     "pl_version": (C.c_int, []),
@@ -58,6 +70,10 @@ EXPORTS = {
     "pl_ocp_init_solver": (C.c_int, [C.c_void_p]),
     "pl_ocp_solve": (C.c_int, [C.c_void_p, C.POINTER(Stats), _dp]),
     "pl_ocp_set_sqp_iters": (C.c_int, [C.c_void_p, C.c_int]),
+    "pl_ocp_set_solver": (C.c_int, [C.c_void_p, C.c_int]),
+    "pl_ocp_set_ip_settings": (C.c_int, [C.c_void_p, C.POINTER(IpSettings)]),
+    "pl_ocp_ip_stats": (C.c_int, [C.c_void_p, C.POINTER(IpStats)]),
+    "pl_ocp_get_lam": (C.c_int, [C.c_void_p, _dp]),
     "pl_casadi_bind": (C.c_int, [C.c_void_p, C.c_int]),
     "pl_casadi_unbind": (None, []),
     "pl_eval_sqp_data": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),

@@ -21,11 +21,17 @@ from .gait import horizon_dts
 
 DYN_CODES = {"whole_body_rnea": 0, "whole_body_acc": 1, "whole_body_aba": 2, "centroidal_vel": 3}
 GAIT_CODES = {"trot": 0, "walk": 1, "stand": 2}
+SOLVER_CODES = {"osqp": 0, "fatrop": 1}
 
 # ocp.py:267-273 plus the OSQP 0.6 library defaults it leaves untouched.
 OSQP_SETTINGS = dict(max_iter=100, alpha=1.4, rho=2e-2, warm_start=True, adaptive_rho=False,
                      sigma=1e-6, eps_abs=1e-3, eps_rel=1e-3, eps_prim_inf=1e-4, eps_dual_inf=1e-4,
                      scaling=10, check_termination=25)
+
+# ocp.py:254-262 (the reference's Fatrop options) plus the restatement's constants
+# (oracle/ip_ref.py IP_SETTINGS: bound_frac, regularisation, line-search trials)
+FATROP_SETTINGS = dict(max_iter=10, tol=1e-3, mu_init=1e-4, bound_push=1e-7, bound_frac=1e-2, delta_w=1e-8,
+                       delta_c=1e-4, ls_max=12, n_refine=2, pad=0)
 
 # ocp_args.py:2-19
 OCP_ARGS = {
@@ -241,6 +247,31 @@ class BatchedOCP:
         """SQP iterations per solve / MPC step (reference: 1, ocp.py:382-383)."""
         _lib.check(_lib.lib().pl_ocp_set_sqp_iters(self.h, int(k)))
 
+    def set_solver(self, solver):
+        """"osqp" (SQP + OSQP, ocp.py:265-313 / 375-422) or "fatrop" (the interior-point
+        restatement of the Fatrop branch, ocp.py:248-263 / 360-373)."""
+        if solver not in SOLVER_CODES:
+            raise ValueError(f"Solver {solver} not supported (choose from {sorted(SOLVER_CODES)})")
+        _lib.check(_lib.lib().pl_ocp_set_solver(self.h, SOLVER_CODES[solver]))
+        self.solver = solver
+
+    def set_ip_settings(self, **kw):
+        """Interior-point settings (defaults: FATROP_SETTINGS, the reference's ocp.py:254-262)."""
+        s = dict(FATROP_SETTINGS)
+        s.update(kw)
+        st = _lib.IpSettings(**{k: s[k] for k, _ in _lib.IpSettings._fields_})
+        _lib.check(_lib.lib().pl_ocp_set_ip_settings(self.h, C.byref(st)))
+
+    def ip_stats(self):
+        stats = (_lib.IpStats * self.batch)()
+        _lib.check(_lib.lib().pl_ocp_ip_stats(self.h, stats))
+        return {k: np.array([np.array(getattr(s, k)) for s in stats]) for k, _ in _lib.IpStats._fields_}
+
+    def get_lam(self):
+        lam = np.zeros((self.batch, self.m))
+        _lib.check(_lib.lib().pl_ocp_get_lam(self.h, _lib.dptr(lam)))
+        return lam
+
     def solve(self, timed=False):
         stats = (_lib.Stats * self.batch)()
         phase = np.zeros(4)
@@ -334,9 +365,8 @@ class OCP:
     """Single-problem OCP with the reference's method surface (ocp.py:11-480)."""
 
     def __init__(self, robot, solver, nodes, dynamics, tau_nodes=3, include_acc=True, include_base=True, device=0):
-        if solver != "osqp":
-            raise ValueError(f"Solver {solver} not supported on the MI355X path (ocp.py:321-322); "
-                             "the Fatrop interior-point path is a later row of the build plan")
+        if solver not in SOLVER_CODES:
+            raise ValueError(f"Solver {solver} not supported (ocp.py:248, 265: 'fatrop' or 'osqp')")
         self.robot = robot
         self.model = robot.model
         self.gait_sequence = robot.gait_sequence
@@ -371,6 +401,9 @@ class OCP:
                                    include_acc=include_acc, include_base=include_base,
                                    gait_type=self.gait_sequence.gait_type if self.gait_sequence else "trot",
                                    gait_period=self.gait_sequence.gait_period if self.gait_sequence else 0.8)
+        if solver == "fatrop":
+            self._backend.set_solver("fatrop")
+            self._backend.set_ip_settings()
         self.p = {"tau_prev": np.zeros(self.nj), "W_diag": np.zeros(self.nj), "ext_force_des": np.zeros(3),
                   "arm_vel_des": np.zeros(3), "x_init": self.x_nom.copy()}
         if self.gait_sequence is not None:
@@ -469,7 +502,10 @@ class OCP:
 
     def solve(self, retract_all=True, sqp_iters=1):
         """ocp.py:375-422 (OSQP branch) on the GPU: `sqp_iters` SQP iterations (the
-        reference runs one, `for _ in range(1)`, ocp.py:382-383)."""
+        reference runs one, `for _ in range(1)`, ocp.py:382-383).  With solver
+        "fatrop", one interior-point solve (ocp.py:360-373) from the warm start; a
+        solve that does not converge returns its last iterate, as the reference's
+        ``opti.debug`` fallback does, and ``lam_g`` holds the multipliers."""
         self._backend.set_sqp_iters(sqp_iters)
         self._backend.set_params(self.param_vector())
         self._backend.set_x(self._x_initial)
@@ -477,6 +513,9 @@ class OCP:
         st = self._backend.solve()
         self.solve_time = time.time() - start
         self.stats = {k: v[0] for k, v in st.items()}
+        if self.solver == "fatrop":  # ocp.py:360-373: stats, retract, lam_g
+            self.stats.update({"ip_" + k: v[0] for k, v in self._backend.ip_stats().items()})
+            self.lam_g = self._backend.get_lam()[0]
         x = self._backend.get_x()[0]
         self.retract_stacked_sol(x, retract_all)
         return x

@@ -62,6 +62,17 @@ SQP_CONFIGS = [
      {"eps_abs": 1e-6, "eps_rel": 1e-6, "max_iter": 2000}, 0),
 ]
 
+# Interior-point (Fatrop branch) fixtures: name, robot, dynamics, N, problems, closed-loop
+# steps of problem 0, gait (oracle/ip_ref.py, reference settings ocp.py:254-262)
+IP_CONFIGS = [
+    ("ip_go2_rnea_n20", "go2", "whole_body_rnea", 20, [("syn", k) for k in range(4)], 3, "trot"),
+    ("ip_go2_rnea_n20_stand", "go2", "whole_body_rnea", 20, [("stand",), ("syn", 30)], 2, "stand"),
+    ("ip_go2_cv_n20", "go2", "centroidal_vel", 20, [("syn", 0), ("syn", 1)], 0, "trot"),
+    ("ip_b2_aba_n40", "b2", "whole_body_aba", 40, [("syn", 0)], 0, "trot"),
+    ("ip_b2g_acc_n50", "b2g", "whole_body_acc", 50, [("syn", 0)], 0, "trot"),
+    ("ip_b2g_rnea_n50", "b2g", "whole_body_rnea", 50, [("syn", 0)], 0, "trot"),
+]
+
 
 def _yaw_quat(deg):
     a = np.deg2rad(deg)
@@ -238,8 +249,64 @@ def sqp_fixture(name, rname, dyn, N, problems, loop_steps, gait, osqp, njac):
           flush=True)
 
 
+def ip_fixture(name, rname, dyn, N, problems, loop_steps, gait):
+    from oracle.ip_ref import IP_SETTINGS, IPRef
+    R = robots.ROBOTS[rname]()
+    R.set_gait_sequence(gait, 0.8)
+    lay = Layout(R, dyn, N)
+    B = len(problems)
+    P, X, XS, T0 = (np.zeros((B, lay.np)), np.zeros((B, lay.n)), np.zeros((B, lay.nx)), np.zeros(B))
+    for b, spec in enumerate(problems):
+        P[b], X[b], XS[b], T0[b] = make_problem(R, lay, dyn, N, spec)
+    mi = IP_SETTINGS["max_iter"]
+    rec = {"P": P, "X": X, "XS": XS, "T0": T0, "gait": np.array(gait), "kinds": np.array([s[0] for s in problems])}
+    per = {k: [] for k in ("x_out", "lam", "s", "zl", "zu", "status", "iter", "err", "mu", "f", "alphas", "trials",
+                           "viol_max")}
+    for b in range(B):
+        o = OracleOCP(R, dyn, N)
+        x, lam, st = IPRef(o).solve(X[b], P[b])
+        g, lbg, ubg = o.eval_g(x, P[b])
+        al = np.zeros(mi)
+        al[:len(st["alphas"])] = st["alphas"]
+        for k, v in (("x_out", x), ("lam", lam), ("s", st["s"]), ("zl", st["zl"]), ("zu", st["zu"]),
+                     ("status", st["status"]), ("iter", st["iter"]), ("err", st["err"]), ("mu", st["mu"]),
+                     ("f", st["f"]), ("alphas", al), ("trials", int(np.sum(st["trials"]))),
+                     ("viol_max", o.violation_max(g, lbg, ubg))):
+            per[k].append(v)
+    rec.update({k: np.array(v) for k, v in per.items()})
+    # closed loop of problem 0 (run_mpc.py:115-143 with the Fatrop solver): warm start,
+    # one interior-point solve, x <- integrate(x, DX[1])
+    if loop_steps > 1:
+        o = OracleOCP(R, dyn, N)
+        xs, x = XS[0].copy(), X[0].copy()
+        states, stl = [], []
+        for k in range(loop_steps):
+            p = P[0].copy()
+            contact, swing = R.gait_sequence.get_gait_schedule(T0[0] + k * DT_MIN, horizon_dts(DT_MIN, DT_MAX, N), N)
+            vals = {"x_init": xs, "contact_schedule": contact, "swing_schedule": swing}
+            for key in vals:
+                o_, s_ = lay.poff[key]
+                p[o_:o_ + s_] = lay.pack(vals)[o_:o_ + s_]
+            if k > 0:
+                x = o.warm_start(x, p)
+            x, _, st = IPRef(o).solve(x, p)
+            DX, _ = o.split(x)
+            xs = o.integrate_state(xs, DX[1])
+            states.append(xs)
+            stl.append([st["status"], st["iter"]])
+        rec["loop_states"] = np.array(states)
+        rec["loop_stats"] = np.array(stl)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **rec)
+    print(name, "status", per["status"], "iter", per["iter"], "err", np.round(per["err"], 4), flush=True)
+
+
 def main():
     only = sys.argv[1:]
+    for cfg in IP_CONFIGS:
+        if cfg[0] in only:
+            ip_fixture(*cfg)
+    if only and all(o.startswith("ip_") for o in only):
+        return
     if not only or "rbd" in only:
         for r in ("go2", "b2", "b2g"):
             rbd_fixture(r)
