@@ -176,6 +176,8 @@ def main():
     ap.add_argument("--dynamics", default="whole_body_rnea")
     ap.add_argument("--nodes", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--solver", default="osqp", choices=["osqp", "fatrop"],
+                    help="osqp: the headline SQP + OSQP path; fatrop: the interior-point restatement (no CPU baseline)")
     ap.add_argument("--dry-run", action="store_true", help="gloo plumbing only, no GPU")
     args = ap.parse_args()
 
@@ -187,7 +189,7 @@ def main():
     if args.dry_run:
         return dry_run(args, world, rank)
     base = None
-    if not args.no_cpu_baseline and world == 1:
+    if not args.no_cpu_baseline and world == 1 and args.solver == "osqp":
         base = cpu_baseline(args.robot, args.dynamics, args.nodes)  # before the GPU is initialised
     dist = pdist.init("nccl")
 
@@ -197,6 +199,9 @@ def main():
     first, _ = shard(B * world, world, rank)
     lay, P, X, XS, T0 = build_batch(R, args.dynamics, args.nodes, B, first)
     bo = BatchedOCP(R, args.dynamics, args.nodes, batch=B, device=local_rank, gait_type="trot", gait_period=0.8)
+    if args.solver == "fatrop":
+        bo.set_solver("fatrop")
+        bo.set_ip_settings()
     bo.set_params(P)
     bo.set_x(X)
     bo.init_solver()
@@ -263,7 +268,9 @@ def main():
             "data": "synthetic (randomised initial state / gait phase / base velocity target, seed 1234 + problem)",
             "config": {"workload": workload, "batch_per_gpu": B,
                        "global_batch": B * world, "nodes": args.nodes, "robot": args.robot,
-                       "dynamics": args.dynamics, "solver": "osqp-sqp (1 SQP iteration, max_iter 100)",
+                       "dynamics": args.dynamics,
+                       "solver": ("osqp-sqp (1 SQP iteration, max_iter 100)" if args.solver == "osqp" else
+                                  "fatrop-equivalent interior point (max_iter 10, tol 1e-3, mu_init 1e-4)"),
                        "parallelism": f"batch-sharded dp{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_admm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -276,6 +283,11 @@ def main():
         }
         if base is not None:
             out["cpu_baseline"] = base
+        if args.solver == "fatrop":
+            ist = bo.ip_stats()  # the last MPC step's solves
+            out["ip_stats"] = {"mean_iter": float(np.mean(ist["iter"])),
+                               "status_counts": {int(k): int(v) for k, v in
+                                                 zip(*np.unique(ist["status"], return_counts=True))}}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
