@@ -170,6 +170,12 @@ int pl_ocp_set_solver(pl_ocp* o, int solver);
 int pl_ocp_set_ip_settings(pl_ocp* o, const pl_ip_settings* s);
 int pl_ocp_ip_stats(pl_ocp* o, pl_ip_stats* stats);   /* [batch] */
 int pl_ocp_get_lam(pl_ocp* o, double* lam);           /* [batch][m]: lam_g (ocp.py:373) */
+/* Parity aid: the interior point's Newton direction from a given state (x set with
+ * pl_ocp_set_x; slacks, multipliers [batch][m], mu [batch]); read it back with
+ * pl_debug_get("ip_dx" / "ip_dl" / "ip_ds") and the step bounds with pl_ocp_ip_stats
+ * (alpha = primal, alpha_z = bound-multiplier fraction-to-boundary step). */
+int pl_debug_ip_direction(pl_ocp* o, const double* s, const double* lam, const double* zl, const double* zu,
+                          const double* mu);
 
 /* CasADi external-function ABI (include/pinoloco_casadi.h): bind the OCP whose
  * shapes / sparsity the exported sqp_data, f_data, g_data, hess_data and

@@ -196,10 +196,11 @@ class IPRef:
             if not (np.all(np.isfinite(dx)) and np.all(np.isfinite(dl))):
                 status = ST_NONFINITE
                 break
-            self.trace.append(dict(W=W, rhat=rhat, rx=rx, rhs=rhs, dx=dx, dl=dl, ds=ds, jdx=J @ dx))
             tau = max(TAU_MIN, 1.0 - mu)
             amax = min(frac_to_boundary(sl, ds, tau, hl), frac_to_boundary(su, -ds, tau, hu))
             az = min(frac_to_boundary(zl, dzl, tau, hl), frac_to_boundary(zu, dzu, tau, hu))
+            self.trace.append(dict(x=x.copy(), s=s.copy(), lam=lam.copy(), zl=zl.copy(), zu=zu.copy(), mu=mu, W=W,
+                                   rhat=rhat, rx=rx, rhs=rhs, dx=dx, dl=dl, ds=ds, jdx=J @ dx, amax=amax, az=az))
             theta = float(np.sum(np.abs(c)))
             phi = self._phi(f, sl, su, hl, hu, mu)
             dphi = float(grad @ dx + np.sum(np.where(hl, -mu / sl, 0.0) * ds + np.where(hu, mu / su, 0.0) * ds))

@@ -52,12 +52,16 @@ PL_HD Dual& operator+=(Dual& a, Dual b) { a.v += b.v; a.d += b.d; return a; }
 PL_HD Dual& operator-=(Dual& a, Dual b) { a.v -= b.v; a.d -= b.d; return a; }
 PL_HD Dual& operator*=(Dual& a, Dual b) { a = a * b; return a; }
 
-PL_HD Dual sin(Dual a) { double s, c; sincos(a.v, &s, &c); return Dual(s, c * a.d); }
-PL_HD Dual cos(Dual a) { double s, c; sincos(a.v, &s, &c); return Dual(c, -s * a.d); }
-PL_HD void sincos_s(double a, double* s, double* c) { sincos(a, s, c); }
+// sin and cos separately: the device library's sincos takes its outputs through
+// private-memory pointers, which costs every kernel a scratch segment
+PL_HD Dual sin(Dual a) { return Dual(::sin(a.v), ::cos(a.v) * a.d); }
+PL_HD Dual cos(Dual a) { return Dual(::cos(a.v), -::sin(a.v) * a.d); }
+PL_HD void sincos_s(double a, double* s, double* c) {
+  *s = ::sin(a);
+  *c = ::cos(a);
+}
 PL_HD void sincos_s(Dual a, Dual* s, Dual* c) {
-  double sv, cv;
-  sincos(a.v, &sv, &cv);
+  const double sv = ::sin(a.v), cv = ::cos(a.v);
   *s = Dual(sv, cv * a.d);
   *c = Dual(cv, -sv * a.d);
 }

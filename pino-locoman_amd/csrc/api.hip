@@ -1321,6 +1321,30 @@ extern "C" int pl_ocp_ip_stats(pl_ocp* o, pl_ip_stats* out) {
   return 0;
 }
 
+extern "C" int pl_debug_ip_direction(pl_ocp* o, const double* S, const double* LAM, const double* ZL,
+                                     const double* ZU, const double* MU) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  if (!h->d.ipinfo) { pl_set_error("no interior-point state (pl_ocp_set_solver(o, PL_SOLVER_IP) first)"); return -1; }
+  const size_t Bm = (size_t)h->B * h->m * 8;
+  PL_CHECK_HIP(hipMemcpyAsync(h->d.ip_s, S, Bm, hipMemcpyHostToDevice, h->stream));
+  PL_CHECK_HIP(hipMemcpyAsync(h->d.ip_lam, LAM, Bm, hipMemcpyHostToDevice, h->stream));
+  PL_CHECK_HIP(hipMemcpyAsync(h->d.ip_zl, ZL, Bm, hipMemcpyHostToDevice, h->stream));
+  PL_CHECK_HIP(hipMemcpyAsync(h->d.ip_zu, ZU, Bm, hipMemcpyHostToDevice, h->stream));
+  std::vector<PlIpInfo> info(h->B);
+  for (int b = 0; b < h->B; ++b) {
+    memset(&info[b], 0, sizeof(PlIpInfo));
+    info[b].mu = MU[b];
+    info[b].active = 1;
+  }
+  PL_CHECK_HIP(hipMemcpyAsync(h->d.ipinfo, info.data(), h->B * sizeof(PlIpInfo), hipMemcpyHostToDevice, h->stream));
+  launch_reset_info(h);
+  enqueue_ip_direction(h);
+  PL_CHECK_HIP(hipGetLastError());
+  PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
 extern "C" int pl_ocp_solve(pl_ocp* o, pl_stats* stats, double* phase_ms) {
   REQUIRE_DEVICE(o);
   if (o->h.solver == PL_SOLVER_IP) {

@@ -73,8 +73,12 @@ __global__ __launch_bounds__(64) void k_eval_values(PlDev d, int B, int N, int n
 // chunk of 64 local columns), thread = local column.  Single-wave blocks retire
 // independently, so the cheap chunks (dx_{i+1} columns skip the tree pass) free their
 // SIMD slot at once.
+#ifndef PL_JAC_WAVES
+#define PL_JAC_WAVES 1
+#endif
 template <int DYN>
-__global__ __launch_bounds__(64) void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PL_JAC_WAVES)))
+void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz) {
   const int bi = blockIdx.x;
   const int b = bi / N, i = bi - (bi / N) * N;
   const PlNode nd = d.nodes[i];
@@ -93,9 +97,10 @@ __global__ __launch_bounds__(64) void k_eval_jac(PlDev d, int B, int N, int n, i
   VecIn<Dual> u{x + nd.x_off + ndx, nullptr, 0.0, lc - ndx};
   VecIn<Dual> dxn{x + nn.x_off, nullptr, 0.0, lc - nd.nw};
   JacEmit e{d.rowidx + nd.ent_off, d.Araw + (size_t)b * nnz + nd.ent_off, e0, e1, 0};
-  __shared__ double2 kst_raw[PL_KIN_STORE_DUAL * 64];  // Dual storage (Dual has constructors)
-  Dual* kst = reinterpret_cast<Dual*>(kst_raw);
-  pl::node_rows<Dual, DYN>(M, O, i, p, dx, u, dxn, e, kst + threadIdx.x, 64);
+  // kinematic outputs: per-lane tangents + one shared value per entry (NodeKin<Dual>)
+  __shared__ double kst_tan[PL_KIN_STORE_DUAL * 64];
+  __shared__ double kst_val[PL_KIN_STORE_DUAL];
+  pl::node_rows<Dual, DYN>(M, O, i, p, dx, u, dxn, e, reinterpret_cast<Dual*>(kst_tan + threadIdx.x), 64, kst_val);
 }
 
 __global__ __launch_bounds__(256) void k_objective(PlDev d, int N, int n, int np) {

@@ -251,9 +251,11 @@ __global__ __launch_bounds__(256) void k_ip_kkt(PlDev d, int N, int n, int m, in
     ip->err = err;
     ip->viol_max = v[11];
     ip->f = d.work[(size_t)b * 8];
-    ip->iter = k;
+    ip->iter = k < 0 ? 0 : k;
     int go = 1;
-    if (nonfinite || !isfinite(err)) {
+    if (k < 0) {
+      // teacher-forced direction (pl_debug_ip_direction): no termination, mu as given
+    } else if (nonfinite || !isfinite(err)) {
       ip->status = ST_NONFINITE;
       go = 0;
     } else if (err <= st.tol) {
@@ -264,7 +266,7 @@ __global__ __launch_bounds__(256) void k_ip_kkt(PlDev d, int N, int n, int m, in
       go = 0;
     }
     double mu_new = mu;
-    if (go) {
+    if (go && k >= 0) {
       for (int q = 0; q < 4; ++q) {
         if (fmax(base, v[6 + q] / sc) > KAPPA_EPS * mus[q]) break;
         if (mus[q + 1] == mus[q]) break;
@@ -272,7 +274,7 @@ __global__ __launch_bounds__(256) void k_ip_kkt(PlDev d, int N, int n, int m, in
         ip->nfilt = 0;
       }
       ip->mu = mu_new;
-    } else {
+    } else if (!go) {
       ip->active = 0;
       d.info[b].done = 1;
     }
@@ -389,7 +391,8 @@ __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int n, int m, int nn
 // Directions, fraction-to-boundary, filter line search and update.  dx = d.xa and
 // J dx = d.za (the ADMM sweep with alpha = 1 on unbounded rows).
 template <int DYN>
-__global__ __launch_bounds__(256) void k_ip_step(PlDev d, int N, int n, int m, int np, PlIpSettings st) {
+__global__ __launch_bounds__(256) void k_ip_step(PlDev d, int N, int n, int m, int np, PlIpSettings st,
+                                                 int dir_only) {
   const int b = blockIdx.x;
   PlIpInfo* ip = d.ipinfo + b;
   if (!ip->active) return;
@@ -470,6 +473,13 @@ __global__ __launch_bounds__(256) void k_ip_step(PlDev d, int N, int n, int m, i
   const double theta = v[2], f0 = d.work[(size_t)b * 8];
   const double phi = f0 - mu * v[3];
   const double dphi = v[4];
+  if (dir_only) {  // pl_debug_ip_direction: the direction and the step bounds only
+    if (threadIdx.x == 0) {
+      ip->alpha = amax;
+      ip->alpha_z = az;
+    }
+    return;
+  }
   if (v[5] != 0.0) {
     if (threadIdx.x == 0) {
       ip->status = ST_NONFINITE;
@@ -632,8 +642,34 @@ void enqueue_ip(PlOcpHandle* h) {
       launch_admm_init(h);
       launch_admm(h, 1, 0, 0);
     }
-    PL_DISPATCH_DYN(h->oc.dyn, k_ip_step, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->np, st);
+    PL_DISPATCH_DYN(h->oc.dyn, k_ip_step, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->np, st,
+                    0);
   }
   h->set = saved;
   hipLaunchKernelGGL(k_ip_finish, dim3((h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B);
+}
+
+// Teacher-forced Newton direction from a given interior-point state (x in d.x; s, lam,
+// zl, zu, mu uploaded by pl_debug_ip_direction): eval, KKT, factor, solve + refinement,
+// directions and step bounds; no line search, no update.
+void enqueue_ip_direction(PlOcpHandle* h) {
+  const PlIpSettings st = h->ip;
+  const PlSettings saved = h->set;
+  h->set.sigma = st.delta_w;
+  h->set.alpha = 1.0;
+  launch_eval_values(h, h->d.x);
+  launch_objective(h);
+  launch_eval_jac(h);
+  hipLaunchKernelGGL(k_ip_kkt, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz,
+                     std::max(h->ncpl_max, 1), -1, st);
+  launch_factor(h);
+  launch_admm_init(h);
+  launch_admm(h, 1, 0, 0);
+  for (int r = 0; r < st.n_refine; ++r) {
+    hipLaunchKernelGGL(k_ip_refine, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, h->m, h->nnz, st.delta_w);
+    launch_admm_init(h);
+    launch_admm(h, 1, 0, 0);
+  }
+  PL_DISPATCH_DYN(h->oc.dyn, k_ip_step, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->np, st, 1);
+  h->set = saved;
 }

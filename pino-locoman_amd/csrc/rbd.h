@@ -61,27 +61,39 @@ template <class S> PL_HD void quat_to_R(const S* qv, S* R) {  // Eigen toRotatio
   R[6] = txz - twy; R[7] = tyz + twx; R[8] = 1.0 - (txx + tyy);
 }
 
+// trace <= 0 branch for the largest diagonal entry I (compile-time indices: a run-time
+// index into R / q would put both arrays in scratch)
+template <int I, class S> PL_HD void R_to_quat_diag(const S* R, S* q) {
+  constexpr int J = (I + 1) % 3, K = (J + 1) % 3;
+  S s = sqrt_s(R[4 * I] - R[4 * J] - R[4 * K] + 1.0);
+  q[I] = 0.5 * s;
+  S inv = 0.5 / s;
+  q[3] = (R[3 * K + J] - R[3 * J + K]) * inv;
+  q[J] = (R[3 * J + I] + R[3 * I + J]) * inv;
+  q[K] = (R[3 * K + I] + R[3 * I + K]) * inv;
+}
+
 template <class S> PL_HD void R_to_quat(const S* R, S* q) {  // Eigen quaternionbase_assign_impl
+  // every branch fills its own local quaternion; one store per component at the end
+  // (stores from several branches into q kept its tangents in scratch)
+  S o[4];
   S t = R[0] + R[4] + R[8];
   if (val(t) > 0.0) {
     S s = sqrt_s(t + 1.0);
-    q[3] = 0.5 * s;
+    o[3] = 0.5 * s;
     S inv = 0.5 / s;
-    q[0] = (R[7] - R[5]) * inv;
-    q[1] = (R[2] - R[6]) * inv;
-    q[2] = (R[3] - R[1]) * inv;
+    o[0] = (R[7] - R[5]) * inv;
+    o[1] = (R[2] - R[6]) * inv;
+    o[2] = (R[3] - R[1]) * inv;
   } else {
     int i = 0;
     if (val(R[4]) > val(R[0])) i = 1;
     if (val(R[8]) > val(R[4 * i])) i = 2;
-    int j = (i + 1) % 3, k = (j + 1) % 3;
-    S s = sqrt_s(R[4 * i] - R[4 * j] - R[4 * k] + 1.0);
-    q[i] = 0.5 * s;
-    S inv = 0.5 / s;
-    q[3] = (R[3 * k + j] - R[3 * j + k]) * inv;
-    q[j] = (R[3 * j + i] + R[3 * i + j]) * inv;
-    q[k] = (R[3 * k + i] + R[3 * i + k]) * inv;
+    if (i == 0) R_to_quat_diag<0>(R, o);
+    else if (i == 1) R_to_quat_diag<1>(R, o);
+    else R_to_quat_diag<2>(R, o);
   }
+  for (int k = 0; k < 4; ++k) q[k] = o[k];
 }
 
 #define PL_TAYLOR_PREC3 1.2207031250000000e-04  // eps^(1/4), pinocchio TaylorSeriesExpansion<double>::precision<3>()
@@ -240,7 +252,10 @@ template <class S> PL_HD void motion_cross_force(const S* v, const S* f, S* out)
 // storage (LDS on the device, interleaved with a stride), so no thread keeps a
 // dynamically indexed register array (which the compiler would put in scratch).
 #define PL_KIN_STORE (PL_MAXV - 6 + 3 * PL_MAXFEET + 7 * PL_MAXCL)  // entries of a NodeKin store
-#define PL_KIN_STORE_DUAL (PL_MAXV - 6 + 3 * PL_MAXFEET)           // without the chain scratch
+#define PL_KIN_STORE_DUAL PL_KIN_STORE
+#ifndef PL_CHAIN_UNROLL
+#define PL_CHAIN_UNROLL 1  // chain loops of tree_pass: rolled (register pressure of the dual pass)
+#endif
 template <class S> struct NodeKin {
   S tau[6];    // RNEA base torques (if want_tau)
   S arm_vel[3];  // relative arm velocity rows (ocp.py:177-179)
@@ -251,6 +266,38 @@ template <class S> struct NodeKin {
   // per joint of the current chain: world motion subspace S_w (6) and S_w . prefix
   PL_HD S& sw(int kk, int c) { return store[(PL_MAXV - 6 + 3 * PL_MAXFEET + 7 * kk + c) * stride]; }
   PL_HD S& alpha(int kk) { return store[(PL_MAXV - 6 + 3 * PL_MAXFEET + 7 * kk + 6) * stride]; }
+  PL_HD void clear(int k) { store[k * stride] = S(0.0); }
+};
+
+// Dual-number store with the value and the tangent of an entry at separate addresses.
+// The Jacobian kernel's 64 lanes evaluate the same primal (one tangent each), so the
+// values go to one shared slot per entry (every writing lane stores identical bits)
+// and only the tangents are per lane: half the LDS of an interleaved Dual store,
+// which lets two single-wave workgroups share a SIMD.  The plain C++ callers point
+// both at an interleaved Dual array (vstride = dstride = 2 x stride).
+struct DualRef {
+  double* v;
+  double* d;
+  PL_HD operator Dual() const { return Dual(*v, *d); }
+  PL_HD DualRef& operator=(const Dual& x) {
+    *v = x.v;
+    *d = x.d;
+    return *this;
+  }
+};
+template <> struct NodeKin<Dual> {
+  Dual tau[6];
+  Dual arm_vel[3];
+  double* vst;  // values   [PL_KIN_STORE_DUAL] x vstride
+  double* dst;  // tangents [PL_KIN_STORE_DUAL] x dstride
+  int vstride, dstride;
+  PL_HD DualRef at(int k) { return DualRef{vst + k * vstride, dst + k * dstride}; }
+  PL_HD DualRef tau_j(int k) { return at(k); }
+  PL_HD DualRef foot_vel(int e, int c) { return at(PL_MAXV - 6 + 3 * e + c); }
+  PL_HD DualRef sw(int kk, int c) { return at(PL_MAXV - 6 + 3 * PL_MAXFEET + 7 * kk + c); }
+  PL_HD DualRef alpha(int kk) { return at(PL_MAXV - 6 + 3 * PL_MAXFEET + 7 * kk + 6); }
+  // a skipped tree pass: zero tangent (the shared value slot belongs to the lanes that ran it)
+  PL_HD void clear(int k) { dst[k * dstride] = 0.0; }
 };
 
 // q / v accessors over x_init + dx (ocp_whole_body_rnea.py:173-181): the free-flyer
@@ -322,19 +369,11 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
     for (int k = 0; k < 3; ++k) op[k] = p0[k];
     S P[6];
     for (int k = 0; k < 6; ++k) P[k] = S(0.0);
-    // chain scratch (S_w, S_w . prefix per joint): registers for the dual-number
-    // Jacobian (LDS there is the occupancy limit), the NodeKin store for values
-    constexpr bool kRegSw = !std::is_same<S, double>::value;
-    S swr[kRegSw ? PL_MAXCL : 1][6], alr[kRegSw ? PL_MAXCL : 1];
-    auto SW = [&](int kk, int c) -> S& {
-      if constexpr (kRegSw) return swr[kk][c];
-      else return out.sw(kk, c);
-    };
-    auto AL = [&](int kk) -> S& {
-      if constexpr (kRegSw) return alr[kk];
-      else return out.alpha(kk);
-    };
-#pragma unroll
+    // chain scratch (S_w, S_w . prefix per joint) in the NodeKin store (LDS on the
+    // device; for the dual numbers only the tangents are per lane)
+    auto SW = [&](int kk, int c) -> decltype(auto) { return out.sw(kk, c); };
+    auto AL = [&](int kk) -> decltype(auto) { return out.alpha(kk); };
+#pragma unroll PL_CHAIN_UNROLL
     for (int kk = 0; kk < PL_MAXCL; ++kk) {
       if (kk >= L) break;
       const int j = first + kk;
@@ -427,7 +466,7 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
     }
     if (want_tau) {
       // tau_j = S_w^T (F_total - prefix_before_j)
-#pragma unroll
+#pragma unroll PL_CHAIN_UNROLL
       for (int kk = 0; kk < PL_MAXCL; ++kk) {
         if (kk >= L) break;
         const int j = first + kk;
@@ -507,7 +546,9 @@ PL_HD void centroidal_pass(const PlModel& M, const PlOcpConst& O, const S* qb, c
       for (int k = 0; k < 6; ++k) H[k] += hw[k];
     }
     if (want_hdot) {
-      for (int e = 0; e < O.nee; ++e) {
+#pragma unroll
+      for (int e = 0; e < PL_MAXFEET + 1; ++e) {  // constant bound: pe stays in registers
+        if (e >= O.nee) break;
         const PlFrameRef& F = (e < O.nfeet) ? O.feet[e] : O.ext;
         if (F.joint != j) continue;
         S t[3];
@@ -561,7 +602,9 @@ PL_HD void centroidal_pass(const PlModel& M, const PlOcpConst& O, const S* qb, c
   }
   if (want_hdot) {
     S dp[3] = {S(0.0), S(0.0), S(-9.81 * m)}, dl[3] = {S(0.0), S(0.0), S(0.0)};
-    for (int e = 0; e < O.nee; ++e) {
+#pragma unroll
+    for (int e = 0; e < PL_MAXFEET + 1; ++e) {
+      if (e >= O.nee) break;
       S f[3] = {forces[3 * e], forces[3 * e + 1], forces[3 * e + 2]};
       S r[3] = {pe[e][0] - com[0], pe[e][1] - com[1], pe[e][2] - com[2]};
       S t[3];

@@ -81,9 +81,12 @@ template <class S> PL_HD VecIn<S> sub_in(const VecIn<S>& a, int off) {
 
 // kstore: caller storage for the run-time indexed kinematic outputs (NodeKin,
 // PL_KIN_STORE entries spaced by kstride).
+// kvals (Dual only): a shared value store for the kinematic outputs (NodeKin<Dual>);
+// null keeps values and tangents interleaved in kstore.
 template <class S, int DYN, class Emit>
 PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double* p, const VecIn<S>& dx,
-                     const VecIn<S>& u, const VecIn<S>& dxn, Emit& emit, S* kstore, int kstride) {
+                     const VecIn<S>& u, const VecIn<S>& dxn, Emit& emit, S* kstore, int kstride,
+                     double* kvals = nullptr) {
   const int nv = O.nv, nq = O.nq, nj = O.nj;
   constexpr bool CV = (DYN == PL_DYN_CV);
   const double* xi = p + O.P.x_init;
@@ -108,8 +111,23 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
   // centroidal_vel keeps the state rows at node 0 (ocp.py:137-140, 170-173)
   const bool state_rows = CV || (type != 0);
   NodeKin<S> kin;
-  kin.store = kstore;
-  kin.stride = kstride;
+  if constexpr (std::is_same<S, Dual>::value) {
+    double* raw = reinterpret_cast<double*>(kstore);
+    if (kvals) {  // shared values, per-lane tangents (kstore holds kstride-strided doubles)
+      kin.vst = kvals;
+      kin.vstride = 1;
+      kin.dst = raw;
+      kin.dstride = kstride;
+    } else {
+      kin.vst = raw;
+      kin.dst = raw + 1;
+      kin.vstride = kin.dstride = 2 * kstride;
+    }
+  } else {
+    (void)kvals;
+    kin.store = kstore;
+    kin.stride = kstride;
+  }
   constexpr bool want_tau = (DYN == PL_DYN_RNEA || DYN == PL_DYN_ACC);
   // A Jacobian column seeded on dx_{i+1}, or (rnea) on tau_j, has a zero tangent in the
   // tree pass and the ABA: every row that reads them then has a zero derivative, so
@@ -128,7 +146,7 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
   if (tree && (want_tau || state_rows)) {
     tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin);
   } else {  // a skipped pass leaves zero (value and tangent) kinematic outputs
-    for (int k = 0; k < PL_KIN_STORE_DUAL; ++k) kin.store[k * kstride] = S(0.0);
+    for (int k = 0; k < PL_KIN_STORE_DUAL; ++k) kin.clear(k);
     for (int k = 0; k < 3; ++k) kin.arm_vel[k] = S(0.0);
   }
   S hg[CV ? 6 : 1], hdot[CV ? 6 : 1];

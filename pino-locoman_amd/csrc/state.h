@@ -275,6 +275,7 @@ void launch_reset_info(PlOcpHandle* h);
 void launch_reset_iterates(PlOcpHandle* h);
 void launch_reset_prof(PlOcpHandle* h);
 void enqueue_ip(PlOcpHandle* h);
+void enqueue_ip_direction(PlOcpHandle* h);
 
 #define PL_CHECK_HIP(expr)                                                        \
   do {                                                                            \

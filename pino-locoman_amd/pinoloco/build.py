@@ -26,8 +26,9 @@ def _hipcc():
 
 
 def _flags():
+    # PL_HIPCC_DEFS: extra -D options for kernel A/B experiments (e.g. -DPL_JAC_WAVES=2)
     return ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-fPIC", "-Wno-unused-result", "-Wno-unused-value",
-            "-I", CSRC, "-I", os.path.join(CSRC, "..", "..", "include")]
+            "-I", CSRC, "-I", os.path.join(CSRC, "..", "..", "include")] + os.environ.get("PL_HIPCC_DEFS", "").split()
 
 
 def _newest_input():

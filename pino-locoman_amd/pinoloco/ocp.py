@@ -272,6 +272,19 @@ class BatchedOCP:
         _lib.check(_lib.lib().pl_ocp_get_lam(self.h, _lib.dptr(lam)))
         return lam
 
+    def ip_direction(self, X, S, LAM, ZL, ZU, MU):
+        """Teacher-forced interior-point Newton direction (parity aid): (dx, dlam, ds,
+        alpha_max, alpha_z) from the given iterate, slacks and multipliers."""
+        self.set_x(X)
+        arrs = [np.ascontiguousarray(np.broadcast_to(np.asarray(a, dtype=np.float64), (self.batch, self.m)))
+                for a in (S, LAM, ZL, ZU)]
+        mu = np.ascontiguousarray(np.broadcast_to(np.asarray(MU, dtype=np.float64), (self.batch,)))
+        _lib.check(_lib.lib().pl_debug_ip_direction(self.h, *[_lib.dptr(a) for a in arrs], _lib.dptr(mu)))
+        B = self.batch
+        st = self.ip_stats()
+        return (self.debug("ip_dx", B * self.n).reshape(B, self.n), self.debug("ip_dl", B * self.m).reshape(B, self.m),
+                self.debug("ip_ds", B * self.m).reshape(B, self.m), st["alpha"], st["alpha_z"])
+
     def solve(self, timed=False):
         stats = (_lib.Stats * self.batch)()
         phase = np.zeros(4)
