@@ -871,6 +871,46 @@ int dalloc(pl_ocp* o, T** p, size_t count) {
   return 0;
 }
 
+// Work list of the Jacobian kernel (k_eval_jac): one lane per non-empty local column.
+// Columns whose dual pass runs the tree / ABA / centroidal recursion come first, packed
+// 64 per wave ACROSS node boundaries and padded to whole waves; then the columns that
+// skip it (dx_{i+1}; rnea tau_j; centroidal h), which are cheap.  The classification
+// mirrors node_rows' skip logic (rows.h); it only affects the schedule.
+int build_jac_list(pl_ocp* o, std::vector<int2>& list) {
+  const PlOcpConst& O = o->h.oc;
+  std::vector<int2> ex, ch;
+  for (int i = 0; i < o->h.N; ++i) {
+    const PlNode& nd = o->nodes[i];
+    const int* cp = o->colptr.data() + nd.colptr_off;
+    for (int lc = 0; lc < nd.ncol; ++lc) {
+      if (cp[lc] == cp[lc + 1]) continue;
+      bool cheap;
+      if (lc >= nd.nw) {
+        cheap = true;
+      } else if (lc < O.ndx) {
+        cheap = O.dyn == PL_DYN_CV && lc < 6;
+      } else {
+        const int k = lc - O.ndx;
+        cheap = O.dyn == PL_DYN_RNEA && k >= O.na + O.nf;
+      }
+      (cheap ? ch : ex).push_back(make_int2(i, lc));
+    }
+  }
+  while (ex.size() % 64) ex.push_back(make_int2(-1, -1));
+  // a wave's lanes hold at most PL_JAC_SLOTS consecutive nodes (shared-value slots)
+  for (size_t w = 0; w < ex.size(); w += 64) {
+    int last = ex[w].x;
+    for (size_t q = w; q < w + 64; ++q) last = std::max(last, ex[q].x);
+    if (last - ex[w].x >= PL_JAC_SLOTS) {
+      pl_set_error("Jacobian wave spans more than %d nodes", PL_JAC_SLOTS);
+      return -1;
+    }
+  }
+  list = ex;
+  list.insert(list.end(), ch.begin(), ch.end());
+  return 0;
+}
+
 template <class T>
 int upload(pl_ocp* o, T** p, const std::vector<T>& v) {
   if (dalloc(o, p, v.size())) return -2;
@@ -1031,6 +1071,15 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= upload(o, &D.kasm, o->kasm);
   rc |= upload(o, &D.kfl, o->kfl);
   rc |= upload(o, &D.kcpl, o->kcpl);
+  {
+    std::vector<int2> jl;
+    if (build_jac_list(o, jl)) {
+      pl_ocp_destroy(o);
+      return -1;
+    }
+    h.jl_len = (int)jl.size();
+    rc |= upload(o, &D.jlist, jl);
+  }
   const size_t n = h.n, m = h.m, nnz = h.nnz;
   rc |= dalloc(o, &D.p, B * h.np);
   rc |= dalloc(o, &D.x, B * n);

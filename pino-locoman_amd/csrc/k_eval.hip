@@ -69,24 +69,27 @@ __global__ __launch_bounds__(64) void k_eval_values(PlDev d, int B, int N, int n
   pl::node_rows<double, DYN>(M, O, i, p, dx, u, dxn, e, kst + threadIdx.x, 64);
 }
 
-// Constraint Jacobian values on the fixed pattern.  Block = one wave = (problem, node,
-// chunk of 64 local columns), thread = local column.  Single-wave blocks retire
-// independently, so the cheap chunks (dx_{i+1} columns skip the tree pass) free their
-// SIMD slot at once.
+// Constraint Jacobian values on the fixed pattern.  One lane = one (node, local column)
+// of the work list d.jlist (api.hip build_jac_list): the columns that run the tree pass
+// are packed 64 per wave across node boundaries, the cheap ones follow; grid (waves, B).
+// Each lane seeds the tangent of its column and writes the column's entries (CSC order
+// inside the node).  Single-wave blocks retire independently.
 #ifndef PL_JAC_WAVES
 #define PL_JAC_WAVES 1
 #endif
 template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PL_JAC_WAVES)))
-void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz) {
-  const int bi = blockIdx.x;
-  const int b = bi / N, i = bi - (bi / N) * N;
+void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz, int jl_len) {
+  const int b = blockIdx.y;
+  const int q = (int)blockIdx.x * 64 + threadIdx.x;
+  const int first = d.jlist[blockIdx.x * 64].x;  // the wave's first node (never padding)
+  if (q >= jl_len) return;
+  const int2 jw = d.jlist[q];
+  if (jw.x < 0) return;
+  const int i = jw.x, lc = jw.y;
   const PlNode nd = d.nodes[i];
-  const int lc = (int)blockIdx.y * 64 + threadIdx.x;  // chunk y: dispatched after every chunk y - 1
-  if (lc >= nd.ncol) return;
   const int* cp = d.colptr + nd.colptr_off;
   const int e0 = cp[lc], e1 = cp[lc + 1];
-  if (e0 == e1) return;
   const PlOcpConst& O = *d.oc;
   const PlModel& M = *d.model;
   const PlNode nn = d.nodes[i + 1];
@@ -97,10 +100,13 @@ void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz) {
   VecIn<Dual> u{x + nd.x_off + ndx, nullptr, 0.0, lc - ndx};
   VecIn<Dual> dxn{x + nn.x_off, nullptr, 0.0, lc - nd.nw};
   JacEmit e{d.rowidx + nd.ent_off, d.Araw + (size_t)b * nnz + nd.ent_off, e0, e1, 0};
-  // kinematic outputs: per-lane tangents + one shared value per entry (NodeKin<Dual>)
+  // kinematic outputs: per-lane tangents + one shared value per entry and node of the
+  // wave (NodeKin<Dual>; the cheap columns read no stored value)
   __shared__ double kst_tan[PL_KIN_STORE_DUAL * 64];
-  __shared__ double kst_val[PL_KIN_STORE_DUAL];
-  pl::node_rows<Dual, DYN>(M, O, i, p, dx, u, dxn, e, reinterpret_cast<Dual*>(kst_tan + threadIdx.x), 64, kst_val);
+  __shared__ double kst_val[PL_JAC_SLOTS * PL_KIN_STORE_DUAL];
+  const int slot = min(i - first, PL_JAC_SLOTS - 1);
+  pl::node_rows<Dual, DYN>(M, O, i, p, dx, u, dxn, e, reinterpret_cast<Dual*>(kst_tan + threadIdx.x), 64,
+                           kst_val + slot * PL_KIN_STORE_DUAL);
 }
 
 __global__ __launch_bounds__(256) void k_objective(PlDev d, int N, int n, int np) {
@@ -147,8 +153,8 @@ void launch_eval_values(PlOcpHandle* h, const double* xsrc) {
 }
 
 void launch_eval_jac(PlOcpHandle* h) {
-  PL_DISPATCH_DYN(h->oc.dyn, k_eval_jac, dim3(h->B * h->N, (h->ncol_max + 63) / 64), dim3(64), 0, h->stream, h->d,
-                  h->B, h->N, h->n, h->np, h->nnz);
+  PL_DISPATCH_DYN(h->oc.dyn, k_eval_jac, dim3((h->jl_len + 63) / 64, h->B), dim3(64), 0, h->stream, h->d, h->B,
+                  h->N, h->n, h->np, h->nnz, h->jl_len);
 }
 
 void launch_objective(PlOcpHandle* h) {

@@ -17,6 +17,7 @@
 #define PL_MAXNJ 32     // actuated joints
 #define PL_MAXFEET 4
 #define PL_MAXNU 128
+#define PL_JAC_SLOTS 3  // nodes per Jacobian wave (k_eval_jac shared-value slots; 4 would exceed 40 KB of LDS per wave)
 
 enum { PL_JT_UNIVERSE = 0, PL_JT_FREEFLYER = 1, PL_JT_REVOLUTE = 2 };
 enum { PL_AX_X = 0, PL_AX_Y = 1, PL_AX_Z = 2, PL_AX_GEN = 3 };

@@ -163,6 +163,7 @@ struct PlDev {
   uint32_t* kcpl;        // factor coupling programs
   double* FS;            // factor scratch [B][fs_stride]: A', G, C^-1 per node
   uint32_t* ttab;        // lane-tile tables [64][PL_ADMM_KM] per distinct (T, K): (I << 24) | (J << 16) | cidx
+  int2* jlist;           // k_eval_jac work list: (node, local column), tree-pass columns first (whole waves)
   // per problem [B][*]
   double* p;         // params
   double* x;         // SQP iterate (decision vector)
@@ -229,6 +230,7 @@ struct PlOcpHandle {
   int admm_fwd_asb;                 // coupling rows too dense for registers: forward steps stage A in LDS
   int sqp_iters;                    // SQP iterations per solve (reference: 1, ocp.py:382-383)
   int admm_waves;                   // ADMM sweep kernel: 2 = k_admm2 (two waves per problem), 1 = k_admm
+  int jl_len;                       // k_eval_jac work-list entries (a multiple of 64 before the cheap part)
   int solver;                       // PL_SOLVER_OSQP (SQP + OSQP ADMM) or PL_SOLVER_IP (interior point)
   PlIpSettings ip;
   long long fs_stride;              // factor scratch per problem (doubles)
