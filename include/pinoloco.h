@@ -56,6 +56,7 @@ typedef struct pl_ocp pl_ocp;
 #define PL_DYN_WHOLE_BODY_ACC 1
 #define PL_DYN_WHOLE_BODY_ABA 2
 #define PL_DYN_CENTROIDAL_VEL 3      /* x = [h (6), q], dx = [dh, dq], u = [v | f] */
+#define PL_DYN_CENTROIDAL_ACC 4      /* x = [q, v], u = [a | f] (include_base) or [a_j | f] */
 
 typedef struct {
   int njoints;                 /* including the universe joint 0 */
@@ -239,6 +240,7 @@ typedef struct pl_dyn pl_dyn;
 #define PL_FN_DIFFERENCE_WB 16 /* state_difference (x0, x1) -> dx                dynamics_whole_body_torque.py:27-40 */
 #define PL_FN_INTEGRATE_CV 17  /* state_integrate (x=[h,q], dx=[dh,dq]) -> x'    dynamics_centroidal_vel.py:12-26 */
 #define PL_FN_DIFFERENCE_CV 18 /* state_difference (x0, x1) -> dx                dynamics_centroidal_vel.py:28-41 */
+#define PL_FN_GAPS_CA 19       /* dynamics_gaps(q, v, a, forces) -> [6]          dynamics_centroidal_acc.py:92-119 */
 int pl_dyn_create(const pl_model* model, const int* foot_frames, int ext_force_frame, int base_frame, int device,
                   pl_dyn** out);
 void pl_dyn_destroy(pl_dyn* d);

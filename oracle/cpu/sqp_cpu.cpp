@@ -756,6 +756,8 @@ extern "C" double cpu_mpc_batch(void* h, int B, const double* P, const double* X
         case PL_DYN_RNEA: run_problem<PL_DYN_RNEA>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
         case PL_DYN_ACC: run_problem<PL_DYN_ACC>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
         case PL_DYN_ABA: run_problem<PL_DYN_ABA>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
+        case PL_DYN_CA: run_problem<PL_DYN_CA>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
+        case PL_DYN_ACCNB: run_problem<PL_DYN_ACCNB>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
         default: run_problem<PL_DYN_CV>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
       }
     }
@@ -780,6 +782,8 @@ extern "C" int cpu_sqp_step(void* h, const double* p, double* x, double* dx, int
     case PL_DYN_RNEA: s = sqp_step<PL_DYN_RNEA>(pr, w, st, p, Pd.data(), x); break;
     case PL_DYN_ACC: s = sqp_step<PL_DYN_ACC>(pr, w, st, p, Pd.data(), x); break;
     case PL_DYN_ABA: s = sqp_step<PL_DYN_ABA>(pr, w, st, p, Pd.data(), x); break;
+    case PL_DYN_CA: s = sqp_step<PL_DYN_CA>(pr, w, st, p, Pd.data(), x); break;
+    case PL_DYN_ACCNB: s = sqp_step<PL_DYN_ACCNB>(pr, w, st, p, Pd.data(), x); break;
     default: s = sqp_step<PL_DYN_CV>(pr, w, st, p, Pd.data(), x); break;
   }
   for (int j = 0; j < pr.n; ++j) dx[j] = w.step[j];

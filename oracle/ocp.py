@@ -76,17 +76,19 @@ class OracleOCP:
         self.ee_frames = self.feet + ([self.ext] if self.ext is not None else [])
         self.tau_nodes = tau_nodes if dynamics == "whole_body_rnea" else 0
         self.include_acc = include_acc
+        self.include_base = include_base
         nv, nj, nf = self.nv, self.nj, self.nf
         if dynamics == "whole_body_rnea":
             self.nx, self.ndx = self.nq + nv, 2 * nv
             na = nv if include_acc else 0
             self.na = na
             self.nu = [na + nf + nj] * tau_nodes + [na + nf] * (nodes - tau_nodes)
-        elif dynamics == "whole_body_acc":
-            assert include_base, "include_base=False (M_bb^-1 base acceleration) is not restated"
+        elif dynamics in ("whole_body_acc", "centroidal_acc"):
+            # u = [a | f] (include_base) or [a_j | f] with the base acceleration from the
+            # dynamics (ocp_whole_body_acc.py:56-63, 124-135; ocp_centroidal_acc.py:15-19)
             self.nx, self.ndx = self.nq + nv, 2 * nv
-            self.na = nv
-            self.nu = [nv + nf] * nodes
+            self.na = nv if include_base else nj
+            self.nu = [self.na + nf] * nodes
         elif dynamics == "whole_body_aba":
             self.nx, self.ndx = self.nq + nv, 2 * nv
             self.nu = [nj + nf] * nodes
@@ -162,8 +164,8 @@ class OracleOCP:
             Q = Qb + Qj + Qv
             if self.dynamics == "whole_body_rnea":
                 R = [1e-3] * self.na + [1e-3] * nf + [1e-4] * nj
-            elif self.dynamics == "whole_body_acc":
-                R = [1e-3] * self.nv + [1e-3] * nf
+            elif self.dynamics in ("whole_body_acc", "centroidal_acc"):
+                R = [1e-3] * self.na + [1e-3] * nf
             else:
                 R = [1e-3] * nj + [1e-3] * nf
         W = [0.0] * nj
@@ -183,8 +185,8 @@ class OracleOCP:
         fd = self.f_des(P)
         if self.dynamics == "whole_body_rnea":
             return np.concatenate([np.zeros(self.na), fd, np.zeros(self.nj)])
-        if self.dynamics == "whole_body_acc":
-            return np.concatenate([np.zeros(self.nv), fd])
+        if self.dynamics in ("whole_body_acc", "centroidal_acc"):
+            return np.concatenate([np.zeros(self.na), fd])
         if self.dynamics == "whole_body_aba":
             return np.concatenate([np.zeros(self.nj), fd])
         return np.concatenate([np.zeros(self.nv), fd])
@@ -257,13 +259,25 @@ class OracleOCP:
                 add(tau[..., 6:] - tau_j, 0, 0)
                 tmax = self.robot.joint_torque_max
                 add(tau_j, -tmax, tmax)
-        elif dyn == "whole_body_acc":
-            a = u[..., :nv]
-            forces = u[..., nv:]
+        elif dyn in ("whole_body_acc", "centroidal_acc"):
+            forces = u[..., self.na:]
+            if self.include_base:
+                a = u[..., :nv]
+            else:  # get_a (ocp_whole_body_acc.py:124-135, ocp_centroidal_acc.py:123-134)
+                a_j = u[..., :nj]
+                if dyn == "whole_body_acc":
+                    a_b = rbd.base_acc_wb(self.M, self.ee_frames, q, v, a_j, forces)
+                else:
+                    a_b = rbd.base_acc_ca(self.M, self.ee_frames, q, v, a_j, forces, self.mass)
+                a = np.concatenate([a_b, a_j], -1)
             add(dx_next[..., :nv] - (dx[..., :nv] + v * dt), 0, 0)
             add(dx_next[..., nv:] - (dx[..., nv:] + a * dt), 0, 0)
-            tau = rbd.rnea_dynamics(self.M, self.ee_frames, q, v, a, forces)
-            add(tau[..., :6], 0, 0)
+            if self.include_base:
+                if dyn == "whole_body_acc":  # dynamics_gaps = RNEA base rows
+                    tau = rbd.rnea_dynamics(self.M, self.ee_frames, q, v, a, forces)
+                    add(tau[..., :6], 0, 0)
+                else:  # A a + dA v - dh (dynamics_centroidal_acc.py:92-119)
+                    add(rbd.gaps_ca(self.M, self.ee_frames, q, v, a, forces, self.mass), 0, 0)
         elif dyn == "whole_body_aba":
             tau_j = u[..., :nj]
             forces = u[..., nj:]
@@ -554,6 +568,8 @@ class OracleOCP:
                 uw = np.concatenate([a_prev, f] + ([U[i][self.na + self.nf:]] if i < self.tau_nodes else []))
             elif self.dynamics == "whole_body_aba":
                 uw = np.concatenate([U[i][:self.nj], f])
+            elif self.dynamics in ("whole_body_acc", "centroidal_acc"):
+                uw = np.concatenate([U[i][:self.na], f])
             else:
                 uw = np.concatenate([U[i][:self.nv], f])
             x[o:o + self.nu[i]] = uw

@@ -302,15 +302,17 @@ def joint_vel(M, i, x):
     return np.stack([z, z, z, a[0] * x[..., iv], a[1] * x[..., iv], a[2] * x[..., iv]], -1)
 
 
-def rnea(M: ModelArrays, q, v, a, fext=None):
-    """pinocchio::rnea(model, data, q, v, a, fext) -- fext[i] in joint-i local frame."""
+def rnea(M: ModelArrays, q, v, a, fext=None, gravity=True):
+    """pinocchio::rnea(model, data, q, v, a, fext) -- fext[i] in joint-i local frame
+    (gravity=False: the same recursion with a zero gravity field)."""
     li, _ = forward_kinematics(M, q)
     nb = M.nj
     vs, as_, fs = [None] * nb, [None] * nb, [None] * nb
     shape = q.shape[:-1]
     dt = np.result_type(q, v, a)
     g = np.zeros(shape + (6,), dtype=dt)
-    g[..., :3] = -M.gravity
+    if gravity:
+        g[..., :3] = -M.gravity
     for i in range(1, nb):
         R, p = li[i]
         par = M.parent[i]
@@ -399,7 +401,7 @@ def crba(M: ModelArrays, q):
     li, _ = forward_kinematics(M, q)
     shape = q.shape[:-1]
     Yc = [np.broadcast_to(M.Y6[i], shape + (6, 6)).copy() for i in range(M.nj)]
-    Mq = np.zeros(shape + (M.nv, M.nv))
+    Mq = np.zeros(shape + (M.nv, M.nv), dtype=q.dtype)  # complex under the complex-step Jacobian
     for i in range(M.nj - 1, 0, -1):
         Si = _S(M, i, shape, float)
         iv, nvi = M.idx_v[i], Si.shape[1]
@@ -606,9 +608,11 @@ def base_acc_wb(M: ModelArrays, frames, q, v, a_j, forces):
     M_bb^-1 (-nle_b - M_bj a_j + sum_k J_c,k[:3, :6]^T f_k) with crba, nonLinearEffects
     and computeFrameJacobian(LOCAL_WORLD_ALIGNED)."""
     Mq = crba(M, q)
-    nle = rnea(M, q, v, np.zeros(M.nv))
-    tb = sum(frame_jacobian_lwa(M, q, fid)[:3, :6].T @ forces[3 * k:3 * k + 3] for k, fid in enumerate(frames))
-    return np.linalg.solve(Mq[:6, :6], -nle[:6] - Mq[:6, 6:] @ a_j + tb)
+    nle = rnea(M, q, v, np.zeros_like(v))
+    tb = sum(np.einsum("...ji,...j->...i", frame_jacobian_lwa(M, q, fid)[..., :3, :6], forces[..., 3 * k:3 * k + 3])
+             for k, fid in enumerate(frames))
+    rhs = -nle[..., :6] - np.einsum("...ij,...j->...i", Mq[..., :6, 6:], a_j) + tb
+    return np.linalg.solve(Mq[..., :6, :6], rhs[..., None])[..., 0]
 
 
 def ab_inv_ocs2(Ab):
@@ -621,3 +625,33 @@ def ab_inv_ocs2(Ab):
     out[:3, 3:] = -Ab[:3, 3:] @ A22i / m
     out[3:, 3:] = A22i
     return out
+
+
+def momentum_rate(M: ModelArrays, q, v, a):
+    """A_G(q) a + dA_G(q, v) v (computeCentroidalMap, dccrba): the rate of the centroidal
+    momentum, as the Newton-Euler sum of the body wrenches without gravity: the root's
+    subtree force of a zero-gravity RNEA, moved to world axes and then to the CoM.
+    Arithmetic only (safe under the complex-step Jacobian); pinned against
+    centroidal_map(q) a + dccrba_v(q, v) in tests/test_oracle.py."""
+    f_root = rnea(M, q, v, a, gravity=False)[..., :6]
+    li, oM = forward_kinematics(M, q)
+    R, p = oM[1]
+    f = act_force(R, p, f_root)  # world axes, about the world origin
+    com = center_of_mass(M, q)
+    return np.concatenate([f[..., :3], f[..., 3:] - cross(com, f[..., :3])], -1)
+
+
+def base_acc_ca(M: ModelArrays, frames, q, v, a_j, forces, mass):
+    """DynamicsCentroidalAcc.base_acc_dynamics (dynamics_centroidal_acc.py:43-90):
+    A_b^-1 (dh - dA v - A_j a_j), with A [0; a_j] + dA v as momentum_rate(q, v, [0; a_j])."""
+    A = centroidal_map(M, q)
+    dh = com_dynamics(M, frames, q, forces, mass, scale=False)
+    a0 = np.concatenate([np.zeros(a_j.shape[:-1] + (6,), dtype=a_j.dtype), a_j], -1)
+    rhs = dh - momentum_rate(M, q, v, a0)
+    return np.linalg.solve(A[..., :, :6], rhs[..., None])[..., 0]
+
+
+def gaps_ca(M: ModelArrays, frames, q, v, a, forces, mass):
+    """DynamicsCentroidalAcc.dynamics_gaps (dynamics_centroidal_acc.py:92-119):
+    A a + dA v - dh."""
+    return momentum_rate(M, q, v, a) - com_dynamics(M, frames, q, forces, mass, scale=False)

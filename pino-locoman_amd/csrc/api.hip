@@ -167,6 +167,7 @@ void build_blocks(PlOcpConst& O, bool has_ext, bool has_arm) {
       add_block(O, type, PL_RB_DYNV, O.nv);
     }
     if (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC) add_block(O, type, PL_RB_RNEA_BASE, 6);
+    if (O.dyn == PL_DYN_CA) add_block(O, type, PL_RB_CA_GAP, 6);
     if (tau) {
       add_block(O, type, PL_RB_TAU_EQ, O.nj);
       add_block(O, type, PL_RB_TAU_BND, O.nj);
@@ -214,12 +215,13 @@ std::vector<std::vector<int>> node_row_deps(const PlModel& M, const PlOcpConst& 
   auto U = [&](int k) { return ndx + k; };
   auto DV = [&](int k) { return cv ? ndx + k : nv + k; };
   auto DXN = [&](int k) { return nw + k; };
-  const int f_off = (O.dyn == PL_DYN_RNEA) ? O.na : ((O.dyn == PL_DYN_ACC || cv) ? nv : nj);
+  const bool accf = O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA || O.dyn == PL_DYN_ACCNB;
+  const int f_off = (O.dyn == PL_DYN_RNEA || accf) ? O.na : (cv ? nv : nj);
   auto F = [&](int k) { return U(f_off + k); };
-  std::vector<int> dynset;  // dependency set of the RNEA / ABA outputs
+  std::vector<int> dynset;  // dependency set of the RNEA / ABA / base-solve outputs
   for (int k = 3; k < nv; ++k) dynset.push_back(DQ(k));
   for (int k = 0; k < nv; ++k) dynset.push_back(DV(k));
-  if (O.dyn == PL_DYN_ABA) {
+  if (O.dyn == PL_DYN_ABA || O.dyn == PL_DYN_ACCNB) {
     for (int k = 0; k < nj; ++k) dynset.push_back(U(k));
   } else {
     for (int k = 0; k < nv; ++k) dynset.push_back(U(k));
@@ -243,10 +245,18 @@ std::vector<std::vector<int>> node_row_deps(const PlModel& M, const PlOcpConst& 
         case PL_RB_INIT: s = {r}; break;
         case PL_RB_DYNQ: s = {DQ(r), DV(r), DXN(r)}; break;
         case PL_RB_DYNV:
-          if (O.dyn == PL_DYN_ABA) { s = dynset; s.push_back(DV(r)); s.push_back(DXN(nv + r)); }
-          else s = {DV(r), U(r), DXN(nv + r)};
+          if (O.dyn == PL_DYN_ABA || (O.dyn == PL_DYN_ACCNB && r < 6)) {
+            s = dynset;
+            s.push_back(DV(r));
+            s.push_back(DXN(nv + r));
+          } else if (O.dyn == PL_DYN_ACCNB) {
+            s = {DV(r), U(r - 6), DXN(nv + r)};
+          } else {
+            s = {DV(r), U(r), DXN(nv + r)};
+          }
           break;
         case PL_RB_RNEA_BASE: s = dynset; break;
+        case PL_RB_CA_GAP: s = dynset; break;
         case PL_RB_TAU_EQ: s = dynset; s.push_back(U(O.na + nf + r)); break;
         case PL_RB_TAU_BND: s = {U(O.na + nf + r)}; break;
         case PL_RB_FZ: s = {F(3 * k + 2)}; break;
@@ -922,13 +932,12 @@ int upload(pl_ocp* o, T** p, const std::vector<T>& v) {
 
 extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int batch, int device, pl_ocp** out) {
   if (!model || !d || !out || batch <= 0) { pl_set_error("bad arguments"); return -1; }
-  if (d->dynamics < 0 || d->dynamics > 3) { pl_set_error("Unknown dynamics type: %d", d->dynamics); return -1; }
+  if (d->dynamics < 0 || d->dynamics > 4) { pl_set_error("Unknown dynamics type: %d", d->dynamics); return -1; }
   if (d->dynamics == PL_DYN_WHOLE_BODY_RNEA && !d->include_acc) {
-    pl_set_error("whole_body_rnea requires include_acc=True on this path");
-    return -1;
-  }
-  if (d->dynamics == PL_DYN_WHOLE_BODY_ACC && !d->include_base) {
-    pl_set_error("whole_body_acc requires include_base=True on this path");
+    // a = (v_{i+1} - v_i) / dt (ocp_whole_body_rnea.py:183-191) couples the RNEA rows of
+    // node i to dv_{i+1}: not the stage-wise structure the block factor needs
+    pl_set_error("whole_body_rnea requires include_acc=True on this path (finite-difference accelerations "
+                 "couple the RNEA rows to the next node; the reference notes the same for Fatrop)");
     return -1;
   }
   if (d->dynamics == PL_DYN_CENTROIDAL_VEL && !d->include_base) {
@@ -944,6 +953,8 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   memset(&O, 0, sizeof(O));
   const PlModel& M = h.model;
   O.dyn = d->dynamics;
+  // whole_body_acc / centroidal_acc without the base in u share the ACCNB rows
+  if ((O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA) && !d->include_base) O.dyn = PL_DYN_ACCNB;
   O.N = d->nodes;
   O.nq = M.nq;
   O.nv = M.nv;
@@ -956,7 +967,8 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   const bool cv = (O.dyn == PL_DYN_CV);
   O.nx = cv ? 6 + M.nq : M.nq + M.nv;   // centroidal_vel: x = [h, q] (ocp_centroidal_vel.py:50-52)
   O.ndx = cv ? 6 + M.nv : 2 * M.nv;
-  O.na = (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC) ? M.nv : 0;
+  O.na = (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA) ? M.nv
+         : (O.dyn == PL_DYN_ACCNB ? M.nq - 7 : 0);
   O.tau_nodes = (O.dyn == PL_DYN_RNEA) ? d->tau_nodes : 0;
   O.mu = d->mu;
   for (int k = 0; k < 4; ++k) O.feet[k] = frame_ref(model, d->foot_frames[k]);
@@ -1701,7 +1713,8 @@ int cas_ready() {
 void cas_u_split(const pl_ocp* o, int& na, int& nf, int& nt) {
   const PlOcpConst& O = o->h.oc;
   if (O.dyn == PL_DYN_RNEA) { na = O.na; nf = O.nf; nt = O.nj; }
-  else if (O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CV) { na = O.nv; nf = O.nf; nt = O.nj; }
+  else if (O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA || O.dyn == PL_DYN_ACCNB) { na = O.na; nf = O.nf; nt = O.nj; }
+  else if (O.dyn == PL_DYN_CV) { na = O.nv; nf = O.nf; nt = O.nj; }
   else { na = 0; nf = O.nf; nt = O.nj; }
 }
 
@@ -1996,10 +2009,15 @@ extern "C" int retract_solution(const double** arg, double** res, casadi_int*, d
         for (int k = 0; k < nv; ++k) a[k] = (un[k] - v[k]) / dt;
         pl::dyn_eval(M, O, F0, PL_FN_BASE_ACC_CV, 0, q, v, a.data() + 6, f, a.data());
       } break;
+      case PL_DYN_ACCNB:  // a = [base_acc_dynamics(q, v, a_j, f), a_j] (ocp_whole_body_acc.py:124-135)
+        for (int k = 0; k < nj; ++k) a[6 + k] = u[k];
+        pl::dyn_eval(M, O, F0, PL_FN_BASE_ACC_WB, 0, q, v, u, f, a.data());
+        break;
       default:
         for (int k = 0; k < nv; ++k) a[k] = u[k];
     }
-    if (O.dyn == PL_DYN_ACC || cv) pl::dyn_eval(M, O, F0, PL_FN_RNEA, 0, q, v, a.data(), f, tau.data());
+    if (O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA || O.dyn == PL_DYN_ACCNB || cv)
+      pl::dyn_eval(M, O, F0, PL_FN_RNEA, 0, q, v, a.data(), f, tau.data());
     // CasADi dense matrices are column-major: element (row i, col k) at k * S + i
     if (res[0]) for (int k = 0; k < nq; ++k) res[0][k * S + i] = q[k];
     if (res[1]) for (int k = 0; k < nv; ++k) res[1][k * S + i] = v[k];

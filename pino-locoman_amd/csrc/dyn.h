@@ -23,7 +23,7 @@
 namespace pl {
 
 // Function codes: PL_FN_* of include/pinoloco.h (the ABI numbers them).
-#define PL_FN_COUNT 19
+#define PL_FN_COUNT 20
 
 // Output length of one sample.
 PL_HD int dyn_out_len(const PlModel& M, int fn) {
@@ -46,7 +46,7 @@ PL_HD void dyn_in_len(const PlModel& M, int fn, int nf, int* len) {
   const int nq = M.nq, nv = M.nv, nj = nq - 7;
   for (int k = 0; k < 4; ++k) len[k] = 0;
   switch (fn) {
-    case PL_FN_RNEA: case PL_FN_GAPS_WB: len[0] = nq; len[1] = nv; len[2] = nv; len[3] = nf; break;
+    case PL_FN_RNEA: case PL_FN_GAPS_WB: case PL_FN_GAPS_CA: len[0] = nq; len[1] = nv; len[2] = nv; len[3] = nf; break;
     case PL_FN_ABA: case PL_FN_BASE_ACC_WB: case PL_FN_BASE_ACC_CV:
       len[0] = nq; len[1] = nv; len[2] = nj; len[3] = nf; break;
     case PL_FN_FRAME_POS: case PL_FN_CRBA: case PL_FN_FRAME_JAC: case PL_FN_CMAP: case PL_FN_COM: len[0] = nq; break;
@@ -285,6 +285,12 @@ PL_HD void dyn_eval(const PlModel& M, const PlOcpConst& O, const PlFrameRef& F, 
     case PL_FN_COM_DYN: {
       double hg[6];
       centroidal_full(M, O, in0, nullptr, in1, hg, out);
+    } break;
+    case PL_FN_GAPS_CA: {  // A a + dA v - dh (dynamics_centroidal_acc.py:92-119)
+      double rate[6], hg[6], hd[6];
+      momentum_rate(M, in0, in1, in2, rate);
+      centroidal_full(M, O, in0, nullptr, in3, hg, hd);
+      for (int k = 0; k < 6; ++k) out[k] = rate[k] - M.total_mass * hd[k];
     } break;
     case PL_FN_GAPS_CV: {
       double hd[6];

@@ -50,7 +50,11 @@ struct PlFrameRef {
   double p[3];
 };
 
-enum { PL_DYN_RNEA = 0, PL_DYN_ACC = 1, PL_DYN_ABA = 2, PL_DYN_CV = 3 };
+// Row-code dynamics kinds.  0-4 are also the public pl_ocp_desc codes (include_base
+// true); PL_DYN_ACCNB is internal: whole_body_acc and centroidal_acc with
+// include_base = False (u = [a_j | f], the base acceleration solved from the 6 base
+// equations), which share their rows.
+enum { PL_DYN_RNEA = 0, PL_DYN_ACC = 1, PL_DYN_ABA = 2, PL_DYN_CV = 3, PL_DYN_CA = 4, PL_DYN_ACCNB = 5 };
 
 // Row-block kinds, emitted per node in the reference's subject_to order
 // (optimization/ocp.py:103-190 + setup_dynamics_constraints of each subclass).
@@ -73,6 +77,7 @@ enum {
   PL_RB_CV_DYNH,      // dh_{i+1} == dh_i + h_dot(q, f) dt         (ocp_centroidal_vel.py:100)
   PL_RB_CV_DYNQ,      // dq_{i+1} == dq_i + v dt, v = u[:nv]       (ocp_centroidal_vel.py:101)
   PL_RB_CV_GAP,       // A(q) v - m h == 0                         (ocp_centroidal_vel.py:103-106)
+  PL_RB_CA_GAP,       // A a + dA v - dh(q, f) == 0               (ocp_centroidal_acc.py:107-109)
   PL_RB_COUNT
 };
 

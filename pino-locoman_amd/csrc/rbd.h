@@ -322,9 +322,36 @@ template <class S> struct RevQArr {  // same interface over a full q array
 //   q, v, a: full configuration / velocity / acceleration (a unused if !want_tau)
 //   forces: 3 * nee world-frame forces (FR, FL, RR, RL[, ee])
 //   qb: free-flyer q[0..7); qrev(k): revolute coordinate q[k]; v[k]: velocity
-template <class S, class QR, class VA, class InA, class InF>
+// Composite-body sums of tree_pass (kComp): about the root origin p0, world axes,
+//   comp[6..8]  = sum_j m_j (c_j - p0),
+//   comp[9..14] = sum_j R_j I_c,j R_j^T + m_j (|r_j|^2 1 - r_j r_j^T)  (xx xy xz yy yz zz),
+// and comp[0..5] = the total body wrench sum_j X_j^* f_j at the world origin (world
+// axes; gravity enters through the base acceleration, contact forces subtracted).
+template <class S>
+PL_HD void comp_add(S* comp, double m, const double* lever, const double* Ic, const S* oR, const S* op, const S* p0) {
+  S lw[3];
+  matvec(oR, lever, lw);
+  S r[3];
+  for (int k = 0; k < 3; ++k) r[k] = op[k] + lw[k] - p0[k];
+  for (int k = 0; k < 3; ++k) comp[6 + k] += m * r[k];
+  S T[9];  // R Ic
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) T[3 * i + j] = oR[3 * i] * Ic[j] + oR[3 * i + 1] * Ic[3 + j] + oR[3 * i + 2] * Ic[6 + j];
+  const S rr = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+  constexpr int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+  for (int q = 0; q < 6; ++q) {
+    const int i = II[q], j = JJ[q];
+    S t = T[3 * i] * oR[3 * j] + T[3 * i + 1] * oR[3 * j + 1] + T[3 * i + 2] * oR[3 * j + 2];
+    t = t - m * (r[i] * r[j]);
+    if (i == j) t = t + m * rr;
+    comp[9 + q] += t;
+  }
+}
+
+template <class S, class QR, class VA, class InA, class InF, bool kComp = false>
 PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const QR& qrev, const VA& v, const InA& a,
-                     const InF& forces, bool want_tau, bool want_vel, NodeKin<S>& out) {
+                     const InF& forces, bool want_tau, bool want_vel, NodeKin<S>& out, S* comp = nullptr,
+                     std::integral_constant<bool, kComp> = {}) {
   // ---- root (free-flyer, joint 1)
   S R0[9];
   quat_to_R(qb + 3, R0);
@@ -353,6 +380,10 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
     S fa[3];
     cross3(pf, fl, fa);
     for (int k = 0; k < 3; ++k) { f1[k] -= fl[k]; f1[3 + k] -= fa[k]; }
+  }
+  if constexpr (kComp) {
+    for (int k = 0; k < 15; ++k) comp[k] = S(0.0);
+    comp_add(comp, M.mass[1], M.lever[1], M.Ic[1], R0, p0, p0);
   }
   // world-frame force accumulated from every chain (at world origin)
   S Fw[6];
@@ -394,6 +425,7 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
       matmul3(oR, Rl, oRj);
       matvec(oR, pl, tmp3);
       for (int k = 0; k < 3; ++k) opj[k] = op[k] + tmp3[k];
+      if constexpr (kComp) comp_add(comp, M.mass[j], M.lever[j], M.Ic[j], oRj, opj, p0);
       if (want_tau) {
         S aj[6];
         act_inv_motion(Rl, pl, pa, aj);
@@ -478,6 +510,11 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
     }
   }
   if (want_tau) {
+    if constexpr (kComp) {  // total wrench at the world origin: chains + the root body's own
+      S f1w[6];
+      act_force(R0, p0, f1, f1w);
+      for (int k = 0; k < 6; ++k) comp[k] = Fw[k] + f1w[k];
+    }
     // root: f1 += actInv_force(M0, Fw)  (world -> root-local)
     S d[3], pxf[3];
     cross3(p0, Fw, pxf);
@@ -612,6 +649,64 @@ PL_HD void centroidal_pass(const PlModel& M, const PlOcpConst& O, const S* qb, c
       for (int k = 0; k < 3; ++k) { dp[k] += f[k]; dl[k] += t[k]; }
     }
     for (int k = 0; k < 3; ++k) { hdot[k] = dp[k] * (1.0 / m); hdot[3 + k] = dl[k] * (1.0 / m); }
+  }
+}
+
+// ---------------------------------------------------------------- base from the base rows
+// The 6 base equations of the floating base, from tree_pass's composite sums:
+//   M_bb = [[m 1, -[h]x], [[h]x, I]] in the root frame (h = R0^T sum m r, I = R0^T I_p0 R0);
+//   base_solve: a_b = -M_bb^-1 tau_b (tau_b = RNEA base rows at a_b = 0), by the Schur
+//   complement on the rotational block (the inertia about the CoM, 3x3 Cholesky).
+template <class S>
+PL_HD void base_solve(double m, const S* R0, const S* comp, const S* tau_b, S* a_b) {
+  S h[3], Iw[9];
+  mattvec(R0, comp + 6, h);
+  const S* c = comp + 9;
+  const S Ip[9] = {c[0], c[1], c[2], c[1], c[3], c[4], c[2], c[4], c[5]};
+  // I = R0^T Ip R0
+  S T[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) T[3 * i + j] = R0[i] * Ip[j] + R0[3 + i] * Ip[3 + j] + R0[6 + i] * Ip[6 + j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Iw[3 * i + j] = T[3 * i] * R0[j] + T[3 * i + 1] * R0[3 + j] + T[3 * i + 2] * R0[6 + j];
+  // Ic = I + (h h^T - |h|^2 1) / m ; rhs = -tau_ang + h x tau_lin / m
+  const double im = 1.0 / m;
+  const S hh = h[0] * h[0] + h[1] * h[1] + h[2] * h[2];
+  S A[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) A[3 * i + j] = Iw[3 * i + j] + (h[i] * h[j] - (i == j ? hh : S(0.0))) * im;
+  S hxt[3];
+  cross3(h, tau_b, hxt);
+  S r[3];
+  for (int k = 0; k < 3; ++k) r[k] = hxt[k] * im - tau_b[3 + k];
+  // Cholesky A = L L^T
+  const S l00 = sqrt_s(A[0]);
+  const S l10 = A[3] / l00, l20 = A[6] / l00;
+  const S l11 = sqrt_s(A[4] - l10 * l10);
+  const S l21 = (A[7] - l20 * l10) / l11;
+  const S l22 = sqrt_s(A[8] - l20 * l20 - l21 * l21);
+  const S y0 = r[0] / l00, y1 = (r[1] - l10 * y0) / l11, y2 = (r[2] - l20 * y0 - l21 * y1) / l22;
+  const S w2 = y2 / l22, w1 = (y1 - l21 * w2) / l11, w0 = (y0 - l10 * w1 - l20 * w2) / l00;
+  const S wa[3] = {w0, w1, w2};
+  S hxw[3];
+  cross3(h, wa, hxw);
+  for (int k = 0; k < 3; ++k) {
+    a_b[k] = (hxw[k] - tau_b[k]) * im;
+    a_b[3 + k] = wa[k];
+  }
+}
+
+// A a + dA v - dh(q, f) (DynamicsCentroidalAcc.dynamics_gaps): the total wrench of
+// tree_pass moved from the world origin to the CoM, c = p0 + sum m r / m.
+template <class S>
+PL_HD void centroidal_gap(double m, const S* p0, const S* comp, S* gap) {
+  S c[3];
+  for (int k = 0; k < 3; ++k) c[k] = p0[k] + comp[6 + k] * (1.0 / m);
+  S cxf[3];
+  cross3(c, comp, cxf);
+  for (int k = 0; k < 3; ++k) {
+    gap[k] = comp[k];
+    gap[3 + k] = comp[3 + k] - cxf[k];
   }
 }
 

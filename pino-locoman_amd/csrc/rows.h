@@ -41,9 +41,11 @@ PL_HD double spline_vel_z(double phase, double period, double h_max, double v_lo
 PL_HD int node_type(const PlOcpConst& O, int i) { return i == 0 ? 0 : (i < O.tau_nodes ? 1 : 2); }
 PL_HD int node_nu(const PlOcpConst& O, int i) {
   if (O.dyn == PL_DYN_RNEA) return O.na + O.nf + (i < O.tau_nodes ? O.nj : 0);
-  if (O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CV) return O.nv + O.nf;
+  if (O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA || O.dyn == PL_DYN_ACCNB) return O.na + O.nf;
+  if (O.dyn == PL_DYN_CV) return O.nv + O.nf;
   return O.nj + O.nf;
 }
+
 
 // Geometric step size dt_i (ocp.py:71-74).
 PL_HD double node_dt(const PlOcpConst& O, const double* p, int i) {
@@ -79,6 +81,13 @@ template <class S> PL_HD VecIn<S> sub_in(const VecIn<S>& a, int off) {
   return r;
 }
 
+// Acceleration input of the tree pass for the include_base = False variants: the base
+// acceleration zeroed (the base rows at a_b = 0 give the right-hand side of the base solve).
+template <class S> struct ZeroBaseAcc {
+  VecIn<S> aj;
+  PL_HD S operator[](int k) const { return k < 6 ? S(0.0) : aj[k - 6]; }
+};
+
 // kstore: caller storage for the run-time indexed kinematic outputs (NodeKin,
 // PL_KIN_STORE entries spaced by kstride).
 // kvals (Dual only): a shared value store for the kinematic outputs (NodeKin<Dual>);
@@ -104,7 +113,11 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
     if constexpr (CV) return u;
     else return VelAcc<S, VecIn<S>>{xi + nq, sub_in(dx, nv)};
   }();
-  const int f_off = (DYN == PL_DYN_RNEA) ? O.na : ((DYN == PL_DYN_ACC || CV) ? nv : nj);
+  // acc family: whole_body_acc (ACC), centroidal_acc (CA), their include_base = False form (ACCNB)
+  constexpr bool ACCF = (DYN == PL_DYN_ACC || DYN == PL_DYN_CA || DYN == PL_DYN_ACCNB);
+  constexpr bool NB = (DYN == PL_DYN_ACCNB);
+  constexpr bool COMP = (DYN == PL_DYN_CA || DYN == PL_DYN_ACCNB);
+  const int f_off = (DYN == PL_DYN_RNEA || ACCF) ? O.na : (CV ? nv : nj);
   const VecIn<S> a = u;                                   // rnea / acc: a = u[0:nv]
   const VecIn<S> forces = sub_in(u, f_off);
   const VecIn<S> tau_j = sub_in(u, DYN == PL_DYN_RNEA ? O.na + O.nf : 0);
@@ -128,7 +141,7 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
     kin.store = kstore;
     kin.stride = kstride;
   }
-  constexpr bool want_tau = (DYN == PL_DYN_RNEA || DYN == PL_DYN_ACC);
+  constexpr bool want_tau = (DYN == PL_DYN_RNEA || ACCF);
   // A Jacobian column seeded on dx_{i+1}, or (rnea) on tau_j, has a zero tangent in the
   // tree pass and the ABA: every row that reads them then has a zero derivative, so
   // the pass is skipped (its values are not emitted for such a column's pattern).
@@ -143,11 +156,36 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
     tree = !(seed_dxn || seed_tau || seed_h || seed_f);
     cen = CV && !(seed_dxn || seed_h);
   }
+  S comp[COMP ? 15 : 1];
   if (tree && (want_tau || state_rows)) {
-    tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin);
+    if constexpr (NB) {
+      tree_pass<S>(M, O, qb, qrev, vel, ZeroBaseAcc<S>{a}, forces, want_tau, state_rows, kin, comp, std::true_type{});
+    } else if constexpr (COMP) {
+      tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin, comp, std::true_type{});
+    } else {
+      tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin);
+    }
   } else {  // a skipped pass leaves zero (value and tangent) kinematic outputs
     for (int k = 0; k < PL_KIN_STORE_DUAL; ++k) kin.clear(k);
     for (int k = 0; k < 3; ++k) kin.arm_vel[k] = S(0.0);
+    for (int k = 0; k < 6; ++k) kin.tau[k] = S(0.0);
+    if constexpr (COMP)
+      for (int k = 0; k < 15; ++k) comp[k] = S(0.0);
+  }
+  // acc family: the base acceleration (include_base = False) or the centroidal gap
+  S abase[NB ? 6 : 1], cgap[DYN == PL_DYN_CA ? 6 : 1];
+  if constexpr (COMP) {
+    if (tree) {
+      S R0[9];
+      quat_to_R(qb + 3, R0);
+      if constexpr (NB) base_solve(M.total_mass, R0, comp, kin.tau, abase);
+      else centroidal_gap(M.total_mass, qb, comp, cgap);
+    } else {
+      for (int k = 0; k < 6; ++k) {
+        if constexpr (NB) abase[k] = S(0.0);
+        else cgap[k] = S(0.0);
+      }
+    }
   }
   S hg[CV ? 6 : 1], hdot[CV ? 6 : 1];
   if constexpr (CV) {
@@ -185,6 +223,7 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
         for (int r = 0; r < nv; ++r) {
           S ar;
           if constexpr (DYN == PL_DYN_ABA) ar = aba_a[r];
+          else if constexpr (NB) ar = r < 6 ? abase[r] : a[r - 6];
           else ar = a[r];
           emit(dxn[nv + r] - (dx[nv + r] + ar * dt), 0.0, 0.0);
         }
@@ -246,6 +285,10 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
       case PL_RB_CV_GAP:
         if constexpr (CV)
           for (int r = 0; r < 6; ++r) emit(hg[r] - M.total_mass * (xi[r] + dx[r]), 0.0, 0.0);
+        break;
+      case PL_RB_CA_GAP:
+        if constexpr (DYN == PL_DYN_CA)
+          for (int r = 0; r < 6; ++r) emit(cgap[r], 0.0, 0.0);
         break;
     }
   }

@@ -20,7 +20,7 @@ from . import _lib
 
 FN = dict(rnea=0, aba=1, frame_pos=2, frame_vel=3, gaps_wb=4, base_acc_wb=5, com_dyn=6, base_vel_cv=7,
           base_acc_cv=8, gaps_cv=9, crba=10, nle=11, frame_jac=12, cmap=13, com=14, integrate_wb=15,
-          difference_wb=16, integrate_cv=17, difference_cv=18)
+          difference_wb=16, integrate_cv=17, difference_cv=18, gaps_ca=19)
 
 
 class _DynHandle:
@@ -178,5 +178,18 @@ class DynamicsCentroidalVel(Dynamics):
         return self._fn("gaps_cv")
 
 
+class DynamicsCentroidalAcc(Dynamics):
+    """dynamics/dynamics_centroidal_acc.py: x = [q, v]; the base equations in centroidal form."""
+
+    def base_acc_dynamics(self, ext_force_frame=None):
+        """(q, v, a_j, forces) -> a_b = A_b^-1 (dh - dA v - A_j a_j) (pinocchio dccrba)."""
+        return self._fn("base_acc_cv", ext_force_frame)
+
+    def dynamics_gaps(self, ext_force_frame=None):
+        """(q, v, a, forces) -> A a + dA v - dh (6)."""
+        return self._fn("gaps_ca", ext_force_frame)
+
+
 DYNAMICS_CLASSES = {"whole_body_rnea": DynamicsWholeBodyTorque, "whole_body_aba": DynamicsWholeBodyTorque,
-                    "whole_body_acc": DynamicsWholeBodyAcc, "centroidal_vel": DynamicsCentroidalVel}
+                    "whole_body_acc": DynamicsWholeBodyAcc, "centroidal_vel": DynamicsCentroidalVel,
+                    "centroidal_acc": DynamicsCentroidalAcc}

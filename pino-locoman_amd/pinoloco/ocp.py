@@ -19,7 +19,8 @@ from . import _lib
 from .dynamics import DYNAMICS_CLASSES, Dynamics  # noqa: F401  (Dynamics: plugin base class)
 from .gait import horizon_dts
 
-DYN_CODES = {"whole_body_rnea": 0, "whole_body_acc": 1, "whole_body_aba": 2, "centroidal_vel": 3}
+DYN_CODES = {"whole_body_rnea": 0, "whole_body_acc": 1, "whole_body_aba": 2, "centroidal_vel": 3,
+             "centroidal_acc": 4}
 GAIT_CODES = {"trot": 0, "walk": 1, "stand": 2}
 SOLVER_CODES = {"osqp": 0, "fatrop": 1}
 
@@ -50,8 +51,9 @@ STATUS_NAMES = {1: "solved", 2: "solved inaccurate", -2: "maximum iterations rea
 class Layout:
     """Variable / parameter bookkeeping (setup_variables / setup_parameters)."""
 
-    def __init__(self, robot, dynamics, nodes, tau_nodes=3):
+    def __init__(self, robot, dynamics, nodes, tau_nodes=3, include_base=True):
         self.dynamics = dynamics
+        self.include_base = include_base
         self.N = nodes
         self.nq, self.nv, self.nj, self.nf = robot.nq, robot.nv, robot.nj, robot.nf
         self.nx = self.nq + self.nv
@@ -69,11 +71,13 @@ class Layout:
             self.na = nv
             self.nu = [nv + nf + nj] * tau_nodes + [nv + nf] * (nodes - tau_nodes)
             self.f_idx, self.tau_idx = nv, nv + nf
-        elif dynamics == "whole_body_acc":
+        elif dynamics in ("whole_body_acc", "centroidal_acc"):
+            # u = [a | f] or, without the base, [a_j | f] (ocp_whole_body_acc.py:56-63,
+            # ocp_centroidal_acc.py:15-19, 57-59)
             self.tau_nodes = 0
-            self.na = nv
-            self.nu = [nv + nf] * nodes
-            self.f_idx, self.tau_idx = nv, nv + nf
+            self.na = nv if include_base else nj
+            self.nu = [self.na + nf] * nodes
+            self.f_idx, self.tau_idx = self.na, self.na + nf
         elif dynamics == "whole_body_aba":
             self.tau_nodes = 0
             self.na = 0
@@ -134,8 +138,8 @@ def default_weights(robot, dynamics, layout):
         R = np.array([1] * robot.nv + [1e-3] * nf, float)
     elif dynamics == "whole_body_rnea":
         R = np.array([1e-3] * layout.na + [1e-3] * nf + [1e-4] * nj, float)
-    elif dynamics == "whole_body_acc":
-        R = np.array([1e-3] * robot.nv + [1e-3] * nf, float)
+    elif dynamics in ("whole_body_acc", "centroidal_acc"):
+        R = np.array([1e-3] * layout.na + [1e-3] * nf, float)
     else:
         R = np.array([1e-3] * nj + [1e-3] * nf, float)
     W = np.zeros(nj)
@@ -153,7 +157,7 @@ class BatchedOCP:
         self.robot = robot
         self.dynamics = dynamics
         self.batch = batch
-        self.layout = Layout(robot, dynamics, nodes, tau_nodes)
+        self.layout = Layout(robot, dynamics, nodes, tau_nodes, include_base)
         self.model_h = ModelCache.get(robot.model)
         s = dict(OSQP_SETTINGS)
         if osqp_settings:
@@ -393,7 +397,7 @@ class OCP:
         self.mass = robot.mass
         self.dynamics = dynamics
         self.dyn = DYNAMICS_CLASSES[dynamics](robot, device=device)
-        self.layout = Layout(robot, dynamics, nodes, tau_nodes)
+        self.layout = Layout(robot, dynamics, nodes, tau_nodes, include_base)
         L = self.layout
         self.nx, self.ndx_opt, self.nu_opt = L.nx, L.ndx, L.nu
         self.f_idx, self.tau_idx = L.f_idx, L.tau_idx
@@ -440,7 +444,9 @@ class OCP:
         f = self._f_des()
         if self.dynamics == "whole_body_rnea":
             return np.concatenate([np.zeros(self.na_opt), f, np.zeros(self.nj)])
-        if self.dynamics in ("whole_body_acc", "centroidal_vel"):
+        if self.dynamics in ("whole_body_acc", "centroidal_acc"):
+            return np.concatenate([np.zeros(self.na_opt), f])
+        if self.dynamics == "centroidal_vel":
             return np.concatenate([np.zeros(self.nv), f])
         return np.concatenate([np.zeros(self.nj), f])
 
@@ -554,6 +560,12 @@ class OCP:
                     self.forces_sol.append(forces)
                     ext = self.ext_force_frame
                     self.a_sol.append(self.dyn.aba_dynamics(ext)(xs[:self.nq], xs[self.nq:], tau_j, forces))
+                elif self.dynamics in ("whole_body_acc", "centroidal_acc") and not self.include_base:
+                    # a = [base_acc_dynamics(q, v, a_j, f), a_j] (ocp_whole_body_acc.py:124-135)
+                    a_j, forces = u[:self.na_opt], u[self.f_idx:]
+                    a_b = self.dyn.base_acc_dynamics(self.ext_force_frame)(xs[:self.nq], xs[self.nq:], a_j, forces)
+                    self.a_sol.append(np.concatenate([a_b, a_j]))
+                    self.forces_sol.append(forces)
                 else:
                     self.a_sol.append(u[:self.na_opt])
                     self.forces_sol.append(u[self.f_idx:self.tau_idx] if self.tau_idx else u[self.f_idx:])
@@ -625,17 +637,20 @@ class OCPCentroidalVel(OCP):
             self.q_sol.append(integ(x_init, DX[-1])[6:])
 
 
-class _CentroidalAcc:
-    def __init__(self, *args, **kwargs):
-        raise NotImplementedError("centroidal_acc (ocp_centroidal_acc.py) is not on the MI355X path: no BASELINE "
-                                  "config uses it (SURVEY.md section 8f, row 3)")
+class OCPCentroidalAcc(OCP):
+    """ocp_centroidal_acc.py: the whole-body state and inputs of OCPWholeBodyAcc with the base
+    equations in centroidal form: the gap A a + dA v - dh (include_base) or the base
+    acceleration A_b^-1 (dh - dA v - A_j a_j) (pinocchio computeCentroidalMap / dccrba)."""
+
+    def __init__(self, robot, solver, nodes, include_base=False):
+        super().__init__(robot, solver, nodes, "centroidal_acc", include_base=include_base)
 
 
 def make_ocp(dynamics, default_args, **kwargs):
     """ocp_factory.py:8-27."""
     ocp_classes = {
         "centroidal_vel": OCPCentroidalVel,
-        "centroidal_acc": _CentroidalAcc,
+        "centroidal_acc": OCPCentroidalAcc,
         "whole_body_acc": OCPWholeBodyAcc,
         "whole_body_aba": OCPWholeBodyABA,
         "whole_body_rnea": OCPWholeBodyRNEA,

@@ -60,6 +60,16 @@ SQP_CONFIGS = [
      {"eps_abs": 1e-5, "eps_rel": 1e-5, "max_iter": 1000}, 0),
     ("go2_rnea_n20_eps6", "go2", "whole_body_rnea", 20, [("stand",)], 1, "stand",
      {"eps_abs": 1e-6, "eps_rel": 1e-6, "max_iter": 2000}, 0),
+    # whole_body_acc / centroidal_acc without the base in u (ocp_whole_body_acc.py:124-135,
+    # ocp_centroidal_acc.py:123-134) and centroidal_acc's gap A a + dA v - dh
+    ("go2_acc_nb_n20", "go2", "whole_body_acc", 20, [("syn", k) for k in range(4)], 3, "trot", {}, 1,
+     {"include_base": False}),
+    ("go2_ca_n20", "go2", "centroidal_acc", 20, [("syn", k) for k in range(4)], 3, "trot", {}, 1,
+     {"include_base": True}),
+    ("go2_ca_nb_n20", "go2", "centroidal_acc", 20, [("syn", k) for k in range(2)], 1, "trot", {}, 1,
+     {"include_base": False}),
+    ("b2g_ca_n50", "b2g", "centroidal_acc", 50, [("syn", 0)], 1, "trot", {}, 1, {"include_base": True}),
+    ("b2g_acc_nb_n50", "b2g", "whole_body_acc", 50, [("syn", 0)], 1, "trot", {}, 1, {"include_base": False}),
 ]
 
 # Interior-point (Fatrop branch) fixtures: name, robot, dynamics, N, problems, closed-loop
@@ -179,10 +189,11 @@ def rbd_fixture(rname, seed=7, count=3):
     np.savez_compressed(os.path.join(HERE, f"rbd_{rname}.npz"), **arrs)
 
 
-def sqp_fixture(name, rname, dyn, N, problems, loop_steps, gait, osqp, njac):
+def sqp_fixture(name, rname, dyn, N, problems, loop_steps, gait, osqp, njac, kw=None):
+    kw = kw or {}
     R = robots.ROBOTS[rname]()
     R.set_gait_sequence(gait, 0.8)
-    lay = Layout(R, dyn, N)
+    lay = Layout(R, dyn, N, **kw)
     settings = dict(REFERENCE_SETTINGS)
     settings.update(osqp)
     B = len(problems)
@@ -190,12 +201,13 @@ def sqp_fixture(name, rname, dyn, N, problems, loop_steps, gait, osqp, njac):
     for b, spec in enumerate(problems):
         P[b], X[b], XS[b], T0[b] = make_problem(R, lay, dyn, N, spec)
     rec = {"P": P, "X": X, "XS": XS, "T0": T0, "gait": np.array(gait), "kinds": np.array([s[0] for s in problems]),
-           "osqp_eps": np.array([settings["eps_abs"], settings["eps_rel"]]), "osqp_max_iter": settings["max_iter"]}
+           "osqp_eps": np.array([settings["eps_abs"], settings["eps_rel"]]), "osqp_max_iter": settings["max_iter"],
+           "include_base": int(kw.get("include_base", True))}
     keys = ("g", "lbg", "ubg", "grad", "f", "J_indptr", "J_indices", "J_data", "dx", "x_new", "xs_next", "status",
             "iters", "accepted", "alpha", "branch", "trials", "viol_max", "quat_trace_le0")
     per = {k: [] for k in keys}
     for b in range(B):
-        o = OracleOCP(R, dyn, N, osqp_settings=settings)
+        o = OracleOCP(R, dyn, N, osqp_settings=settings, **kw)
         x, p = X[b], P[b]
         g, lbg, ubg = o.eval_g(x, p)
         f, grad = o.f_and_grad(x, p)
@@ -221,7 +233,7 @@ def sqp_fixture(name, rname, dyn, N, problems, loop_steps, gait, osqp, njac):
     # closed loop of problem 0 (run_mpc.py:127-143): per step gait at t0 + k dt_min,
     # warm start, one SQP iteration, x <- integrate(x, DX[1]); per-step solver stats
     if loop_steps > 1:
-        o = OracleOCP(R, dyn, N, osqp_settings=settings)
+        o = OracleOCP(R, dyn, N, osqp_settings=settings, **kw)
         xs, x = XS[0].copy(), X[0].copy()
         states, u0s, lst = [], [], []
         for k in range(loop_steps):

@@ -43,6 +43,8 @@ extern "C" int th_node_rows(const void* model, const void* oc, int i, const doub
     case PL_DYN_RNEA: return run<PL_DYN_RNEA>(M, O, i, p, dx, u, dxn, seed, g, lb, ub, tan);
     case PL_DYN_ACC: return run<PL_DYN_ACC>(M, O, i, p, dx, u, dxn, seed, g, lb, ub, tan);
     case PL_DYN_CV: return run<PL_DYN_CV>(M, O, i, p, dx, u, dxn, seed, g, lb, ub, tan);
+    case PL_DYN_CA: return run<PL_DYN_CA>(M, O, i, p, dx, u, dxn, seed, g, lb, ub, tan);
+    case PL_DYN_ACCNB: return run<PL_DYN_ACCNB>(M, O, i, p, dx, u, dxn, seed, g, lb, ub, tan);
     default: return run<PL_DYN_ABA>(M, O, i, p, dx, u, dxn, seed, g, lb, ub, tan);
   }
 }

@@ -56,6 +56,17 @@ def check_surface(name, device):
     _close(cv.dynamics_gaps()(G["h"], q, v), G["gaps_cv"])
     _close(cv.base_vel_dynamics()(G["h"], q, G["v_j"]), G["base_vel_cv"], 1e-10)
     _close(cv.base_acc_dynamics(ext)(q, v, G["a_j"], f), G["base_acc_cv"], 1e-10)
+    # DynamicsCentroidalAcc (dynamics_centroidal_acc.py): its base_acc equals the centroidal_vel
+    # one; the gap A a + dA v - dh against the oracle (computeCentroidalMap + dccrba restated)
+    from oracle import rbd as orbd
+    from pinoloco.dynamics import DynamicsCentroidalAcc
+    ca = DynamicsCentroidalAcc(R, device=device)
+    Mo = orbd.ModelArrays(R.model)
+    fr = list(G["frames"])
+    want = np.stack([orbd.centroidal_map(Mo, q[b]) @ a[b] + orbd.dccrba_v(Mo, q[b], v[b])
+                     - orbd.com_dynamics(Mo, fr, q[b], f[b], R.mass, scale=False) for b in range(len(q))])
+    _close(ca.dynamics_gaps(ext)(q, v, a, f), want, 1e-10)
+    _close(ca.base_acc_dynamics(ext)(q, v, G["a_j"], f), G["base_acc_cv"], 1e-10)
     # single points give 1-D results; state maps round-trip
     x = np.concatenate([q[0], v[0]])
     dx = np.concatenate([G["dq"][0], v[1]])

@@ -31,6 +31,11 @@ CONFIGS = [("go2_rnea_n20", "go2", "whole_body_rnea", 20), ("go2_cv_n20", "go2",
 # edge-case fixtures (tests/golden/make_golden.py): gaits, quaternion branch, OSQP
 # termination at 25/50/75/100, infeasible QPs, line-search branches 2 and 3
 EDGE = [(f"go2_rnea_n20_{k}", "go2", "whole_body_rnea", 20) for k in ("walk", "stand", "eps2", "infeas", "eps5", "eps6")]
+# acc family beyond the BASELINE configs: whole_body_acc / centroidal_acc with include_base
+# False (base acceleration from the base equations) and centroidal_acc's gap A a + dA v - dh
+ACCF = [("go2_acc_nb_n20", "go2", "whole_body_acc", 20), ("go2_ca_n20", "go2", "centroidal_acc", 20),
+        ("go2_ca_nb_n20", "go2", "centroidal_acc", 20), ("b2g_ca_n50", "b2g", "centroidal_acc", 50),
+        ("b2g_acc_nb_n50", "b2g", "whole_body_acc", 50)]
 
 
 def _rel(a, b):
@@ -50,14 +55,15 @@ def _batched(rname, dyn, N, G, B=None):
     settings, gait = _settings(G)
     R = make_robot(rname, gait)
     B = B or G["P"].shape[0]
-    bo = BatchedOCP(R, dyn, N, batch=B, device=0, osqp_settings=settings, gait_type=gait)
+    ib = bool(int(G["include_base"])) if "include_base" in G else True
+    bo = BatchedOCP(R, dyn, N, batch=B, device=0, osqp_settings=settings, gait_type=gait, include_base=ib)
     bo.set_params(G["P"][:B])
     bo.set_x(G["X"][:B])
     bo.init_solver()
     return R, bo
 
 
-@pytest.mark.parametrize("name,rname,dyn,N", CONFIGS)
+@pytest.mark.parametrize("name,rname,dyn,N", CONFIGS + ACCF)
 def test_eval_sqp_data_matches_golden(name, rname, dyn, N):
     G = golden(f"sqp_{name}.npz")
     R, bo = _batched(rname, dyn, N, G)
@@ -79,7 +85,7 @@ def test_eval_sqp_data_matches_golden(name, rname, dyn, N):
     bo.close()
 
 
-@pytest.mark.parametrize("name,rname,dyn,N", CONFIGS + EDGE)
+@pytest.mark.parametrize("name,rname,dyn,N", CONFIGS + EDGE + ACCF)
 def test_sqp_step_matches_golden(name, rname, dyn, N):
     """One SQP iteration per problem: solver outcome exact, step <= 1e-8; the max
     violation at the returned point <= 1e-10 against the oracle's metric at the same
@@ -90,7 +96,7 @@ def test_sqp_step_matches_golden(name, rname, dyn, N):
     st = bo.solve()
     dx = bo.get_step()
     xn = bo.get_x()
-    o = OracleOCP(R, dyn, N)
+    o = OracleOCP(R, dyn, N, include_base=bool(int(G["include_base"])) if "include_base" in G else True)
     for b in range(G["P"].shape[0]):
         assert st["status"][b] == G["status"][b], b
         assert st["admm_iters"][b] == G["iters"][b], b
@@ -130,7 +136,7 @@ def test_fixture_coverage():
     assert gaits == {"trot", "walk", "stand"} and trace > 0
 
 
-@pytest.mark.parametrize("name,rname,dyn,N", [CONFIGS[0], CONFIGS[1], EDGE[0], EDGE[1], EDGE[4]])
+@pytest.mark.parametrize("name,rname,dyn,N", [CONFIGS[0], CONFIGS[1], EDGE[0], EDGE[1], EDGE[4], ACCF[0], ACCF[1]])
 def test_device_mpc_loop_matches_oracle_loop(name, rname, dyn, N):
     """run_mpc.py:127-143 executed on the device (gait, x_init, warm start, solve,
     x <- integrate(x, DX[1])) vs the oracle's closed loop in the golden file: states
@@ -368,3 +374,25 @@ def test_casadi_external_functions_match_golden():
     assert np.array_equal(H.diagonal(), hd)
     casadi_ext.unbind()
     bo.close()
+
+
+def test_make_ocp_centroidal_acc_surface():
+    """make_ocp("centroidal_acc", include_base=False) (ocp_factory.py:9-15): the GPU solve of
+    the fixture problem, and the retract fills a = [base_acc_dynamics(q, v, a_j, f), a_j]
+    (ocp_centroidal_acc.py:123-134)."""
+    from pinoloco.ocp import OCP_ARGS, make_ocp
+    G = golden("sqp_go2_ca_nb_n20.npz")
+    R = make_robot("go2")
+    ocp = make_ocp("centroidal_acc", OCP_ARGS["centroidal_acc"], robot=R, solver="osqp", nodes=20, include_base=False)
+    ocp.param_vector = lambda: G["P"][0]
+    ocp._x_initial = G["X"][0].copy()
+    ocp.p["x_init"] = G["XS"][0]
+    ocp.init_solver()
+    x = ocp.solve()
+    assert ocp.stats["status"] == int(G["status"][0])
+    assert _rel(x, G["x_new"][0]) <= 2e-7
+    a0 = ocp.a_sol[0]
+    assert a0.shape == (R.nv,)
+    q0, v0 = ocp.q_sol[0], ocp.v_sol[0]
+    ab = ocp.dyn.base_acc_dynamics(R.ext_force_frame)(q0, v0, a0[6:], ocp.forces_sol[0])
+    assert np.abs(a0[:6] - ab).max() <= 1e-12 * max(1.0, np.abs(ab).max())

@@ -43,21 +43,28 @@ def _consts(bo):
     return mb, ob
 
 
-@pytest.mark.parametrize("rname,dyn,N,nodes_checked", [
-    ("go2", "whole_body_rnea", 20, None),
-    ("b2", "whole_body_aba", 40, [0, 1, 2, 3, 20, 39]),
-    ("b2g", "whole_body_acc", 50, [0, 1, 25, 49]),
-    ("b2g", "whole_body_rnea", 50, [0, 2, 3, 26, 49]),
-    ("go2", "centroidal_vel", 20, None),
+@pytest.mark.parametrize("rname,dyn,N,nodes_checked,kw", [
+    ("go2", "whole_body_rnea", 20, None, {}),
+    ("b2", "whole_body_aba", 40, [0, 1, 2, 3, 20, 39], {}),
+    ("b2g", "whole_body_acc", 50, [0, 1, 25, 49], {}),
+    ("b2g", "whole_body_rnea", 50, [0, 2, 3, 26, 49], {}),
+    ("go2", "centroidal_vel", 20, None, {}),
+    # ocp_whole_body_acc.py / ocp_centroidal_acc.py without the base in u, and the
+    # centroidal gap A a + dA v - dh
+    ("go2", "whole_body_acc", 20, [0, 1, 7, 19], {"include_base": False}),
+    ("b2g", "whole_body_acc", 50, [0, 30], {"include_base": False}),
+    ("go2", "centroidal_acc", 20, [0, 1, 7, 19], {"include_base": True}),
+    ("b2g", "centroidal_acc", 50, [0, 30], {"include_base": True}),
+    ("go2", "centroidal_acc", 20, [0, 12], {"include_base": False}),
 ])
-def test_node_rows_and_dual_jacobian(harness, rname, dyn, N, nodes_checked):
+def test_node_rows_and_dual_jacobian(harness, rname, dyn, N, nodes_checked, kw):
     from pinoloco.ocp import BatchedOCP
     from pinoloco.synthetic import build_batch
     R = make_robot(rname)
-    bo = BatchedOCP(R, dyn, N, batch=1, device=-1)
+    bo = BatchedOCP(R, dyn, N, batch=1, device=-1, **kw)
     mb, ob = _consts(bo)
-    o = OracleOCP(R, dyn, N)
-    lay, P, X, _, _ = build_batch(R, dyn, N, 1, 17)
+    o = OracleOCP(R, dyn, N, **kw)
+    lay, P, X, _, _ = build_batch(R, dyn, N, 1, 17, **kw)
     rng = np.random.default_rng(4)
     p = P[0].copy()
     x = X[0] + rng.normal(0, 0.05, o.n)
