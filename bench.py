@@ -169,7 +169,7 @@ def dry_run(args, world, rank):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=80)  # >= 10 s timed at the headline config
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1024, help="problems per GPU")
     ap.add_argument("--robot", default="b2g")
