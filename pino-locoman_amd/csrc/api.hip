@@ -1035,7 +1035,12 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   h.ip = PlIpSettings{1e-3, 1e-4, 1e-7, 1e-2, 1e-8, 1e-4, 10, 12, 2, 0};
   // ADMM sweep kernel: one wave per problem (k_admm); PL_ADMM_WAVES=2 selects the
   // two-waves-per-problem variant (k_admm2.hip; measured slower)
-  h.admm_waves = (getenv("PL_ADMM_WAVES") && atoi(getenv("PL_ADMM_WAVES")) == 2) ? 2 : 1;
+  // ADMM sweep: one wave per problem fills every SIMD once B >= 1024 (256 CUs x 4); below
+  // that the two-waves-per-problem kernel uses the idle SIMDs (measured: B2 aba N=40 at
+  // B = 256 +20 %, one Go2 problem +32 %; at B = 1024 it is 7 % slower).  PL_ADMM_WAVES
+  // (1 or 2) overrides.
+  h.admm_waves = batch <= 512 ? 2 : 1;
+  if (const char* w = getenv("PL_ADMM_WAVES")) h.admm_waves = atoi(w) == 2 ? 2 : 1;
   if (h.admm_waves == 2 && !admm2_supported(&h)) h.admm_waves = 1;
   h.gait_type = d->gait_type;
   h.gait_period = d->gait_period;
