@@ -26,6 +26,7 @@
 #include <cmath>
 #include <vector>
 
+#include "dyn.h"
 #include "rows.h"
 #include "targets.h"
 
@@ -146,9 +147,11 @@ void violation(const Problem& pr, const double* p, const double* x, const double
 template <int DYN>
 void eval_jac(const Problem& pr, const double* p, const double* x, Work& w, double* Ax) {
   Dual kst[PL_KIN_STORE];
+  double aba_sh[PL_ABA_SH];
   const int ndx = pr.O.ndx;
   for (int i = 0; i < pr.N; ++i) {
     const int xo = pr.x_off[i], xn = pr.x_off[i + 1], ncol = pr.nw[i] + ndx;
+    if (DYN == PL_DYN_ABA) pl::aba_primal(pr.M, pr.O, p, x + xo, aba_sh);  // ABA tangent by implicit function
     for (int lc = 0; lc < ncol; ++lc) {
       const int c = pr.jc_node_base[i] + lc;
       if (pr.jc_ptr[c] == pr.jc_ptr[c + 1]) continue;
@@ -156,7 +159,7 @@ void eval_jac(const Problem& pr, const double* p, const double* x, Work& w, doub
       pl::VecIn<Dual> u{x + xo + ndx, nullptr, 0.0, lc - ndx};
       pl::VecIn<Dual> dxn{x + xn, nullptr, 0.0, lc - pr.nw[i]};
       TEmit e{w.tan.data(), 0};
-      pl::node_rows<Dual, DYN>(pr.M, pr.O, i, p, dx, u, dxn, e, kst, 1);
+      pl::node_rows<Dual, DYN>(pr.M, pr.O, i, p, dx, u, dxn, e, kst, 1, nullptr, aba_sh);
       for (int q = pr.jc_ptr[c]; q < pr.jc_ptr[c + 1]; ++q) Ax[pr.jc_list[q].second] = w.tan[pr.jc_list[q].first];
     }
   }

@@ -235,6 +235,62 @@ PL_HD void momentum_rate(const PlModel& M, const double* q, const double* v, con
   for (int k = 0; k < 3; ++k) { out[k] = Hd[k]; out[3 + k] = Hd[3 + k] - cx[k]; }
 }
 
+// Shared primal of the ABA Jacobian lanes of one node (rows.h PL_ABA_SH): q, v from
+// x_init + dx; the mass matrix by RNEA columns (as crba below), its Cholesky factor, and
+// a = M^-1 ([0; tau_j] - RNEA(q, v, 0, f)).  Split in two so a wave can spread the
+// RNEA columns over its lanes: column c < nv is M e_c + t0, c = nv is t0 = RNEA(q, 0, 0),
+// c = nv + 1 is RNEA(q, v, 0, f); aba_primal_finish combines them (raw: (nv + 2) x nv).
+PL_HD void aba_primal_column(const PlModel& M, const PlOcpConst& O, const double* p, const double* dx, int c,
+                             double* out) {
+  const int nq = O.nq, nv = O.nv, nj = O.nj;
+  const double* xi = p + O.P.x_init;
+  const double* u = dx + O.ndx;
+  double q[PL_MAXQ], v[PL_MAXV], z[PL_MAXV], e[PL_MAXV];
+  VecIn<double> dq{dx, nullptr, 0.0, -1};
+  integrate_ff<double>(xi, dq, q);
+  for (int k = 7; k < nq; ++k) q[k] = xi[k] + dx[k - 1];
+  for (int k = 0; k < nv; ++k) {
+    v[k] = xi[nq + k] + dx[nv + k];
+    z[k] = 0.0;
+    e[k] = (k == c) ? 1.0 : 0.0;
+  }
+  if (c < nv) rnea_full(M, O, q, z, e, nullptr, out);
+  else if (c == nv) rnea_full(M, O, q, z, z, nullptr, out);
+  else rnea_full(M, O, q, v, z, u + nj, out);  // nle - J^T f
+}
+
+PL_HD void aba_primal_finish(const PlOcpConst& O, const double* dx, const double* raw, double* sh) {
+  const int nv = O.nv;
+  const double* u = dx + O.ndx;
+  const double* t0 = raw + nv * nv;
+  const double* bq = raw + (nv + 1) * nv;
+  double* L = sh + PL_MAXV;
+  for (int c = 0; c < nv; ++c)
+    for (int r = c; r < nv; ++r) L[r * (r + 1) / 2 + c] = raw[c * nv + r] - t0[r];
+  for (int c = 0; c < nv; ++c) {  // Cholesky in place
+    double* Lc = L + c * (c + 1) / 2;
+    double dd = Lc[c];
+    for (int k = 0; k < c; ++k) dd -= Lc[k] * Lc[k];
+    dd = sqrt(dd);
+    Lc[c] = dd;
+    for (int r = c + 1; r < nv; ++r) {
+      double* Lr = L + r * (r + 1) / 2;
+      double t = Lr[c];
+      for (int k = 0; k < c; ++k) t -= Lr[k] * Lc[k];
+      Lr[c] = t / dd;
+    }
+  }
+  for (int k = 0; k < nv; ++k) sh[k] = (k < 6 ? 0.0 : u[k - 6]) - bq[k];
+  chol_solve(L, nv, sh);
+}
+
+// Serial form (host callers: the CPU baseline and the host row tests).
+PL_HD void aba_primal(const PlModel& M, const PlOcpConst& O, const double* p, const double* dx, double* sh) {
+  double raw[(PL_MAXV + 2) * PL_MAXV];
+  for (int c = 0; c < O.nv + 2; ++c) aba_primal_column(M, O, p, dx, c, raw + c * O.nv);
+  aba_primal_finish(O, dx, raw, sh);
+}
+
 // One sample of function `fn`.  O carries the contact frames (feet [+ ext], nee)
 // and the base frame; F is the frame argument of the frame functions.
 PL_HD void dyn_eval(const PlModel& M, const PlOcpConst& O, const PlFrameRef& F, int fn, int flags,

@@ -7,6 +7,7 @@
 // uses one single-wave workgroup per (problem, node, 64-column chunk) and one
 // thread per local column, each thread seeding the tangent of its column and
 // writing the column's entries of the fixed sparsity pattern (CSC order inside the node).
+#include "dyn.h"
 #include "eval_common.h"
 
 using pl::VecIn;
@@ -83,10 +84,39 @@ void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz, int jl_len) {
   const int b = blockIdx.y;
   const int q = (int)blockIdx.x * 64 + threadIdx.x;
   const int first = d.jlist[blockIdx.x * 64].x;  // the wave's first node (never padding)
-  if (q >= jl_len) return;
-  const int2 jw = d.jlist[q];
-  if (jw.x < 0) return;
+  const bool valid = q < jl_len && d.jlist[min(q, jl_len - 1)].x >= 0;
+  const int2 jw = valid ? d.jlist[q] : make_int2(first, 0);
   const int i = jw.x, lc = jw.y;
+  const int slot = min(i - first, PL_JAC_SLOTS - 1);
+  // kinematic outputs: per-lane tangents + one shared value per entry and node of the
+  // wave (NodeKin<Dual>; the cheap columns read no stored value)
+  __shared__ double kst_tan[PL_KIN_STORE_DUAL * 64];
+  __shared__ double kst_val[PL_JAC_SLOTS * PL_KIN_STORE_DUAL];
+  double* aba_slot = nullptr;
+  if constexpr (DYN == PL_DYN_ABA) {
+    // the shared primal of each node of the wave (tree-pass columns only): its lanes split
+    // the nv + 2 RNEA columns (raw, in kst_tan before node_rows uses it), then the node's
+    // first lane factors M and solves for a
+    __shared__ double aba_sh[PL_JAC_SLOTS * PL_ABA_SH];
+    aba_slot = aba_sh + slot * PL_ABA_SH;
+    const int nv = d.oc->nv;
+    double* raw = kst_tan + slot * ((PL_KIN_STORE_DUAL * 64) / PL_JAC_SLOTS);
+    const bool tree = valid && lc < d.nodes[i].nw;
+    int s0 = threadIdx.x, s1 = threadIdx.x;  // this lane's node segment [s0, s1]
+    const int wb = (int)blockIdx.x * 64;
+    if (tree) {
+      while (s0 > 0 && d.jlist[wb + s0 - 1].x == i) --s0;
+      while (s1 < 63 && wb + s1 + 1 < jl_len && d.jlist[wb + s1 + 1].x == i) ++s1;
+    }
+    const double* pb = d.p + (size_t)b * np;
+    const double* dxi = d.x + (size_t)b * n + d.nodes[i].x_off;
+    if (tree)
+      for (int c = threadIdx.x - s0; c < nv + 2; c += s1 - s0 + 1) pl::aba_primal_column(*d.model, *d.oc, pb, dxi, c, raw + c * nv);
+    __syncthreads();
+    if (tree && threadIdx.x == s0) pl::aba_primal_finish(*d.oc, dxi, raw, aba_slot);
+    __syncthreads();
+  }
+  if (!valid) return;
   const PlNode nd = d.nodes[i];
   const int* cp = d.colptr + nd.colptr_off;
   const int e0 = cp[lc], e1 = cp[lc + 1];
@@ -100,13 +130,8 @@ void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz, int jl_len) {
   VecIn<Dual> u{x + nd.x_off + ndx, nullptr, 0.0, lc - ndx};
   VecIn<Dual> dxn{x + nn.x_off, nullptr, 0.0, lc - nd.nw};
   JacEmit e{d.rowidx + nd.ent_off, d.Araw + (size_t)b * nnz + nd.ent_off, e0, e1, 0};
-  // kinematic outputs: per-lane tangents + one shared value per entry and node of the
-  // wave (NodeKin<Dual>; the cheap columns read no stored value)
-  __shared__ double kst_tan[PL_KIN_STORE_DUAL * 64];
-  __shared__ double kst_val[PL_JAC_SLOTS * PL_KIN_STORE_DUAL];
-  const int slot = min(i - first, PL_JAC_SLOTS - 1);
   pl::node_rows<Dual, DYN>(M, O, i, p, dx, u, dxn, e, reinterpret_cast<Dual*>(kst_tan + threadIdx.x), 64,
-                           kst_val + slot * PL_KIN_STORE_DUAL);
+                           kst_val + slot * PL_KIN_STORE_DUAL, aba_slot);
 }
 
 __global__ __launch_bounds__(256) void k_objective(PlDev d, int N, int n, int np) {

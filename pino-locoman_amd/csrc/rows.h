@@ -90,12 +90,37 @@ template <class S> struct ZeroBaseAcc {
 
 // kstore: caller storage for the run-time indexed kinematic outputs (NodeKin,
 // PL_KIN_STORE entries spaced by kstride).
+// Shared primal of the ABA Jacobian (k_eval_jac<ABA>): a = ABA(q, v, tau_j, f) in
+// [0, PL_MAXV) and the Cholesky factor of the joint-space mass matrix M(q) (packed lower)
+// from PL_MAXV on.
+#define PL_ABA_SH (PL_MAXV + PL_MAXV * (PL_MAXV + 1) / 2)
+struct ShAcc {  // the shared primal acceleration as a constant (zero tangent)
+  const double* a;
+  PL_HD Dual operator[](int k) const { return Dual(a[k], 0.0); }
+};
+// x <- L^-T L^-1 x (L packed lower, row i at i (i + 1) / 2)
+PL_HD void chol_solve(const double* L, int n, double* x) {
+  for (int i = 0; i < n; ++i) {
+    const double* Li = L + i * (i + 1) / 2;
+    double t = x[i];
+    for (int k = 0; k < i; ++k) t -= Li[k] * x[k];
+    x[i] = t / Li[i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double t = x[i];
+    for (int k = i + 1; k < n; ++k) t -= L[k * (k + 1) / 2 + i] * x[k];
+    x[i] = t / L[i * (i + 1) / 2 + i];
+  }
+}
+
 // kvals (Dual only): a shared value store for the kinematic outputs (NodeKin<Dual>);
-// null keeps values and tangents interleaved in kstore.
+// null keeps values and tangents interleaved in kstore.  aba_sh (Dual, ABA only): the
+// node's shared primal (PL_ABA_SH); the ABA tangent then comes from the implicit
+// function M a' = [0; tau_j'] - RNEA'(q', v', f' | a) instead of a dual ABA.
 template <class S, int DYN, class Emit>
 PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double* p, const VecIn<S>& dx,
                      const VecIn<S>& u, const VecIn<S>& dxn, Emit& emit, S* kstore, int kstride,
-                     double* kvals = nullptr) {
+                     double* kvals = nullptr, const double* aba_sh = nullptr) {
   const int nv = O.nv, nq = O.nq, nj = O.nj;
   constexpr bool CV = (DYN == PL_DYN_CV);
   const double* xi = p + O.P.x_init;
@@ -157,7 +182,31 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
     cen = CV && !(seed_dxn || seed_h);
   }
   S comp[COMP ? 15 : 1];
-  if (tree && (want_tau || state_rows)) {
+  S aba_a[DYN == PL_DYN_ABA ? PL_MAXV : 1];
+  bool aba_done = false;
+  if constexpr (DYN == PL_DYN_ABA && std::is_same<S, Dual>::value) {
+    {  // aba_sh is required for the dual ABA rows (pl::aba_primal computes it)
+      if (tree) {
+        // one tree pass at the shared primal a: the RNEA tangent and the state rows
+        tree_pass<S>(M, O, qb, qrev, vel, ShAcc{aba_sh}, forces, true, state_rows, kin);
+        double r[PL_MAXV];
+        for (int k = 0; k < 6; ++k) r[k] = -kin.tau[k].d;
+        for (int k = 0; k < nj; ++k) {
+          const Dual t = kin.tau_j(k);
+          r[6 + k] = tau_j[k].d - t.d;
+        }
+        chol_solve(aba_sh + PL_MAXV, nv, r);
+        for (int k = 0; k < nv; ++k) aba_a[k] = Dual(aba_sh[k], r[k]);
+      } else {
+        for (int k = 0; k < PL_KIN_STORE_DUAL; ++k) kin.clear(k);
+        for (int k = 0; k < 3; ++k) kin.arm_vel[k] = S(0.0);
+        for (int k = 0; k < nv; ++k) aba_a[k] = S(0.0);
+      }
+      aba_done = true;
+    }
+  }
+  if (aba_done) {
+  } else if (tree && (want_tau || state_rows)) {
     if constexpr (NB) {
       tree_pass<S>(M, O, qb, qrev, vel, ZeroBaseAcc<S>{a}, forces, want_tau, state_rows, kin, comp, std::true_type{});
     } else if constexpr (COMP) {
@@ -195,9 +244,9 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
       for (int k = 0; k < 6; ++k) { hg[k] = S(0.0); hdot[k] = S(0.0); }
     }
   }
-  S aba_a[DYN == PL_DYN_ABA ? PL_MAXV : 1];
-  if constexpr (DYN == PL_DYN_ABA) {
-    if (tree) {
+  if constexpr (DYN == PL_DYN_ABA && !std::is_same<S, Dual>::value) {
+    if (aba_done) {
+    } else if (tree) {
       S q[PL_MAXQ], v[PL_MAXV];
       for (int k = 0; k < 7; ++k) q[k] = qb[k];
       for (int k = 7; k < nq; ++k) q[k] = qrev(k);

@@ -2,6 +2,7 @@
 // targets.h) so the CPU test suite can check the row function and its dual-number
 // Jacobian against the numpy oracle without a GPU.  Not linked into the product.
 #include <cstring>
+#include "dyn.h"
 #include "rows.h"
 #include "targets.h"
 
@@ -28,7 +29,9 @@ int run(const PlModel& M, const PlOcpConst& O, int i, const double* p, const dou
   pl::VecIn<Dual> a{dx, nullptr, 0.0, seed}, b{u, nullptr, 0.0, seed - ndx}, c{dxn, nullptr, 0.0, seed - nw};
   DEmit e{tan, 0};
   Dual kst[PL_KIN_STORE];
-  pl::node_rows<Dual, DYN>(M, O, i, p, a, b, c, e, kst, 1);
+  double aba_sh[PL_ABA_SH];
+  if (DYN == PL_DYN_ABA) pl::aba_primal(M, O, p, dx, aba_sh);
+  pl::node_rows<Dual, DYN>(M, O, i, p, a, b, c, e, kst, 1, nullptr, aba_sh);
   return e.r;
 }
 }  // namespace
