@@ -45,7 +45,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 
 
 TRAFFIC_FILE = os.path.join(HERE, "profiles", "traffic", "admm_traffic.json")
-TRAFFIC_SOURCES = ("pino-locoman_amd/csrc/k_admm.hip", "pino-locoman_amd/csrc/state.h")
+TRAFFIC_SOURCES = ("pino-locoman_amd/csrc/k_admm.hip", "pino-locoman_amd/csrc/admm_common.h",
+                   "pino-locoman_amd/csrc/state.h")
 
 
 def admm_bytes_per_problem_iter(sz, node_table, padded=False):
