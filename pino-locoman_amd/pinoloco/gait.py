@@ -4,7 +4,7 @@ Restates ``utils/gait_sequence.py`` of the reference:
 ``GaitSequence`` (``:5-77``), ``get_spline_vel_z`` (``:96-107``) and the OCS2
 ``CubicSpline`` (``:110-133``).  The schedule is host work done once per MPC
 step; the spline is evaluated again inside the HIP row kernels
-(``csrc/ocp_rows.h``) on the same parameters.
+(``csrc/rows.h``) on the same parameters.
 """
 from __future__ import annotations
 

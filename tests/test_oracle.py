@@ -174,3 +174,33 @@ def test_osqp_restatement_kkt():
     assert np.abs(Pd * x + q + A.T @ y).max() < 1e-4
     # complementarity: y < 0 only at the lower bound, y > 0 only at the upper bound
     assert np.all((y > 1e-6) <= (np.abs(Ax - u) < 1e-4)) and np.all((y < -1e-6) <= (np.abs(Ax - l) < 1e-4))
+
+
+@pytest.mark.parametrize("name,rname,dyn,N", [("go2_rnea_n20_walk", "go2", "whole_body_rnea", 20),
+                                             ("go2_cv_n20", "go2", "centroidal_vel", 20)])
+def test_rho_classification_independent_of_scaling_step(name, rname, dyn, N):
+    """The reference calls osqp_prob.update(q=, Ax=, l=, u=) (ocp.py:395); OSQP 0.6's
+    wrapper applies update_bounds before update_A, so it classifies the rows (equality
+    when the scaled width u-l < RHO_TOL) with the previous step's E, while the device and
+    the oracle use the current E.  For this problem family both give the same classes:
+    equality rows have width 0, and every finite two-sided row is so wide that the
+    scaled width clears RHO_TOL by orders of magnitude under either E."""
+    from oracle.osqp_ref import RHO_TOL
+    G = golden(f"sqp_{name}.npz")
+    gait = str(G["gait"]) if "gait" in G else "trot"
+    R = make_robot(rname, gait)
+    o = OracleOCP(R, dyn, N)
+    p = G["P"][0]
+    o.init_solver(G["X"][0], p)
+    Es = []
+    for x in (G["X"][0], G["x_new"][0]):  # this step's and the next step's linearisation
+        Ax = o.jacobian_values(x, p)
+        A = sp.csc_matrix((Ax, o.pattern.indices, o.pattern.indptr), shape=o.pattern.shape)
+        Es.append(o.osqp._scale(o.hess_diag, o.f_and_grad(x, p)[1], A)[4])
+    _, lbg, ubg = o.eval_g(G["x_new"][0], p)
+    w = ubg - lbg
+    two = np.isfinite(w) & (w > 0)
+    assert np.array_equal(w * Es[0] < RHO_TOL, w * Es[1] < RHO_TOL)
+    margin = min((w[two] * E[two]).min() for E in Es) / RHO_TOL
+    print(f"{name}: narrowest scaled two-sided row = {margin:.3g} x RHO_TOL")
+    assert margin > 10.0
