@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpinoloco.so")
+# PINOLOCO_LIB: load another build of the same sources (kernel A/B experiments)
+LIB_PATH = os.environ.get("PINOLOCO_LIB") or os.path.join(HERE, "libpinoloco.so")
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int)
