@@ -251,9 +251,11 @@ int pl_dyn_eval(pl_dyn* d, int fn, int batch, int frame, int flags, const double
 
 /* Timing of the dominant kernel (ADMM sweeps) with HIP events on the handle's
  * stream: pl_ocp_profile(o, 1) clears and starts, pl_ocp_profile_read returns
- * [total_ms, launches, problem_iterations]. pl_ocp_sizes (out[10]): [n, m, nnz,
- * factor doubles per problem, largest node block, N, ADMM gather program length,
- * its LDS-resident part, ADMM LDS bytes per workgroup, A values per thread]. */
+ * [total_ms, launches, problem_iterations]. pl_ocp_sizes (out[12]): [n, m, nnz,
+ * factor doubles per problem, largest node block, N, ADMM gather program length
+ * (u16 words, LDS-resident), problems per ADMM workgroup, ADMM LDS bytes per
+ * workgroup, A values per thread, A values per problem staged in LDS by the sweep,
+ * largest node's A count]. */
 int pl_ocp_profile(pl_ocp* o, int enable);
 int pl_ocp_profile_read(pl_ocp* o, double* out);
 int pl_ocp_sizes(const pl_ocp* o, long long* out);

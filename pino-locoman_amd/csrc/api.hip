@@ -1576,13 +1576,16 @@ extern "C" int pl_ocp_profile_read(pl_ocp* o, double* out) {
 
 int admm_lds_bytes(const PlOcpHandle* h);
 int admm_ppw(const PlOcpHandle* h);
+int admm_asb_cap(const PlOcpHandle* h);
 
 // Sizes: [n, m, nnz, S_stride (doubles), nw_max, N, ADMM programs (u16, LDS-resident),
-// problems per ADMM workgroup, ADMM LDS bytes per workgroup, A values per lane / 64].
+// problems per ADMM workgroup, ADMM LDS bytes per workgroup, A values per lane / 64,
+// A values per problem staged in LDS by the one-wave sweep, largest node's A count].
 extern "C" int pl_ocp_sizes(const pl_ocp* o, long long* out) {
   if (!o) { pl_set_error("null handle"); return -1; }
   out[0] = o->h.n; out[1] = o->h.m; out[2] = o->h.nnz; out[3] = o->h.S_stride; out[4] = o->h.nw_max; out[5] = o->h.N;
   out[6] = (long long)o->aprog.size(); out[7] = admm_ppw(&o->h); out[8] = admm_lds_bytes(&o->h); out[9] = o->h.admm_asr;
+  out[10] = admm_asb_cap(&o->h); out[11] = o->h.nent_max;
   return 0;
 }
 

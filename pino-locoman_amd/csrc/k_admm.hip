@@ -772,6 +772,8 @@ int admm_lds_bytes(const PlOcpHandle* h) { return (int)admm_config(h).lds; }
 
 int admm_ppw(const PlOcpHandle* h) { return admm_config(h).ppw; }
 
+int admm_asb_cap(const PlOcpHandle* h) { return admm_config(h).lm.asb_cap; }
+
 void launch_admm(PlOcpHandle* h, int niter, int check, int it_base) {
   (void)it_base;
   const AdmmCfg c = admm_config(h);

@@ -350,10 +350,10 @@ class BatchedOCP:
         return {"admm_ms": out[0], "launches": int(out[1]), "problem_iters": int(out[2])}
 
     def sizes(self):
-        out = (C.c_longlong * 10)()
+        out = (C.c_longlong * 12)()
         _lib.check(_lib.lib().pl_ocp_sizes(self.h, out))
         return dict(zip(("n", "m", "nnz", "S_stride", "nw_max", "N", "admm_prog", "admm_ppw", "admm_lds_bytes",
-                         "admm_asr"), [int(v) for v in out]))
+                         "admm_asr", "admm_asb_cap", "nent_max"), [int(v) for v in out]))
 
     def close(self):
         if getattr(self, "h", None):
