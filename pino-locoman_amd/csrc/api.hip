@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "../../include/pinoloco.h"
@@ -1689,6 +1690,9 @@ extern "C" int pl_debug_admm(pl_ocp* o, int niter, int reset) {
 // library: shapes and sparsity come from the OCP bound with pl_casadi_bind (same process:
 // ca.external dlopens the already-loaded library).  Evaluations run on the bound handle's
 // device (problem slot 0); J_g is returned in CasADi's compressed-column order.
+// Every entry point takes one process-wide lock (CasADi may evaluate from several
+// threads, e.g. a threaded map; the bound handle has one stream and one staging
+// buffer), and each evaluation waits on its stream once, after all its copies.
 namespace {
 typedef long long casadi_int;
 struct CasadiState {
@@ -1699,6 +1703,8 @@ struct CasadiState {
   std::vector<double> buf;
 };
 CasadiState g_cas;
+std::mutex g_cas_mu;
+#define PL_CAS_LOCK std::lock_guard<std::mutex> cas_lock_(g_cas_mu)
 
 std::vector<casadi_int> dense_sp(int nrow, int ncol) {
   std::vector<casadi_int> s{nrow, ncol};
@@ -1740,22 +1746,24 @@ int cas_eval(const double** arg, bool jac) {
   launch_eval_values(h, h->d.x);
   if (jac) launch_eval_jac(h);
   launch_objective(h);
-  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess) return 1;
-  return 0;
+  return hipGetLastError() != hipSuccess;
 }
 
+// enqueue one device -> host copy of an output (null outputs are skipped)
 int cas_get(const double* dev, size_t count, double* host) {
   if (!host) return 0;
   PlOcpHandle* h = &g_cas.o->h;
-  if (hipMemcpyAsync(host, dev, count * 8, hipMemcpyDeviceToHost, h->stream) != hipSuccess) return 1;
-  return hipStreamSynchronize(h->stream) != hipSuccess;
+  return hipMemcpyAsync(host, dev, count * 8, hipMemcpyDeviceToHost, h->stream) != hipSuccess;
 }
+
+int cas_wait() { return hipStreamSynchronize(g_cas.o->h.stream) != hipSuccess; }
 }  // namespace
 
 extern "C" int pl_casadi_bind(pl_ocp* o, int retract_steps) {
   if (!o) { pl_set_error("null handle"); return -1; }
   const PlOcpHandle& h = o->h;
   if (retract_steps < 1 || retract_steps > h.N) { pl_set_error("retract_steps %d outside [1, N]", retract_steps); return -1; }
+  PL_CAS_LOCK;
   CasadiState& c = g_cas;
   c.o = o;
   c.steps = retract_steps;
@@ -1813,9 +1821,13 @@ extern "C" int pl_casadi_bind(pl_ocp* o, int retract_steps) {
   return 0;
 }
 
-extern "C" void pl_casadi_unbind(void) { g_cas.o = nullptr; }
+extern "C" void pl_casadi_unbind(void) {
+  PL_CAS_LOCK;
+  g_cas.o = nullptr;
+}
 
 static void cas_forget(const pl_ocp* o) {
+  PL_CAS_LOCK;
   if (g_cas.o == o) g_cas.o = nullptr;
 }
 
@@ -1854,10 +1866,12 @@ extern "C" const char* sqp_data_name_out(casadi_int i) {
   return cas_name(n, 5, i);
 }
 extern "C" const casadi_int* sqp_data_sparsity_in(casadi_int i) {
+  PL_CAS_LOCK;
   if (!cas_ready()) return nullptr;
   return i == 0 ? g_cas.sp_x.data() : (i == 1 ? g_cas.sp_p.data() : nullptr);
 }
 extern "C" const casadi_int* sqp_data_sparsity_out(casadi_int i) {
+  PL_CAS_LOCK;
   if (!cas_ready()) return nullptr;
   switch (i) {
     case 0: return g_cas.sp_n1.data();
@@ -1867,15 +1881,17 @@ extern "C" const casadi_int* sqp_data_sparsity_out(casadi_int i) {
   }
 }
 extern "C" int sqp_data(const double** arg, double** res, casadi_int*, double*, int) {
+  PL_CAS_LOCK;
   if (!cas_ready() || cas_eval(arg, true)) return 1;
   PlOcpHandle* h = &g_cas.o->h;
-  if (cas_get(h->d.grad, h->n, res[0])) return 1;
-  if (res[1]) {
-    g_cas.buf.resize(h->nnz);
-    if (cas_get(h->d.Araw, h->nnz, g_cas.buf.data())) return 1;
+  if (res[1]) g_cas.buf.resize(h->nnz);
+  // every copy is enqueued (| does not short-circuit) and waited for before returning
+  if (cas_get(h->d.grad, h->n, res[0]) | cas_get(h->d.Araw, h->nnz, res[1] ? g_cas.buf.data() : nullptr) |
+      cas_get(h->d.g, h->m, res[2]) | cas_get(h->d.lbg, h->m, res[3]) | cas_get(h->d.ubg, h->m, res[4]) | cas_wait())
+    return 1;
+  if (res[1])
     for (size_t k = 0; k < g_cas.J_perm.size(); ++k) res[1][k] = g_cas.buf[g_cas.J_perm[k]];
-  }
-  return cas_get(h->d.g, h->m, res[2]) || cas_get(h->d.lbg, h->m, res[3]) || cas_get(h->d.ubg, h->m, res[4]);
+  return 0;
 }
 
 // f_data(x, p) -> (f, grad_f)
@@ -1890,18 +1906,18 @@ extern "C" const char* f_data_name_out(casadi_int i) {
 }
 extern "C" const casadi_int* f_data_sparsity_in(casadi_int i) { return sqp_data_sparsity_in(i); }
 extern "C" const casadi_int* f_data_sparsity_out(casadi_int i) {
+  PL_CAS_LOCK;
   if (!cas_ready()) return nullptr;
   return i == 0 ? g_cas.sp_11.data() : (i == 1 ? g_cas.sp_n1.data() : nullptr);
 }
 extern "C" int f_data(const double** arg, double** res, casadi_int*, double*, int) {
+  PL_CAS_LOCK;
   if (!cas_ready() || cas_eval(arg, false)) return 1;
   PlOcpHandle* h = &g_cas.o->h;
-  if (res[0]) {
-    double w[8];
-    if (cas_get(h->d.work, 8, w)) return 1;
-    res[0][0] = w[0];
-  }
-  return cas_get(h->d.grad, h->n, res[1]);
+  double w[8];
+  if (cas_get(h->d.work, 8, w) | cas_get(h->d.grad, h->n, res[1]) | cas_wait()) return 1;
+  if (res[0]) res[0][0] = w[0];
+  return 0;
 }
 
 // g_data(x, p) -> (g, lbg, ubg)
@@ -1916,13 +1932,16 @@ extern "C" const char* g_data_name_out(casadi_int i) {
 }
 extern "C" const casadi_int* g_data_sparsity_in(casadi_int i) { return sqp_data_sparsity_in(i); }
 extern "C" const casadi_int* g_data_sparsity_out(casadi_int i) {
+  PL_CAS_LOCK;
   if (!cas_ready()) return nullptr;
   return (i >= 0 && i < 3) ? g_cas.sp_m1.data() : nullptr;
 }
 extern "C" int g_data(const double** arg, double** res, casadi_int*, double*, int) {
+  PL_CAS_LOCK;
   if (!cas_ready() || cas_eval(arg, false)) return 1;
   PlOcpHandle* h = &g_cas.o->h;
-  return cas_get(h->d.g, h->m, res[0]) || cas_get(h->d.lbg, h->m, res[1]) || cas_get(h->d.ubg, h->m, res[2]);
+  return cas_get(h->d.g, h->m, res[0]) | cas_get(h->d.lbg, h->m, res[1]) | cas_get(h->d.ubg, h->m, res[2]) |
+         cas_wait();
 }
 
 // hess_data(x, p) -> hess_f (diagonal pattern; constant, ocp.py:293-296)
@@ -1934,10 +1953,12 @@ extern "C" const char* hess_data_name_in(casadi_int i) {
 extern "C" const char* hess_data_name_out(casadi_int i) { return i == 0 ? "o0" : nullptr; }
 extern "C" const casadi_int* hess_data_sparsity_in(casadi_int i) { return sqp_data_sparsity_in(i); }
 extern "C" const casadi_int* hess_data_sparsity_out(casadi_int i) {
+  PL_CAS_LOCK;
   if (!cas_ready()) return nullptr;
   return i == 0 ? g_cas.sp_H.data() : nullptr;
 }
 extern "C" int hess_data(const double** arg, double** res, casadi_int*, double*, int) {
+  PL_CAS_LOCK;
   if (!cas_ready()) return 1;
   pl_ocp* o = g_cas.o;
   PlOcpHandle* h = &o->h;
@@ -1947,7 +1968,7 @@ extern "C" int hess_data(const double** arg, double** res, casadi_int*, double*,
   if (!arg[1] || hipMemcpyAsync(h->d.p, arg[1], h->np * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess) return 1;
   launch_hess(h);
   if (hipGetLastError() != hipSuccess) return 1;
-  return cas_get(h->d.P, h->n, res[0]);
+  return cas_get(h->d.P, h->n, res[0]) | cas_wait();
 }
 
 // retract_solution(sol_x, x_init) -> (q, v, a, forces, tau), first `steps` nodes, node-major
@@ -1962,10 +1983,12 @@ extern "C" const char* retract_solution_name_out(casadi_int i) {
   return cas_name(n, 5, i);
 }
 extern "C" const casadi_int* retract_solution_sparsity_in(casadi_int i) {
+  PL_CAS_LOCK;
   if (!cas_ready()) return nullptr;
   return i == 0 ? g_cas.sp_x.data() : (i == 1 ? g_cas.sp_xinit.data() : nullptr);
 }
 extern "C" const casadi_int* retract_solution_sparsity_out(casadi_int i) {
+  PL_CAS_LOCK;
   if (!cas_ready()) return nullptr;
   switch (i) {
     case 0: return g_cas.sp_q.data();
@@ -1982,6 +2005,7 @@ extern "C" const casadi_int* retract_solution_sparsity_out(casadi_int i) {
 // cv: v from the inputs, a by forward difference with the base part from the
 // centroidal base_acc_dynamics; the step sizes are the bound handle's (problem 0).
 extern "C" int retract_solution(const double** arg, double** res, casadi_int*, double*, int) {
+  PL_CAS_LOCK;
   if (!cas_ready() || !arg[0] || !arg[1]) return 1;
   const pl_ocp* o = g_cas.o;
   const PlModel& M = o->h.model;

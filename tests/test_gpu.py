@@ -372,6 +372,17 @@ def test_casadi_external_functions_match_golden():
     from oracle.ocp import OracleOCP
     hd = OracleOCP(R, "whole_body_rnea", 20).compute_hess_diag(p)
     assert np.array_equal(H.diagonal(), hd)
+    # concurrent evaluations (as from a threaded CasADi map; ctypes drops the GIL): the
+    # library's lock serialises them on the bound handle, and every result is the serial one
+    from concurrent.futures import ThreadPoolExecutor
+    fn = casadi_ext.ExternalFunction("sqp_data")
+    xs = [x + 1e-3 * k for k in range(8)]
+    with ThreadPoolExecutor(4) as ex:
+        par = list(ex.map(lambda xk: fn(xk, p), xs))
+    for xk, got in zip(xs, par):
+        want = fn(xk, p)
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[2], want[2])
+        assert (got[1] != want[1]).nnz == 0
     casadi_ext.unbind()
     bo.close()
 
