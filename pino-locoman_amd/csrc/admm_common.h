@@ -98,6 +98,14 @@ __device__ __forceinline__ void gst(T* base, int idx, T v) {
   *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (unsigned)idx * (unsigned)sizeof(T)) = v;
 }
 
+// LDS f64 add without return (ds_add_f64): one instruction per lane, no round trip.  The
+// lanes of one instruction and the instructions of one wave are applied in a fixed order,
+// so the sums are deterministic (bit-identical for a problem in any batch).
+__device__ __forceinline__ void lds_add(double* p, double v) {
+  typedef __attribute__((address_space(3))) double* LPtr;
+  __hip_atomic_fetch_add((LPtr)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 __device__ __forceinline__ int div_k(int t, int K, unsigned km) { return K == 1 ? t : (int)__umulhi((unsigned)t, km); }
 
 __device__ __forceinline__ void tile_ij(int t, int& I, int& J) {

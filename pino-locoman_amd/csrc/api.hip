@@ -594,6 +594,10 @@ int build_admm_prog(pl_ocp* o) {
       for (auto& c : ch) pair(c.first, c.second);
       mark(a.rchptr);
       for (int x : ptr) P.push_back((uint16_t)x);
+      std::vector<int> own;
+      for (int r = 0; r < nd.nrow; ++r)
+        for (int k = ptr[r]; k < ptr[r + 1]; ++k) own.push_back(r);
+      bytes(a.rchr, a.rchn, [&](int k) { return own[k]; });
       ch.clear();
       ptr.assign(1, 0);
       for (int c = 0; c < nd.ncol; ++c) {
@@ -605,6 +609,10 @@ int build_admm_prog(pl_ocp* o) {
       for (auto& c : ch) pair(c.first, c.second);
       mark(a.cchptr);
       for (int x : ptr) P.push_back((uint16_t)x);
+      own.clear();
+      for (int c = 0; c < nd.ncol; ++c)
+        for (int k = ptr[c]; k < ptr[c + 1]; ++k) own.push_back(c);
+      bytes(a.cchc, a.cchn, [&](int k) { return own[k]; });
       h.chunk_max = std::max(h.chunk_max, std::max(a.rchn, a.cchn));
     }
     a.prog = intern(aprogs, aoff, o->aprog, P);

@@ -237,6 +237,23 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     int curI = -1;
     double sa[4] = {0.0, 0.0, 0.0, 0.0};
     bool use_tt = false;
+#if PL_ADMM_ATOMIC
+    // accumulate y in LDS with ds_add_f64 (no return, no dependent round trips):
+    // output 4 I + r lives at acc5[5 I + r] (a stride of 5 doubles spreads the banks)
+    double* acc5 = seg;
+    for (int o = lane; o < 5 * T; o += 64) acc5[o] = 0.0;
+    wsync();
+    auto emit_row = [&](int I0) __attribute__((always_inline)) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lds_add(acc5 + I0 * 5 + r, sa[r]);
+    };
+#else
+    auto emit_row = [&](int I0) __attribute__((always_inline)) {
+      double2* sp = reinterpret_cast<double2*>(seg + (lane + I0) * 4);
+      sp[0] = make_double2(sa[0], sa[1]);
+      sp[1] = make_double2(sa[2], sa[3]);
+    };
+#endif
     auto pass = [&](int kb, bool last_pass) __attribute__((always_inline)) {
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
@@ -273,18 +290,20 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
               cp[2] += R.s[k][2 * r + 1].x * vi[r];
               cp[3] += R.s[k][2 * r + 1].y * vi[r];
             }
+#if PL_ADMM_ATOMIC
+            (void)cidx;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) lds_add(acc5 + J * 5 + c, cp[c]);
+#else
             // column-major packed off-diagonal index: the partials of one output tile
             // column are contiguous
             double2* cpp = reinterpret_cast<double2*>(colp + cidx * 4);
             cpp[0] = make_double2(cp[0], cp[1]);
             cpp[1] = make_double2(cp[2], cp[3]);
+#endif
           }
           if (I != curI) {
-            if (curI >= 0) {
-              double2* sp = reinterpret_cast<double2*>(seg + (lane + curI) * 4);
-              sp[0] = make_double2(sa[0], sa[1]);
-              sp[1] = make_double2(sa[2], sa[3]);
-            }
+            if (curI >= 0) emit_row(curI);
             curI = I;
 #pragma unroll
             for (int r = 0; r < 4; ++r) sa[r] = rp[r];
@@ -309,12 +328,16 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
         pass(kb, kb + KM >= K);
       }
     }
-    if (curI >= 0) {
-      double2* sp = reinterpret_cast<double2*>(seg + (lane + curI) * 4);
-      sp[0] = make_double2(sa[0], sa[1]);
-      sp[1] = make_double2(sa[2], sa[3]);
-    }
+    if (curI >= 0) emit_row(curI);
     wsync();
+#if PL_ADMM_ATOMIC
+    (void)km;
+#pragma unroll
+    for (int mm = 0; mm < MV; ++mm) {
+      const int o = lane + 64 * mm;
+      if (o < nw) y[o] = acc5[(o >> 2) * 5 + (o & 3)];
+    }
+#else
 #pragma unroll
     for (int mm = 0; mm < MV; ++mm) {
       const int o = lane + 64 * mm;
@@ -328,6 +351,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
         y[o] = rs + cs;
       }
     }
+#endif
     wsync();
   };
 
@@ -509,6 +533,11 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
           const uint8_t* rowc = reinterpret_cast<const uint8_t*>(P + an[i].rowc);
           const uint32_t* rch = reinterpret_cast<const uint32_t*>(P + an[i].rch);
           const int rchn = an[i].rchn;
+#if PL_ADMM_ATOMIC
+          const uint8_t* rchr = reinterpret_cast<const uint8_t*>(P + an[i].rchr);
+          for (int o = lane; o < an[i].nrow; o += 64) part[o] = 0.0;  // row sums, by LDS f64 adds
+          wsync();
+#endif
           for (int c0 = 0; c0 < rchn; c0 += 128) {  // two rounds of chunks per batch
             double acc[2];
 #pragma unroll
@@ -526,8 +555,14 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
               acc[u] = a;
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
-              if (c0 + lane + 64 * u < rchn) part[c0 + lane + 64 * u] = acc[u];
+            for (int u = 0; u < 2; ++u) {
+              const int ch = c0 + lane + 64 * u;
+#if PL_ADMM_ATOMIC
+              if (ch < rchn) lds_add(part + rchr[ch], acc[u]);
+#else
+              if (ch < rchn) part[ch] = acc[u];
+#endif
+            }
           }
         }
         wsync();
@@ -542,8 +577,13 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
           for (int mm = 0; mm < MR; ++mm) {
             const int r = lane + 64 * mm;
             if (r < nrow) {
+#if PL_ADMM_ATOMIC
+              (void)rcp;
+              const double zt = part[r];
+#else
               const int k0 = P[rcp + r], k1 = P[rcp + r + 1];
               const double zt = lds_sum<4>(part, k0, k1, 1, zslot);
+#endif
               const double zrel = alpha * zt + (1.0 - alpha) * LR.z[mm];
               double zn = zrel + (1.0 / LR.rho[mm]) * LR.y[mm];
               zn = fmin(fmax(zn, LR.l[mm]), LR.u[mm]);
@@ -563,6 +603,12 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
           const uint8_t* colr = reinterpret_cast<const uint8_t*>(P + an[i].colr);
           const uint32_t* cch = reinterpret_cast<const uint32_t*>(P + an[i].cch);
           const int cchn = an[i].cchn;
+#if PL_ADMM_ATOMIC
+          // column sums by LDS f64 adds (the z update's reads of `part` are ahead in LDS order)
+          const uint8_t* cchc = reinterpret_cast<const uint8_t*>(P + an[i].cchc);
+          for (int o = lane; o < an[i].ncol; o += 64) part[o] = 0.0;
+          wsync();
+#endif
           for (int c0 = 0; c0 < cchn; c0 += 128) {  // two rounds of chunks per batch
             double acc[2];
 #pragma unroll
@@ -580,8 +626,14 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
               acc[u] = a;
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
-              if (c0 + lane + 64 * u < cchn) part[c0 + lane + 64 * u] = acc[u];
+            for (int u = 0; u < 2; ++u) {
+              const int ch = c0 + lane + 64 * u;
+#if PL_ADMM_ATOMIC
+              if (ch < cchn) lds_add(part + cchc[ch], acc[u]);
+#else
+              if (ch < cchn) part[ch] = acc[u];
+#endif
+            }
           }
         }
       });
@@ -598,11 +650,20 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
             set2(pxa, mm, xnew);
             set2(pdx, mm, xnew - LC.x[mm]);
             double acc = sigma * xnew - LC.q[mm];
+#if PL_ADMM_ATOMIC
+            (void)ccp0;
+            acc += part[c];
+#else
             const int k0 = P[ccp0 + c], k1 = P[ccp0 + c + 1];
             acc += lds_sum<4>(part, k0, k1, 1, zslot);
+#endif
             if (c < ndx) {  // rows of node i on dx_{i+1} complete rhs_{i+1}
+#if PL_ADMM_ATOMIC
+              const double a2 = part[nw + c];
+#else
               const int f0 = P[ccp0 + nw + c], f1 = P[ccp0 + nw + c + 1];
               const double a2 = lds_sum<4>(part, f0, f1, 1, zslot);
+#endif
               prn = rkeep + a2;
               if (i == 0) r1[c] = prn;
             }
@@ -727,11 +788,16 @@ AdmmCfg admm_config(const PlOcpHandle* h) {
   // partials (mat-vec) | chunk sums and rho z - y (row / column gathers)
   lm.red = o;
   lm.tcpl = o;
+#if PL_ADMM_ATOMIC
+  const int matv = 5 * T;  // the mat-vec accumulator acc5 (no segments, no column partials)
+  lm.colp = o;
+#else
   const int segn = (64 + T) * 4;
+  const int matv = segn + T * (T - 1) / 2 * 4;
   lm.colp = o + segn;
+#endif
   lm.trow = o + up2(h->chunk_max);
-  o += up2(std::max(std::max(segn + T * (T - 1) / 2 * 4, up2(h->chunk_max) + h->nrow_max),
-                    std::max(h->ncpl_max, 1)));
+  o += up2(std::max(std::max(matv, up2(h->chunk_max) + h->nrow_max), std::max(h->ncpl_max, 1)));
   lm.asb = o;
   // problems per workgroup: 4 puts one wave on every SIMD of every CU once B >= 4 x 256
   c.ppw = h->B >= 1024 ? 4 : (h->B >= 512 ? 2 : 1);

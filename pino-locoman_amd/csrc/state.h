@@ -53,6 +53,7 @@ struct PlNode {
 //   row chunks (<= PL_CHUNK entries of one row): rchn chunks rch[] = (q0, q1) into rowe/rowc,
 //                                                rchptr[nrow+1] = first chunk of each row
 //   column chunks (<= PL_CHUNK entries):         cchn chunks cch[] = (e0, e1), cchptr[ncol+1]
+//   owner of each chunk (u8):                    rchr[rchn] = local row, cchc[cchn] = local col
 //
 // Factor layout (k_factor writes, k_admm streams): the lower triangle of S_i in
 // 4x4 tiles (I, J), J <= I < T, packed row-major t = I (I + 1) / 2 + J (diagonal
@@ -61,6 +62,9 @@ struct PlNode {
 // s_off + ((k * 8 + j) * 64 + l) * 2, so each 16-byte load of a wave is 1 KiB contiguous.
 #define PL_CHUNK 6
 // ADMM sweep kernel limits (one wave per problem, k_admm.hip)
+#ifndef PL_ADMM_ATOMIC
+#define PL_ADMM_ATOMIC 1  // k_admm mat-vec: accumulate y with LDS f64 atomics (0: segment sums)
+#endif
 #define PL_ADMM_KM 4        // factor tile slots per lane held in registers (more: extra passes)
 #define PL_ADMM_CWM 2       // w entries per coupling row held in registers (more: LDS path)
 #define PL_ADMM_XCM 1       // coupling entries per dx_{i+1} column held in registers
@@ -73,7 +77,7 @@ struct PlAdmmNode {
   int x_off, row_off, ent_off, s_off;
   int prog, prog_len;
   int rowe, rowc, colr, cwptr, cwp, cxptr, cxp, ccptr, ccp, xcptr, xcp;
-  int rchn, rch, rchptr, cchn, cch, cchptr;
+  int rchn, rch, rchptr, cchn, cch, cchptr, rchr, cchc;
   int fprog, flen, f_rowptr, f_cplr, f_rowp;
   int f_cwptr, f_cwp, f_xcptr, f_xcp, f_cxptr, f_cxp;  // coupling lists of the factor program
   int ttab;  // offset (u32) of the node's lane-tile table in d.ttab (-1: more than PL_ADMM_KM slots)
