@@ -81,7 +81,9 @@ typedef struct {
   int nodes;                   /* N */
   int tau_nodes;               /* OCP_ARGS["whole_body_rnea"]["tau_nodes"] (ocp_args.py:16) */
   int include_acc;             /* must be 1 (ocp_args.py:17) */
-  int include_base;            /* must be 1 for whole_body_acc / centroidal_vel (ocp_args.py:5-11) */
+  int include_base;            /* acc / centroidal_acc / centroidal_vel: 1 = base in u (ocp_args.py:5-11);
+                                  0 = base acceleration / velocity from the dynamics
+                                  (ocp_whole_body_acc.py:124-135, ocp_centroidal_vel.py:119-129) */
   int n_feet;                  /* 4: FR, FL, RR, RL (utils/gait_sequence.py:7) */
   int foot_frames[4];
   int ext_force_frame;         /* -1: none */

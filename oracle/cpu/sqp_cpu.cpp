@@ -605,7 +605,7 @@ StepStats mpc_step(const Problem& pr, Work& w, OsqpState& st, double* p, const d
   StepStats s = sqp_step<DYN>(pr, w, st, p, Pd, x);
   const double* dx1 = x + pr.x_off[1];
   double qn[PL_MAXQ];
-  if (O.dyn == PL_DYN_CV) {
+  if (PL_IS_CV(O.dyn)) {
     pl::VecIn<double> acc{dx1 + 6, nullptr, 0.0, -1};
     pl::integrate_q<double>(pr.M, xs + 6, acc, qn);
     for (int j = 0; j < 6; ++j) xs[j] += dx1[j];
@@ -761,6 +761,7 @@ extern "C" double cpu_mpc_batch(void* h, int B, const double* P, const double* X
         case PL_DYN_ABA: run_problem<PL_DYN_ABA>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
         case PL_DYN_CA: run_problem<PL_DYN_CA>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
         case PL_DYN_ACCNB: run_problem<PL_DYN_ACCNB>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
+        case PL_DYN_CVNB: run_problem<PL_DYN_CVNB>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
         default: run_problem<PL_DYN_CV>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
       }
     }
@@ -787,6 +788,7 @@ extern "C" int cpu_sqp_step(void* h, const double* p, double* x, double* dx, int
     case PL_DYN_ABA: s = sqp_step<PL_DYN_ABA>(pr, w, st, p, Pd.data(), x); break;
     case PL_DYN_CA: s = sqp_step<PL_DYN_CA>(pr, w, st, p, Pd.data(), x); break;
     case PL_DYN_ACCNB: s = sqp_step<PL_DYN_ACCNB>(pr, w, st, p, Pd.data(), x); break;
+    case PL_DYN_CVNB: s = sqp_step<PL_DYN_CVNB>(pr, w, st, p, Pd.data(), x); break;
     default: s = sqp_step<PL_DYN_CV>(pr, w, st, p, Pd.data(), x); break;
   }
   for (int j = 0; j < pr.n; ++j) dx[j] = w.step[j];

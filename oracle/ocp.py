@@ -93,9 +93,10 @@ class OracleOCP:
             self.nx, self.ndx = self.nq + nv, 2 * nv
             self.nu = [nj + nf] * nodes
         elif dynamics == "centroidal_vel":
-            assert include_base
+            # u = [v | f] (include_base) or [v_j | f] (ocp_centroidal_vel.py:19-23, 56-57)
             self.nx, self.ndx = 6 + self.nq, 6 + nv
-            self.nu = [nv + nf] * nodes
+            self.nv_opt = nv if include_base else nj
+            self.nu = [self.nv_opt + nf] * nodes
         else:
             raise ValueError(f"Unknown dynamics type: {dynamics}")
         self.x_off = []
@@ -159,7 +160,7 @@ class OracleOCP:
         Qv = [2000, 2000, 1000, 1000, 1000, 2000] + [1] * nj
         if self.dynamics == "centroidal_vel":
             Q = [1000] * 6 + Qb + Qj
-            R = [1] * self.nv + [1e-3] * nf
+            R = [1] * self.nv_opt + [1e-3] * nf
         else:
             Q = Qb + Qj + Qv
             if self.dynamics == "whole_body_rnea":
@@ -189,7 +190,7 @@ class OracleOCP:
             return np.concatenate([np.zeros(self.na), fd])
         if self.dynamics == "whole_body_aba":
             return np.concatenate([np.zeros(self.nj), fd])
-        return np.concatenate([np.zeros(self.nv), fd])
+        return np.concatenate([np.zeros(self.nv_opt), fd])
 
     def dx_des(self, P):
         xi = P["x_init"]
@@ -243,8 +244,12 @@ class OracleOCP:
         dyn = self.dynamics
         if dyn == "centroidal_vel":
             h, q = self.state(dx, P)
-            v = u[..., :nv]
-            forces = u[..., nv:]
+            if self.include_base:
+                v = u[..., :nv]
+            else:  # get_v: v_b = base_vel_dynamics(h, q, v_j) (ocp_centroidal_vel.py:119-129)
+                v_j = u[..., :nj]
+                v = np.concatenate([rbd.base_vel_cv(self.M, h, q, v_j, self.mass), v_j], -1)
+            forces = u[..., self.nv_opt:]
         else:
             q, v = self.state(dx, P)
         if dyn == "whole_body_rnea":
@@ -288,8 +293,9 @@ class OracleOCP:
             hdot = self._com_dynamics(q, forces)
             add(dx_next[..., :6] - (dx[..., :6] + hdot * dt), 0, 0)
             add(dx_next[..., 6:] - (dx[..., 6:] + v * dt), 0, 0)
-            hg = rbd.centroidal_momentum(self.M, q, v)
-            add(hg - h * self.mass, 0, 0)
+            if self.include_base:  # dynamics_gaps (ocp_centroidal_vel.py:104-107)
+                hg = rbd.centroidal_momentum(self.M, q, v)
+                add(hg - h * self.mass, 0, 0)
 
         skip_state = (i == 0 and dyn != "centroidal_vel")
         fvel = None
@@ -571,7 +577,7 @@ class OracleOCP:
             elif self.dynamics in ("whole_body_acc", "centroidal_acc"):
                 uw = np.concatenate([U[i][:self.na], f])
             else:
-                uw = np.concatenate([U[i][:self.nv], f])
+                uw = np.concatenate([U[i][:self.nv_opt], f])
             x[o:o + self.nu[i]] = uw
         return x
 

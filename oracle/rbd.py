@@ -592,8 +592,9 @@ def com_dynamics(M: ModelArrays, frames, q, forces, mass, scale=True):
 
 def base_vel_cv(M: ModelArrays, h, q, v_j, mass):
     """base_vel_dynamics (dynamics_centroidal_vel.py:73-89): A_b^-1 (m h - A_j v_j)."""
-    A = centroidal_map(M, q)
-    return np.linalg.solve(A[:, :6], h * mass - A[:, 6:] @ v_j)
+    A = centroidal_map(M, q)  # (..., 6, nv); h, v_j may carry the same leading dims
+    rhs = h * mass - (A[..., :, 6:] @ np.asarray(v_j)[..., None])[..., 0]
+    return np.linalg.solve(A[..., :, :6], rhs[..., None])[..., 0]
 
 
 def base_acc_cv(M: ModelArrays, frames, q, v, a_j, forces, mass):

@@ -155,14 +155,14 @@ void build_blocks(PlOcpConst& O, bool has_ext, bool has_arm) {
     O.nblk[type] = 0;
     const bool first = (type == 0);
     const bool tau = (O.dyn == PL_DYN_RNEA) && (type == 1 || (type == 0 && O.tau_nodes > 0));
-    const bool cv = (O.dyn == PL_DYN_CV);
+    const bool cv = PL_IS_CV(O.dyn);
     // centroidal_vel keeps the state rows at node 0 (ocp.py:137-140, 170-173)
     const bool state = !first || cv;
     if (first) add_block(O, type, PL_RB_INIT, O.ndx);
     if (cv) {  // setup_dynamics_constraints (ocp_centroidal_vel.py:85-107)
       add_block(O, type, PL_RB_CV_DYNH, 6);
       add_block(O, type, PL_RB_CV_DYNQ, O.nv);
-      add_block(O, type, PL_RB_CV_GAP, 6);
+      if (O.dyn == PL_DYN_CV) add_block(O, type, PL_RB_CV_GAP, 6);  // include_base only
     } else {
       add_block(O, type, PL_RB_DYNQ, O.nv);
       add_block(O, type, PL_RB_DYNV, O.nv);
@@ -210,14 +210,22 @@ std::vector<std::vector<int>> node_row_deps(const PlModel& M, const PlOcpConst& 
   const int type = pl::node_type(O, i);
   const int nv = O.nv, nj = O.nj, nf = O.nf, ndx = O.ndx;
   const int nw = ndx + nu;
-  const bool cv = (O.dyn == PL_DYN_CV);
-  // dx = [dq, dv] (whole body) or [dh, dq] with v = u[:nv] (centroidal_vel)
+  const bool cv = PL_IS_CV(O.dyn), cvnb = O.dyn == PL_DYN_CVNB;
+  // dx = [dq, dv] (whole body) or [dh, dq] with v = u[:nv] (centroidal_vel); without the
+  // base, v = [v_b(h, q, v_j), v_j] with u = [v_j | f]
   auto DQ = [&](int k) { return cv ? 6 + k : k; };
   auto U = [&](int k) { return ndx + k; };
   auto DV = [&](int k) { return cv ? ndx + k : nv + k; };
+  auto add_v = [&](std::vector<int>& s, int k) {
+    if (!cvnb) { s.push_back(DV(k)); return; }
+    if (k >= 6) { s.push_back(U(k - 6)); return; }
+    for (int c = 0; c < 6; ++c) s.push_back(c);
+    for (int c = 3; c < nv; ++c) s.push_back(DQ(c));
+    for (int c = 0; c < nj; ++c) s.push_back(U(c));
+  };
   auto DXN = [&](int k) { return nw + k; };
   const bool accf = O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA || O.dyn == PL_DYN_ACCNB;
-  const int f_off = (O.dyn == PL_DYN_RNEA || accf) ? O.na : (cv ? nv : nj);
+  const int f_off = (O.dyn == PL_DYN_RNEA || accf) ? O.na : (O.dyn == PL_DYN_CV ? nv : nj);
   auto F = [&](int k) { return U(f_off + k); };
   std::vector<int> dynset;  // dependency set of the RNEA / ABA / base-solve outputs
   for (int k = 3; k < nv; ++k) dynset.push_back(DQ(k));
@@ -232,8 +240,8 @@ std::vector<std::vector<int>> node_row_deps(const PlModel& M, const PlOcpConst& 
     std::vector<int> s;
     for (int k = 3; k < 6; ++k) s.push_back(DQ(k));
     for (int v : support_v(M, fr.joint)) s.push_back(DQ(v));
-    for (int k = 0; k < 6; ++k) s.push_back(DV(k));
-    for (int v : support_v(M, fr.joint)) s.push_back(DV(v));
+    for (int k = 0; k < 6; ++k) add_v(s, k);
+    for (int v : support_v(M, fr.joint)) add_v(s, v);
     return s;
   };
   std::vector<std::vector<int>> rows;
@@ -268,13 +276,13 @@ std::vector<std::vector<int>> node_row_deps(const PlModel& M, const PlOcpConst& 
         case PL_RB_EXT: s = {F(3 * O.nfeet + r)}; break;
         case PL_RB_ARM: s = frame_deps(O.arm); break;
         case PL_RB_QJ: s = {DQ(6 + r)}; break;
-        case PL_RB_VJ: s = {DV(6 + r)}; break;
+        case PL_RB_VJ: add_v(s, 6 + r); break;
         case PL_RB_CV_DYNH:  // h_dot(q, forces): orientation + joints, every force
           s = {r, DXN(r)};
           for (int k = 3; k < nv; ++k) s.push_back(DQ(k));
           for (int k = 0; k < nf; ++k) s.push_back(F(k));
           break;
-        case PL_RB_CV_DYNQ: s = {DQ(r), DV(r), DXN(6 + r)}; break;
+        case PL_RB_CV_DYNQ: s = {DQ(r), DXN(6 + r)}; add_v(s, r); break;
         case PL_RB_CV_GAP:  // A(q) v - m h
           s = {r};
           for (int k = 3; k < nv; ++k) s.push_back(DQ(k));
@@ -907,7 +915,7 @@ int build_jac_list(pl_ocp* o, std::vector<int2>& list) {
       if (lc >= nd.nw) {
         cheap = true;
       } else if (lc < O.ndx) {
-        cheap = O.dyn == PL_DYN_CV && lc < 6;
+        cheap = O.dyn == PL_DYN_CV && lc < 6;  // (without the base, h enters v_b: not cheap)
       } else {
         const int k = lc - O.ndx;
         cheap = O.dyn == PL_DYN_RNEA && k >= O.na + O.nf;
@@ -949,10 +957,6 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
                  "couple the RNEA rows to the next node; the reference notes the same for Fatrop)");
     return -1;
   }
-  if (d->dynamics == PL_DYN_CENTROIDAL_VEL && !d->include_base) {
-    pl_set_error("centroidal_vel requires include_base=True on this path (OCP_ARGS default, ocp_args.py:5)");
-    return -1;
-  }
   if (d->nodes < 2 || d->n_feet != 4) { pl_set_error("need nodes >= 2 and 4 feet"); return -1; }
   pl_ocp* o = new pl_ocp();
   PlOcpHandle& h = o->h;
@@ -964,6 +968,8 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   O.dyn = d->dynamics;
   // whole_body_acc / centroidal_acc without the base in u share the ACCNB rows
   if ((O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA) && !d->include_base) O.dyn = PL_DYN_ACCNB;
+  // centroidal_vel without the base velocity in u (the class default, ocp_centroidal_vel.py:9-23)
+  if (O.dyn == PL_DYN_CV && !d->include_base) O.dyn = PL_DYN_CVNB;
   O.N = d->nodes;
   O.nq = M.nq;
   O.nv = M.nv;
@@ -973,7 +979,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   const bool has_arm = d->arm_ee_frame >= 0;
   O.nf = 12 + (has_ext ? 3 : 0);
   O.nee = 4 + (has_ext ? 1 : 0);
-  const bool cv = (O.dyn == PL_DYN_CV);
+  const bool cv = PL_IS_CV(O.dyn);
   O.nx = cv ? 6 + M.nq : M.nq + M.nv;   // centroidal_vel: x = [h, q] (ocp_centroidal_vel.py:50-52)
   O.ndx = cv ? 6 + M.nv : 2 * M.nv;
   O.na = (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA) ? M.nv
@@ -1737,6 +1743,7 @@ void cas_u_split(const pl_ocp* o, int& na, int& nf, int& nt) {
   if (O.dyn == PL_DYN_RNEA) { na = O.na; nf = O.nf; nt = O.nj; }
   else if (O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA || O.dyn == PL_DYN_ACCNB) { na = O.na; nf = O.nf; nt = O.nj; }
   else if (O.dyn == PL_DYN_CV) { na = O.nv; nf = O.nf; nt = O.nj; }
+  else if (O.dyn == PL_DYN_CVNB) { na = O.nj; nf = O.nf; nt = O.nj; }
   else { na = 0; nf = O.nf; nt = O.nj; }
 }
 
@@ -1812,7 +1819,7 @@ extern "C" int pl_casadi_bind(pl_ocp* o, int retract_steps) {
   for (int j = 0; j < h.n; ++j) c.sp_H.push_back(j);
   int na, nf, nt;
   cas_u_split(o, na, nf, nt);
-  if (h.oc.dyn == PL_DYN_CV && retract_steps >= h.N) {
+  if (PL_IS_CV(h.oc.dyn) && retract_steps >= h.N) {
     pl_set_error("centroidal_vel retract needs node i + 1's velocities: retract_steps < N");
     c.o = nullptr;
     return -1;
@@ -2022,8 +2029,8 @@ extern "C" int retract_solution(const double** arg, double** res, casadi_int*, d
   int na, nf, nt;
   cas_u_split(o, na, nf, nt);
   const int ntau = (int)g_cas.sp_tau[1];
-  const bool cv = O.dyn == PL_DYN_CV;
-  std::vector<double> xs(O.nx), a(nv), tau(nv);
+  const bool cv = PL_IS_CV(O.dyn);
+  std::vector<double> xs(O.nx), a(nv), tau(nv), vfull(nv), vnext(nv);
   PlFrameRef F0;
   memset(&F0, 0, sizeof(F0));
   const double* p = o->h_params.data();
@@ -2039,13 +2046,24 @@ extern "C" int retract_solution(const double** arg, double** res, casadi_int*, d
     const double* q = cv ? xs.data() + 6 : xs.data();
     const double* v = cv ? u : xs.data() + nq;
     const double* f = u + (O.dyn == PL_DYN_ABA ? nj : na);
+    if (O.dyn == PL_DYN_CVNB) {  // v = [base_vel_dynamics(h, q, v_j), v_j] (ocp_centroidal_vel.py:228-235)
+      pl::dyn_eval(M, O, F0, PL_FN_BASE_VEL_CV, 0, xs.data(), q, u, nullptr, vfull.data());
+      for (int k = 0; k < nj; ++k) vfull[6 + k] = u[k];
+      v = vfull.data();
+    }
     switch (O.dyn) {
       case PL_DYN_ABA:
         pl::dyn_eval(M, O, F0, PL_FN_ABA, 0, q, v, u, f, a.data());
         break;
-      case PL_DYN_CV: {
+      case PL_DYN_CV:
+      case PL_DYN_CVNB: {
         const double dt = pl::node_dt(O, p, i);
         const double* un = arg[0] + o->nodes[i + 1].x_off + o->h.ndx;
+        if (O.dyn == PL_DYN_CVNB) {  // v_next from this node's h, q (ocp_centroidal_vel.py:240-246)
+          pl::dyn_eval(M, O, F0, PL_FN_BASE_VEL_CV, 0, xs.data(), q, un, nullptr, vnext.data());
+          for (int k = 0; k < nj; ++k) vnext[6 + k] = un[k];
+          un = vnext.data();
+        }
         for (int k = 0; k < nv; ++k) a[k] = (un[k] - v[k]) / dt;
         pl::dyn_eval(M, O, F0, PL_FN_BASE_ACC_CV, 0, q, v, a.data() + 6, f, a.data());
       } break;

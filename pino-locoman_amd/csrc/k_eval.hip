@@ -169,6 +169,7 @@ __global__ __launch_bounds__(256) void k_hess(PlDev d, int N, int n, int np) {
     case PL_DYN_CV: hipLaunchKernelGGL(KERNEL<PL_DYN_CV>, __VA_ARGS__); break;     \
     case PL_DYN_CA: hipLaunchKernelGGL(KERNEL<PL_DYN_CA>, __VA_ARGS__); break;     \
     case PL_DYN_ACCNB: hipLaunchKernelGGL(KERNEL<PL_DYN_ACCNB>, __VA_ARGS__); break; \
+    case PL_DYN_CVNB: hipLaunchKernelGGL(KERNEL<PL_DYN_CVNB>, __VA_ARGS__); break;   \
     default: hipLaunchKernelGGL(KERNEL<PL_DYN_ABA>, __VA_ARGS__); break;           \
   }
 
@@ -341,7 +342,7 @@ __global__ void k_mpc_finish(PlDev d, int B, int n, int nx) {
   double* xs = d.xstate + (size_t)b * nx;
   const double* dx1 = d.x + (size_t)b * n + d.nodes[1].x_off;
   double qn[PL_MAXQ];
-  if (O.dyn == PL_DYN_CV) {  // x = [h, q]: h + dh, integrate(q, dq) (dynamics_centroidal_vel.py:12-26)
+  if (PL_IS_CV(O.dyn)) {  // x = [h, q]: h + dh, integrate(q, dq) (dynamics_centroidal_vel.py:12-26)
     VecIn<double> acc{dx1 + 6, nullptr, 0.0, -1};
     pl::integrate_q<double>(M, xs + 6, acc, qn);
     for (int k = 0; k < 6; ++k) xs[k] += dx1[k];

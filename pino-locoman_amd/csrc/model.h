@@ -53,8 +53,12 @@ struct PlFrameRef {
 // Row-code dynamics kinds.  0-4 are also the public pl_ocp_desc codes (include_base
 // true); PL_DYN_ACCNB is internal: whole_body_acc and centroidal_acc with
 // include_base = False (u = [a_j | f], the base acceleration solved from the 6 base
-// equations), which share their rows.
-enum { PL_DYN_RNEA = 0, PL_DYN_ACC = 1, PL_DYN_ABA = 2, PL_DYN_CV = 3, PL_DYN_CA = 4, PL_DYN_ACCNB = 5 };
+// equations), which share their rows; PL_DYN_CVNB is internal too: centroidal_vel with
+// include_base = False (u = [v_j | f], the base velocity v_b = A_b^-1 (m h - A_j v_j)).
+enum { PL_DYN_RNEA = 0, PL_DYN_ACC = 1, PL_DYN_ABA = 2, PL_DYN_CV = 3, PL_DYN_CA = 4, PL_DYN_ACCNB = 5,
+       PL_DYN_CVNB = 6 };
+// centroidal_vel in either form: x = [h, q], dx = [dh, dq]
+#define PL_IS_CV(d) ((d) == PL_DYN_CV || (d) == PL_DYN_CVNB)
 
 // Row-block kinds, emitted per node in the reference's subject_to order
 // (optimization/ocp.py:103-190 + setup_dynamics_constraints of each subclass).

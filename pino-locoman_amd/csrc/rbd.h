@@ -560,14 +560,20 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
 //          over the contact frames FR, FL, RR, RL (+ the external-force frame).
 // Bodies are pushed to world coordinates as they are visited (as in tree_pass), so
 // only the running sums stay live.  want_h = false skips the velocity recursion.
-template <class S, class QR, class VA, class InF>
+// CI: also the CoM c -> cinfo[0, 3) and the composite rotational inertia about the CoM in
+// world axes -> cinfo[3, 9) = (xx, xy, xz, yy, yz, zz), for the base-velocity solve (a
+// compile-time switch, so the other instantiations compile exactly as without it).
+template <class S, class QR, class VA, class InF, bool CI = false>
 PL_HD void centroidal_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const QR& qrev, const VA& v,
-                           const InF& forces, bool want_h, bool want_hdot, S* hg, S* hdot) {
+                           const InF& forces, bool want_h, bool want_hdot, S* hg, S* hdot,
+                           S* cinfo = nullptr, std::integral_constant<bool, CI> = {}) {
   S R0[9];
   quat_to_R(qb + 3, R0);
   S p0[3] = {qb[0], qb[1], qb[2]};
-  S mc[3], H[6], pe[PL_MAXFEET + 1][3];
+  S mc[3], H[6], pe[PL_MAXFEET + 1][3], Io[CI ? 6 : 1];
   for (int k = 0; k < 3; ++k) mc[k] = S(0.0);
+  if constexpr (CI)
+    for (int k = 0; k < 6; ++k) Io[k] = S(0.0);
   for (int k = 0; k < 6; ++k) H[k] = S(0.0);
   for (int e = 0; e < PL_MAXFEET + 1; ++e)
     for (int k = 0; k < 3; ++k) pe[e][k] = S(0.0);
@@ -576,6 +582,23 @@ PL_HD void centroidal_pass(const PlModel& M, const PlOcpConst& O, const S* qb, c
     S lc[3];
     matvec(oR, M.lever[j], lc);
     for (int k = 0; k < 3; ++k) mc[k] += M.mass[j] * (op[k] + lc[k]);
+    if constexpr (CI) {  // inertia about the world origin: oR Ic oR^T + m (|p|^2 1 - p p^T)
+      S T[9], Iw[9], pj[3];
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+          T[3 * r + c] = oR[3 * r] * M.Ic[j][c] + oR[3 * r + 1] * M.Ic[j][3 + c] + oR[3 * r + 2] * M.Ic[j][6 + c];
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) Iw[3 * r + c] = T[3 * r] * oR[3 * c] + T[3 * r + 1] * oR[3 * c + 1] + T[3 * r + 2] * oR[3 * c + 2];
+      for (int k = 0; k < 3; ++k) pj[k] = op[k] + lc[k];
+      const S pp = pj[0] * pj[0] + pj[1] * pj[1] + pj[2] * pj[2];
+      const double mj = M.mass[j];
+      Io[0] += Iw[0] + mj * (pp - pj[0] * pj[0]);
+      Io[1] += Iw[1] - mj * pj[0] * pj[1];
+      Io[2] += Iw[2] - mj * pj[0] * pj[2];
+      Io[3] += Iw[4] + mj * (pp - pj[1] * pj[1]);
+      Io[4] += Iw[5] - mj * pj[1] * pj[2];
+      Io[5] += Iw[8] + mj * (pp - pj[2] * pj[2]);
+    }
     if (want_h) {
       S hl[6], hw[6];
       inertia_mul(M.mass[j], M.lever[j], M.Ic[j], vj, hl);
@@ -632,6 +655,16 @@ PL_HD void centroidal_pass(const PlModel& M, const PlOcpConst& O, const S* qb, c
   const double m = M.total_mass;
   S com[3];
   for (int k = 0; k < 3; ++k) com[k] = mc[k] * (1.0 / m);
+  if constexpr (CI) {  // parallel axis to the CoM: I_c = I_o - m (|c|^2 1 - c c^T)
+    const S cc = com[0] * com[0] + com[1] * com[1] + com[2] * com[2];
+    for (int k = 0; k < 3; ++k) cinfo[k] = com[k];
+    cinfo[3] = Io[0] - m * (cc - com[0] * com[0]);
+    cinfo[4] = Io[1] + m * com[0] * com[1];
+    cinfo[5] = Io[2] + m * com[0] * com[2];
+    cinfo[6] = Io[3] - m * (cc - com[1] * com[1]);
+    cinfo[7] = Io[4] + m * com[1] * com[2];
+    cinfo[8] = Io[5] - m * (cc - com[2] * com[2]);
+  }
   if (want_h) {  // shift the angular momentum from the world origin to the CoM
     S cxl[3];
     cross3(com, H, cxl);
@@ -650,6 +683,31 @@ PL_HD void centroidal_pass(const PlModel& M, const PlOcpConst& O, const S* qb, c
     }
     for (int k = 0; k < 3; ++k) { hdot[k] = dp[k] * (1.0 / m); hdot[3 + k] = dl[k] * (1.0 / m); }
   }
+}
+
+// base_vel_dynamics (dynamics_centroidal_vel.py:73-89): v_b = A_b^-1 (m h - A_j v_j).  A_b
+// maps the local base twist to the momentum of the robot moving rigidly with the base:
+// linear m (R0 v + w_w x (c - p0)), angular I_c w_w (w_w = R0 w).  hj = A_j v_j (the
+// momentum at zero base velocity), ci = centroidal_pass's cinfo.
+template <class S>
+PL_HD void base_vel_solve(double m, const S* R0, const S* p0, const S* ci, const S* h, const S* hj, S* vb) {
+  S b[6];
+  for (int k = 0; k < 6; ++k) b[k] = m * h[k] - hj[k];
+  const S* I = ci + 3;  // xx xy xz yy yz zz
+  const S l00 = sqrt_s(I[0]);
+  const S l10 = I[1] / l00, l20 = I[2] / l00;
+  const S l11 = sqrt_s(I[3] - l10 * l10);
+  const S l21 = (I[4] - l20 * l10) / l11;
+  const S l22 = sqrt_s(I[5] - l20 * l20 - l21 * l21);
+  const S y0 = b[3] / l00, y1 = (b[4] - l10 * y0) / l11, y2 = (b[5] - l20 * y0 - l21 * y1) / l22;
+  const S w2 = y2 / l22, w1 = (y1 - l21 * w2) / l11, w0 = (y0 - l10 * w1 - l20 * w2) / l00;
+  const S ww[3] = {w0, w1, w2};
+  S d[3], wxd[3], lin[3];
+  for (int k = 0; k < 3; ++k) d[k] = ci[k] - p0[k];
+  cross3(ww, d, wxd);
+  for (int k = 0; k < 3; ++k) lin[k] = b[k] * (1.0 / m) - wxd[k];
+  mattvec(R0, lin, vb);
+  mattvec(R0, ww, vb + 3);
 }
 
 // ---------------------------------------------------------------- base from the base rows

@@ -43,7 +43,7 @@ PL_HD int node_nu(const PlOcpConst& O, int i) {
   if (O.dyn == PL_DYN_RNEA) return O.na + O.nf + (i < O.tau_nodes ? O.nj : 0);
   if (O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA || O.dyn == PL_DYN_ACCNB) return O.na + O.nf;
   if (O.dyn == PL_DYN_CV) return O.nv + O.nf;
-  return O.nj + O.nf;
+  return O.nj + O.nf;  // aba: [tau_j | f]; centroidal_vel without the base: [v_j | f]
 }
 
 
@@ -122,7 +122,8 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
                      const VecIn<S>& u, const VecIn<S>& dxn, Emit& emit, S* kstore, int kstride,
                      double* kvals = nullptr, const double* aba_sh = nullptr) {
   const int nv = O.nv, nq = O.nq, nj = O.nj;
-  constexpr bool CV = (DYN == PL_DYN_CV);
+  constexpr bool CV = PL_IS_CV(DYN);
+  constexpr bool CVNB = (DYN == PL_DYN_CVNB);  // v = [base_vel_dynamics(h, q, v_j), v_j]
   const double* xi = p + O.P.x_init;
   const double dt = node_dt(O, p, i);
   const int type = node_type(O, i);
@@ -134,15 +135,35 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
   S qb[7];
   integrate_ff<S>(xq, dq, qb);
   const RevQ<S, VecIn<S>> qrev{xq, dq};
+  // centroidal_vel without the base: one centroidal pass at v = [0, v_j] gives A_j v_j,
+  // h_dot, the CoM and the composite inertia, then v_b = A_b^-1 (m h - A_j v_j)
+  // (ocp_centroidal_vel.py:119-129, dynamics_centroidal_vel.py:73-89)
+  S vnb[CVNB ? PL_MAXV : 1], hdot_nb[CVNB ? 6 : 1];
+  if constexpr (CVNB) {
+    bool run = true;
+    if constexpr (!std::is_same<S, double>::value) run = !(dxn.seed >= 0 && dxn.seed < O.ndx);
+    if (run) {
+      S hj[6], ci[9], hcur[6], R0[9];
+      centroidal_pass<S>(M, O, qb, qrev, ZeroBaseAcc<S>{u}, sub_in(u, nj), true, true, hj, hdot_nb, ci,
+                         std::true_type{});
+      for (int k = 0; k < 6; ++k) hcur[k] = xi[k] + dx[k];
+      quat_to_R(qb + 3, R0);
+      base_vel_solve(M.total_mass, R0, qb, ci, hcur, hj, vnb);
+    } else {
+      for (int k = 0; k < 6; ++k) { vnb[k] = S(0.0); hdot_nb[k] = S(0.0); }
+    }
+    for (int k = 0; k < nj; ++k) vnb[6 + k] = u[k];
+  }
   const auto vel = [&]() {
-    if constexpr (CV) return u;
+    if constexpr (CVNB) return static_cast<const S*>(vnb);
+    else if constexpr (CV) return u;
     else return VelAcc<S, VecIn<S>>{xi + nq, sub_in(dx, nv)};
   }();
   // acc family: whole_body_acc (ACC), centroidal_acc (CA), their include_base = False form (ACCNB)
   constexpr bool ACCF = (DYN == PL_DYN_ACC || DYN == PL_DYN_CA || DYN == PL_DYN_ACCNB);
   constexpr bool NB = (DYN == PL_DYN_ACCNB);
   constexpr bool COMP = (DYN == PL_DYN_CA || DYN == PL_DYN_ACCNB);
-  const int f_off = (DYN == PL_DYN_RNEA || ACCF) ? O.na : (CV ? nv : nj);
+  const int f_off = (DYN == PL_DYN_RNEA || ACCF) ? O.na : (DYN == PL_DYN_CV ? nv : nj);
   const VecIn<S> a = u;                                   // rnea / acc: a = u[0:nv]
   const VecIn<S> forces = sub_in(u, f_off);
   const VecIn<S> tau_j = sub_in(u, DYN == PL_DYN_RNEA ? O.na + O.nf : 0);
@@ -176,10 +197,11 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
   if constexpr (!std::is_same<S, double>::value) {
     const bool seed_dxn = dxn.seed >= 0 && dxn.seed < O.ndx;
     const bool seed_tau = DYN == PL_DYN_RNEA && u.seed >= O.na + O.nf && u.seed < O.na + O.nf + nj;
-    const bool seed_h = CV && dx.seed >= 0 && dx.seed < 6;
-    const bool seed_f = CV && u.seed >= nv && u.seed < nv + O.nf;
+    // (without the base, h enters the kinematics through v_b; its centroidal pass ran above)
+    const bool seed_h = DYN == PL_DYN_CV && dx.seed >= 0 && dx.seed < 6;
+    const bool seed_f = CV && u.seed >= f_off && u.seed < f_off + O.nf;
     tree = !(seed_dxn || seed_tau || seed_h || seed_f);
-    cen = CV && !(seed_dxn || seed_h);
+    cen = DYN == PL_DYN_CV && !(seed_dxn || seed_h);
   }
   S comp[COMP ? 15 : 1];
   S aba_a[DYN == PL_DYN_ABA ? PL_MAXV : 1];
@@ -237,7 +259,9 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
     }
   }
   S hg[CV ? 6 : 1], hdot[CV ? 6 : 1];
-  if constexpr (CV) {
+  if constexpr (CVNB) {
+    for (int k = 0; k < 6; ++k) hdot[k] = hdot_nb[k];
+  } else if constexpr (CV) {
     if (cen) {
       centroidal_pass<S>(M, O, qb, qrev, vel, forces, true, true, hg, hdot);
     } else {

@@ -15,7 +15,7 @@ namespace pl {
 
 PL_HD void compute_dx_des(const PlModel& M, const PlOcpConst& O, const double* p, double* dxd) {
   const double* xi = p + O.P.x_init;
-  if (O.dyn == PL_DYN_CV) {
+  if (PL_IS_CV(O.dyn)) {
     // x_des = [base_vel_des, q0], dx_des = [h_des - h, difference(q, q0)] (ocp_centroidal_vel.py:61-63)
     for (int k = 0; k < 6; ++k) dxd[k] = p[O.P.base_vel_des + k] - xi[k];
     difference_q(M, xi + 6, O.q0, dxd + 6);

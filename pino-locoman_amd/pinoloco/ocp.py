@@ -60,12 +60,14 @@ class Layout:
         self.ndx = 2 * self.nv
         nv, nj, nf = self.nv, self.nj, self.nf
         if dynamics == "centroidal_vel":
-            # x = [h (6), q], dx = [dh, dq], u = [v | f] (ocp_centroidal_vel.py:49-66)
+            # x = [h (6), q], dx = [dh, dq], u = [v | f] or, without the base, [v_j | f]
+            # (ocp_centroidal_vel.py:19-23, 49-66)
             self.nx, self.ndx = 6 + self.nq, 6 + nv
             self.tau_nodes = 0
             self.na = 0
-            self.nu = [nv + nf] * nodes
-            self.f_idx, self.tau_idx = nv, None
+            self.nv_opt = nv if include_base else nj
+            self.nu = [self.nv_opt + nf] * nodes
+            self.f_idx, self.tau_idx = self.nv_opt, None
         elif dynamics == "whole_body_rnea":
             self.tau_nodes = tau_nodes
             self.na = nv
@@ -135,7 +137,7 @@ def default_weights(robot, dynamics, layout):
     Q = np.array(Qb + Qj + Qv, float)
     if dynamics == "centroidal_vel":  # ocp_centroidal_vel.py:23-47
         Q = np.array([1000] * 6 + Qb + Qj, float)
-        R = np.array([1] * robot.nv + [1e-3] * nf, float)
+        R = np.array([1] * layout.nv_opt + [1e-3] * nf, float)
     elif dynamics == "whole_body_rnea":
         R = np.array([1e-3] * layout.na + [1e-3] * nf + [1e-4] * nj, float)
     elif dynamics in ("whole_body_acc", "centroidal_acc"):
@@ -447,7 +449,7 @@ class OCP:
         if self.dynamics in ("whole_body_acc", "centroidal_acc"):
             return np.concatenate([np.zeros(self.na_opt), f])
         if self.dynamics == "centroidal_vel":
-            return np.concatenate([np.zeros(self.nv), f])
+            return np.concatenate([np.zeros(self.layout.nv_opt), f])
         return np.concatenate([np.zeros(self.nj), f])
 
     def set_weights(self):
@@ -505,7 +507,7 @@ class OCP:
                 if self.dynamics == "whole_body_aba":
                     u = np.concatenate([u_prev[:self.nj], f_des])
                 elif self.dynamics == "centroidal_vel":  # ocp_centroidal_vel.py:152-158
-                    u = np.concatenate([u_prev[:self.nv], f_des])
+                    u = np.concatenate([u_prev[:self.layout.nv_opt], f_des])
                 else:
                     u = np.concatenate([u_prev[:self.na_opt], f_des])
                     if self.dynamics == "whole_body_rnea" and i < self.tau_nodes:
@@ -596,14 +598,13 @@ class OCPWholeBodyABA(OCP):
 
 
 class OCPCentroidalVel(OCP):
-    """ocp_centroidal_vel.py: x = [h, q], dx = [dh, dq], u = [v | forces]."""
+    """ocp_centroidal_vel.py: x = [h, q], dx = [dh, dq], u = [v | forces] or, with
+    include_base=False (the class default), u = [v_j | forces] and the base velocity
+    v_b = A_b^-1 (m h - A_j v_j) inside the rows (ocp_centroidal_vel.py:119-129)."""
 
     def __init__(self, robot, solver, nodes, include_base=False):
-        if not include_base:
-            raise ValueError("centroidal_vel with include_base=False (base velocity from A_b^-1, "
-                             "ocp_centroidal_vel.py:118-127) is not on the MI355X path; OCP_ARGS uses True")
         super().__init__(robot, solver, nodes, "centroidal_vel", include_base=include_base)
-        self.nv_opt = self.nv
+        self.nv_opt = self.layout.nv_opt
 
     def retract_stacked_sol(self, sol_x, retract_all=True):
         """ocp_centroidal_vel.py:195-260: q, h from the state; v from the inputs; a by a
@@ -619,15 +620,23 @@ class OCPCentroidalVel(OCP):
         self.U_prev = [np.array(u) for u in U]
         dts = self.dts
         base_acc = self.dyn.base_acc_dynamics(self.ext_force_frame)
+        base_vel = self.dyn.base_vel_dynamics()
+        nvo = self.nv_opt
         for i in range(self.nodes):
             if not (i == 0 or retract_all):
                 continue
             xs = integ(x_init, DX[i])
-            q = xs[6:]
+            h, q = xs[:6], xs[6:]
             u = U[i]
-            v, forces = u[:self.nv], u[self.f_idx:]
+            forces = u[self.f_idx:]
+
+            def vel(uu):  # v from the inputs; without the base, v_b at this node's h, q (:228-246)
+                if self.include_base:
+                    return np.asarray(uu[:nvo], float)
+                return np.concatenate([np.asarray(base_vel(h, q, uu[:nvo]), float).ravel(), uu[:nvo]])
+            v = vel(u)
             k = i if i + 1 < self.nodes else i - 1
-            a = (U[k + 1][:self.nv] - U[k][:self.nv]) / dts[k]
+            a = (vel(U[k + 1]) - vel(U[k])) / dts[k]
             a_b = base_acc(q, v, a[6:], forces)
             self.q_sol.append(q)
             self.v_sol.append(v)

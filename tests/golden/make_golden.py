@@ -70,6 +70,10 @@ SQP_CONFIGS = [
      {"include_base": False}),
     ("b2g_ca_n50", "b2g", "centroidal_acc", 50, [("syn", 0)], 1, "trot", {}, 1, {"include_base": True}),
     ("b2g_acc_nb_n50", "b2g", "whole_body_acc", 50, [("syn", 0)], 1, "trot", {}, 1, {"include_base": False}),
+    # centroidal_vel without the base velocity in u (the OCPCentroidalVel default,
+    # ocp_centroidal_vel.py:9-23, 119-129): v_b = A_b^-1 (m h - A_j v_j) inside the rows
+    ("go2_cv_nb_n20", "go2", "centroidal_vel", 20, [("syn", k) for k in range(4)], 3, "trot", {}, 2,
+     {"include_base": False}),
 ]
 
 # Interior-point (Fatrop branch) fixtures: name, robot, dynamics, N, problems, closed-loop

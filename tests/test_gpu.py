@@ -35,7 +35,9 @@ EDGE = [(f"go2_rnea_n20_{k}", "go2", "whole_body_rnea", 20) for k in ("walk", "s
 # False (base acceleration from the base equations) and centroidal_acc's gap A a + dA v - dh
 ACCF = [("go2_acc_nb_n20", "go2", "whole_body_acc", 20), ("go2_ca_n20", "go2", "centroidal_acc", 20),
         ("go2_ca_nb_n20", "go2", "centroidal_acc", 20), ("b2g_ca_n50", "b2g", "centroidal_acc", 50),
-        ("b2g_acc_nb_n50", "b2g", "whole_body_acc", 50)]
+        ("b2g_acc_nb_n50", "b2g", "whole_body_acc", 50),
+        # centroidal_vel with include_base=False (v_b = A_b^-1 (m h - A_j v_j) in the rows)
+        ("go2_cv_nb_n20", "go2", "centroidal_vel", 20)]
 
 
 def _rel(a, b):
@@ -136,7 +138,8 @@ def test_fixture_coverage():
     assert gaits == {"trot", "walk", "stand"} and trace > 0
 
 
-@pytest.mark.parametrize("name,rname,dyn,N", [CONFIGS[0], CONFIGS[1], EDGE[0], EDGE[1], EDGE[4], ACCF[0], ACCF[1]])
+@pytest.mark.parametrize("name,rname,dyn,N", [CONFIGS[0], CONFIGS[1], EDGE[0], EDGE[1], EDGE[4], ACCF[0], ACCF[1],
+                                               ACCF[5]])
 def test_device_mpc_loop_matches_oracle_loop(name, rname, dyn, N):
     """run_mpc.py:127-143 executed on the device (gait, x_init, warm start, solve,
     x <- integrate(x, DX[1])) vs the oracle's closed loop in the golden file: states
@@ -407,3 +410,34 @@ def test_make_ocp_centroidal_acc_surface():
     q0, v0 = ocp.q_sol[0], ocp.v_sol[0]
     ab = ocp.dyn.base_acc_dynamics(R.ext_force_frame)(q0, v0, a0[6:], ocp.forces_sol[0])
     assert np.abs(a0[:6] - ab).max() <= 1e-12 * max(1.0, np.abs(ab).max())
+
+
+def test_make_ocp_centroidal_vel_nb_surface():
+    """make_ocp("centroidal_vel", include_base=False) -- the OCPCentroidalVel default
+    (ocp_centroidal_vel.py:9-23): the GPU solve of the fixture problem; the retract's
+    v = [base_vel_dynamics(h, q, v_j), v_j] reproduces the momentum, A(q) v = m h, and
+    a = [base_acc_dynamics(q, v, a_j, f), a_j] (ocp_centroidal_vel.py:224-253)."""
+    from oracle import rbd
+    from pinoloco.ocp import OCP_ARGS, make_ocp
+    from pinoloco.synthetic import DT_MAX, DT_MIN
+    G = golden("sqp_go2_cv_nb_n20.npz")
+    R = make_robot("go2")
+    ocp = make_ocp("centroidal_vel", OCP_ARGS["centroidal_vel"], robot=R, solver="osqp", nodes=20,
+                   include_base=False)
+    ocp.set_time_params(DT_MIN, DT_MAX)  # the fixture's step sizes (for the retract's dts)
+    ocp.param_vector = lambda: G["P"][0]
+    ocp._x_initial = G["X"][0].copy()
+    ocp.p["x_init"] = G["XS"][0]
+    ocp.init_solver()
+    x = ocp.solve()
+    assert ocp.stats["status"] == int(G["status"][0])
+    assert _rel(x, G["x_new"][0]) <= 2e-7
+    M = rbd.ModelArrays(R.model)
+    q0, v0, f0 = ocp.q_sol[0], ocp.v_sol[0], ocp.forces_sol[0]
+    h0 = G["XS"][0][:6] + ocp.DX_prev[0][:6]
+    assert v0.shape == (R.nv,)
+    hg = rbd.centroidal_momentum(M, q0, v0)
+    assert np.abs(hg - R.mass * h0).max() <= 1e-10 * max(1.0, np.abs(hg).max())
+    a_j = (ocp.U_prev[1][:R.nj] - ocp.U_prev[0][:R.nj]) / ocp.dts[0]
+    a_b = rbd.base_acc_cv(M, list(R.foot_frames), q0, v0, a_j, f0, R.mass)
+    assert _rel(ocp.a_sol[0], np.concatenate([a_b, a_j])) < 1e-10

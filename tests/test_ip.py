@@ -37,9 +37,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # Trajectories that amplify 1e-12 differences of the Newton directions into different
 # filter / fraction-to-boundary decisions within the 10 iterations (the cold, infeasible
 # centroidal start: measured x 2.4e-6 after 10 steps, and a different final status once
-# the device sin / cos changed in the last bit).  Their per-iteration directions are
-# pinned by test_ip_gpu_teacher_forced_directions instead.
-CHAOTIC = {("ip_go2_cv_n20", 1)}
+# the device sin / cos changed in the last bit).  Both cold centroidal_vel starts are: two
+# builds of the same sources whose inlining differs give Jacobians 7e-17 apart and problem
+# 0's step sizes then differ by 0.08 after 10 iterations (r02e, tools/gpu_bits.py).  Their
+# per-iteration directions are pinned by test_ip_gpu_teacher_forced_directions instead.
+CHAOTIC = {("ip_go2_cv_n20", 0), ("ip_go2_cv_n20", 1)}
 
 
 def _rel(a, b):
@@ -181,7 +183,8 @@ def test_make_ocp_fatrop_surface():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,rname,dyn,N,b", [("ip_go2_cv_n20", "go2", "centroidal_vel", 20, 1),
+@pytest.mark.parametrize("name,rname,dyn,N,b", [("ip_go2_cv_n20", "go2", "centroidal_vel", 20, 0),
+                                                ("ip_go2_cv_n20", "go2", "centroidal_vel", 20, 1),
                                                 ("ip_go2_rnea_n20", "go2", "whole_body_rnea", 20, 0)])
 def test_ip_gpu_teacher_forced_directions(name, rname, dyn, N, b):
     """Every iteration's Newton direction from the ORACLE's iterate (teacher forcing): dx,

@@ -204,3 +204,36 @@ def test_rho_classification_independent_of_scaling_step(name, rname, dyn, N):
     margin = min((w[two] * E[two]).min() for E in Es) / RHO_TOL
     print(f"{name}: narrowest scaled two-sided row = {margin:.3g} x RHO_TOL")
     assert margin > 10.0
+
+
+def test_centroidal_vel_without_base_momentum_identity():
+    """centroidal_vel with include_base=False (ocp_centroidal_vel.py:119-129): the rows use
+    v = [base_vel_dynamics(h, q, v_j), v_j], which reproduces the momentum A(q) v = m h, so
+    the include_base form's gap rows vanish there; no gap rows, u = [v_j | f]; the fixture
+    evaluates (g, grad, f) the same way."""
+    R = make_robot("go2")
+    o = OracleOCP(R, "centroidal_vel", 20, include_base=False)
+    ob = OracleOCP(R, "centroidal_vel", 20, include_base=True)
+    assert o.nu[0] == R.nj + R.nf and ob.nu[0] == R.nv + R.nf
+    G = golden("sqp_go2_cv_nb_n20.npz")
+    x, p = G["X"][1], G["P"][1]
+    g, lbg, ubg = o.eval_g(x, p)
+    np.testing.assert_allclose(g, G["g"][1], rtol=1e-12, atol=1e-10)
+    P = o.unpack(p)
+    DX, U = o.split(x)
+    rng = np.random.default_rng(3)
+    for i in (0, 7):
+        dx = DX[i] + rng.normal(0, 0.05, o.ndx)
+        h, q = o.state(dx, P)
+        v_j = U[i][:R.nj] + rng.normal(0, 0.3, R.nj)
+        v = np.concatenate([rbd.base_vel_cv(o.M, h, q, v_j, o.mass), v_j])
+        hg = rbd.centroidal_momentum(o.M, q, v)
+        np.testing.assert_allclose(hg, o.mass * h, rtol=1e-12, atol=1e-12)
+        rows_nb = sum(r[0].shape[-1] for r in o.node_rows(i, dx, U[i], DX[i + 1], P))
+        ub = np.concatenate([v, U[i][R.nj:]])
+        rows_b = ob.node_rows(i, dx, ub, DX[i + 1], P)
+        assert rows_nb == sum(r[0].shape[-1] for r in rows_b) - 6
+        # the include_base form's gap row block (after the 6 + nv dynamics rows) is 0 at this v
+        gap = rows_b[2][0]
+        assert gap.shape[-1] == 6
+        assert np.abs(gap).max() < 1e-10 * max(1.0, o.mass * np.abs(h).max())

@@ -56,6 +56,9 @@ def _consts(bo):
     ("go2", "centroidal_acc", 20, [0, 1, 7, 19], {"include_base": True}),
     ("b2g", "centroidal_acc", 50, [0, 30], {"include_base": True}),
     ("go2", "centroidal_acc", 20, [0, 12], {"include_base": False}),
+    # centroidal_vel without the base: v_b = A_b^-1 (m h - A_j v_j) inside the rows
+    ("go2", "centroidal_vel", 20, [0, 1, 9, 19], {"include_base": False}),
+    ("b2", "centroidal_vel", 20, [0, 10], {"include_base": False}),
 ])
 def test_node_rows_and_dual_jacobian(harness, rname, dyn, N, nodes_checked, kw):
     from pinoloco.ocp import BatchedOCP
