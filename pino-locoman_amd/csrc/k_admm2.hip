@@ -67,7 +67,7 @@ __device__ __forceinline__ void lds_barrier() {
 struct AdmmLds2 {
   int prog_dbl;
   int per_prob;
-  int v, y, xn, r1, red, segn, colp, trow, zero, asb, asb_cap;
+  int v, y, xn, r1, red, segn, colp, trow, zero, asb, asb_cap, accn;
 };
 
 }  // namespace
@@ -104,6 +104,12 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
   double* colp = W + lm.colp;
   double* part = W + lm.red;
   double* trow = W + lm.trow;
+  // PL_ADMM_ATOMIC: per-wave LDS f64-add accumulators (the mat-vec outputs, then the row
+  // and column sums); the two waves' halves are added in a fixed order, so the sums stay
+  // deterministic
+  double* acch = W + lm.red + lm.accn * h;
+  double* acc0 = W + lm.red;
+  double* acc1 = W + lm.red + lm.accn;
   double* asb = W + lm.asb;
   double* zslot = W + lm.zero;
   if (lane == 0 && h == 0) *zslot = 0.0;
@@ -218,6 +224,10 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
     const unsigned km = an[i].kmagic;
     const double2* v2 = reinterpret_cast<const double2*>(v);
     if (act) {
+#if PL_ADMM_ATOMIC
+      for (int o = lane; o < 5 * T; o += 64) acch[o] = 0.0;
+      wsync();
+#else
       // zero the segments of every tile row the lane's run touches (the other wave may
       // own that row's tiles of this lane)
       {
@@ -233,9 +243,20 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
           }
         }
       }
+#endif
       int curI = -1;
       double sa[4] = {0.0, 0.0, 0.0, 0.0};
       bool use_tt = false;
+      auto emit_row = [&](int I0) __attribute__((always_inline)) {
+#if PL_ADMM_ATOMIC
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lds_add(acch + I0 * 5 + r, sa[r]);
+#else
+        double2* sp = reinterpret_cast<double2*>(segh + (lane + I0) * 4);
+        sp[0] = make_double2(sa[0], sa[1]);
+        sp[1] = make_double2(sa[2], sa[3]);
+#endif
+      };
       auto pass = [&](int j0, bool last_pass) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < KH; ++k) {
@@ -272,16 +293,18 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
                 cp[2] += R.s[k][2 * r + 1].x * vi[r];
                 cp[3] += R.s[k][2 * r + 1].y * vi[r];
               }
+#if PL_ADMM_ATOMIC
+              (void)cidx;
+#pragma unroll
+              for (int c = 0; c < 4; ++c) lds_add(acch + J * 5 + c, cp[c]);
+#else
               double2* cpp = reinterpret_cast<double2*>(colp + cidx * 4);
               cpp[0] = make_double2(cp[0], cp[1]);
               cpp[1] = make_double2(cp[2], cp[3]);
+#endif
             }
             if (I != curI) {
-              if (curI >= 0) {
-                double2* sp = reinterpret_cast<double2*>(segh + (lane + curI) * 4);
-                sp[0] = make_double2(sa[0], sa[1]);
-                sp[1] = make_double2(sa[2], sa[3]);
-              }
+              if (curI >= 0) emit_row(curI);
               curI = I;
 #pragma unroll
               for (int r = 0; r < 4; ++r) sa[r] = rp[r];
@@ -307,13 +330,16 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
           pass(j0, j0 + KH >= nh);
         }
       }
-      if (curI >= 0) {
-        double2* sp = reinterpret_cast<double2*>(segh + (lane + curI) * 4);
-        sp[0] = make_double2(sa[0], sa[1]);
-        sp[1] = make_double2(sa[2], sa[3]);
-      }
+      if (curI >= 0) emit_row(curI);
     }
     lds_barrier();
+#if PL_ADMM_ATOMIC
+    (void)km;
+    if (act && cl < nw) {
+      const int o = (cl >> 2) * 5 + (cl & 3);
+      y[cl] = acc0[o] + acc1[o];
+    }
+#else
     if (act && cl < nw) {
       const int I = cl >> 2, r = cl & 3;
       const int t0 = I * (I + 1) / 2;
@@ -323,6 +349,7 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
       const double cs = lds_sum(colp + r, cb, cb + T - 1 - I, 4, zslot);
       y[cl] = rs + cs;
     }
+#endif
     lds_barrier();
   };
 
@@ -481,6 +508,11 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
           const uint8_t* rowc = reinterpret_cast<const uint8_t*>(P + an[i].rowc);
           const uint32_t* rch = reinterpret_cast<const uint32_t*>(P + an[i].rch);
           const int rchn = an[i].rchn;
+#if PL_ADMM_ATOMIC
+          const uint8_t* rchr = reinterpret_cast<const uint8_t*>(P + an[i].rchr);
+          for (int o = lane; o < an[i].nrow; o += 64) acch[o] = 0.0;
+          wsync();
+#endif
           for (int c0 = 0; c0 < rchn; c0 += 128) {
             const int ch = c0 + cl;
             const uint32_t cw = rch[min(ch, rchn - 1)];
@@ -492,7 +524,11 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
               const double t = A(rowe[qq]) * y[rowc[qq]];
               a += k < len ? t : 0.0;
             }
+#if PL_ADMM_ATOMIC
+            if (ch < rchn) lds_add(acch + rchr[ch], a);
+#else
             if (ch < rchn) part[ch] = a;
+#endif
           }
         });
         prefetch_LR(kind1, i1, LRn);
@@ -506,8 +542,13 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
         for (int j = 0; j < 2; ++j) {
           const int r = lane + 64 * (2 * j + h);
           if (r < nrow) {
+#if PL_ADMM_ATOMIC
+            (void)rcp;
+            const double zt = acc0[r] + acc1[r];
+#else
             const int k0 = P[rcp + r], k1 = P[rcp + r + 1];
             const double zt = lds_sum<4>(part, k0, k1, 1, zslot);
+#endif
             const double zrel = alpha * zt + (1.0 - alpha) * LR.z[j];
             double zn = zrel + (1.0 / LR.rho[j]) * LR.y[j];
             zn = fmin(fmax(zn, LR.l[j]), LR.u[j]);
@@ -527,6 +568,11 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
           const uint8_t* colr = reinterpret_cast<const uint8_t*>(P + an[i].colr);
           const uint32_t* cch = reinterpret_cast<const uint32_t*>(P + an[i].cch);
           const int cchn = an[i].cchn;
+#if PL_ADMM_ATOMIC
+          const uint8_t* cchc = reinterpret_cast<const uint8_t*>(P + an[i].cchc);
+          for (int o = lane; o < an[i].ncol; o += 64) acch[o] = 0.0;
+          wsync();
+#endif
           for (int c0 = 0; c0 < cchn; c0 += 128) {
             const int ch = c0 + cl;
             const uint32_t cw = cch[min(ch, cchn - 1)];
@@ -538,7 +584,11 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
               const double t = A(e) * trow[colr[e]];
               a += k < len ? t : 0.0;
             }
+#if PL_ADMM_ATOMIC
+            if (ch < cchn) lds_add(acch + cchc[ch], a);
+#else
             if (ch < cchn) part[ch] = a;
+#endif
           }
         });
       }
@@ -550,11 +600,20 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
         pxa = xnew;
         pdx = xnew - LC.x;
         double acc = sigma * xnew - LC.q;
+#if PL_ADMM_ATOMIC
+        (void)ccp0;
+        acc += acc0[cl] + acc1[cl];
+#else
         const int k0 = P[ccp0 + cl], k1 = P[ccp0 + cl + 1];
         acc += lds_sum<4>(part, k0, k1, 1, zslot);
+#endif
         if (cl < ndx) {
+#if PL_ADMM_ATOMIC
+          const double a2 = acc0[nw + cl] + acc1[nw + cl];
+#else
           const int f0 = P[ccp0 + nw + cl], f1 = P[ccp0 + nw + cl + 1];
           const double a2 = lds_sum<4>(part, f0, f1, 1, zslot);
+#endif
           prn = rkeep + a2;
           if (i == 0) r1[cl] = prn;
         }
@@ -657,9 +716,19 @@ AdmmCfg2 admm2_config(const PlOcpHandle* h) {
   // partials | row / column chunk sums and rho z - y
   lm.red = o;
   lm.segn = (64 + T) * 4;
+#if PL_ADMM_ATOMIC
+  // [acc0 | acc1 | rho z - y]: per-wave accumulators of the mat-vec (5 T) and of the
+  // row / column sums, then trow
+  lm.accn = up2(std::max(5 * T, std::max(std::max(h->nrow_max, h->ncol_max), 1)));
+  lm.colp = o;
+  lm.trow = o + 2 * lm.accn;
+  o += up2(std::max(2 * lm.accn + h->nrow_max, 128));
+#else
+  lm.accn = 0;
   lm.colp = o + 2 * lm.segn;
   lm.trow = o + up2(h->chunk_max);
   o += up2(std::max(std::max(2 * lm.segn + T * (T - 1) / 2 * 4, up2(h->chunk_max) + h->nrow_max), 128));
+#endif
   lm.asb = o;
   c.ppw = h->B >= 1024 ? 4 : (h->B >= 512 ? 2 : 1);
   const int budget = 160 * 1024 / 8;
