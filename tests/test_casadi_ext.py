@@ -145,3 +145,48 @@ def test_retract_solution_dynamics_outputs(dyn):
             assert np.abs(tau[i] - want_t).max() < 1e-12 * max(1, np.abs(want_t).max())
     casadi_ext.unbind()
     bo.close()
+
+
+@pytest.mark.gpu
+def test_retract_solution_centroidal_vel_without_base():
+    """retract_solution of centroidal_vel with include_base=False (ocp_centroidal_vel.py:
+    284-318): v = [base_vel_dynamics(h, q, v_j), v_j], the next node's v_b at this node's
+    h, q, a = [base_acc_dynamics(q, v, a_j, f), a_j] with the finite-difference a_j, and
+    tau the RNEA joint rows; against the oracle."""
+    from oracle import rbd
+    from oracle.ocp import OracleOCP
+    from pinoloco import casadi_ext
+    from pinoloco.gait import horizon_dts
+    from pinoloco.ocp import BatchedOCP
+    from pinoloco.synthetic import DT_MAX, DT_MIN, build_batch
+    R = make_robot("go2")
+    N = 6
+    _, P, _, _, _ = build_batch(R, "centroidal_vel", N, 1, 0, include_base=False)
+    bo = BatchedOCP(R, "centroidal_vel", N, batch=1, device=0, include_base=False)
+    bo.set_params(P)  # the step sizes of the finite-difference accelerations
+    casadi_ext.bind(bo, 3)
+    o = OracleOCP(R, "centroidal_vel", N, include_base=False)
+    rng = np.random.default_rng(6)
+    sol = rng.normal(size=bo.n) * 0.1
+    x_init = np.concatenate([rng.normal(size=6) * 0.2, R.q0])
+    q, v, a, f, tau = casadi_ext.ExternalFunction("retract_solution")(sol, x_init)
+    M = rbd.ModelArrays(R.model)
+    frames = list(R.foot_frames)
+    dts = horizon_dts(DT_MIN, DT_MAX, N)
+    DX, U = o.split(sol)
+    nj = R.nj
+    for i in range(3):
+        xs = o.integrate_state(x_init, DX[i])
+        h, qi = xs[:6], xs[6:]
+        vi = np.concatenate([rbd.base_vel_cv(M, h, qi, U[i][:nj], R.mass), U[i][:nj]])
+        vn = np.concatenate([rbd.base_vel_cv(M, h, qi, U[i + 1][:nj], R.mass), U[i + 1][:nj]])
+        a_j = (vn - vi)[6:] / dts[i]
+        want_a = np.concatenate([rbd.base_acc_cv(M, frames, qi, vi, a_j, U[i][nj:], R.mass), a_j])
+        want_t = rbd.rnea_dynamics(M, frames, qi, vi, want_a, U[i][nj:])[6:]
+        assert np.abs(q[i] - qi).max() < 1e-13
+        assert np.abs(v[i] - vi).max() < 1e-11 * max(1, np.abs(vi).max())
+        assert np.abs(a[i] - want_a).max() < 1e-9 * max(1, np.abs(want_a).max())
+        assert np.array_equal(f[i], U[i][nj:])
+        assert np.abs(tau[i] - want_t).max() < 1e-9 * max(1, np.abs(want_t).max())
+    casadi_ext.unbind()
+    bo.close()
