@@ -31,10 +31,16 @@ def _flags():
             "-I", CSRC, "-I", os.path.join(CSRC, "..", "..", "include")] + os.environ.get("PL_HIPCC_DEFS", "").split()
 
 
-# Per-source code-generation options.  k_admm runs one wave per SIMD (no other wave hides
-# its latency): the iterative ILP scheduler cuts its launch 25.0 -> 24.5 ms at the headline
-# config (tools/gpu_libs.sh, r02f); the same option slows the other kernels, so it is not global.
-SOURCE_FLAGS = {"k_admm.hip": ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"]}
+# Per-source code-generation options.  The ADMM sweeps run one or two waves per SIMD (no
+# other wave hides their latency): the iterative ILP scheduler cuts k_admm 25.0 -> 24.5 ms
+# per launch at the headline config and k_admm2 14.2 -> 13.8 ms at config 3
+# (tools/gpu_libs.sh, tools/gpu_libs2.sh, profiles/r02f/sched/); it slows k_factor and
+# k_eval_jac<0>, so it is not global.
+_ILP = ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"]
+SOURCE_FLAGS = {"k_admm.hip": _ILP, "k_admm2.hip": _ILP}
+# PL_ILP_SOURCES: more sources to build with that scheduler (comma list, A/B experiments)
+for _src in filter(None, os.environ.get("PL_ILP_SOURCES", "").split(",")):
+    SOURCE_FLAGS[_src] = _ILP
 
 
 def _newest_input():
