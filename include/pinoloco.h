@@ -251,6 +251,19 @@ int pl_dyn_sizes(const pl_dyn* d, int fn, int flags, int* in_len, int* out_len);
 int pl_dyn_eval(pl_dyn* d, int fn, int batch, int frame, int flags, const double* in0, const double* in1,
                 const double* in2, const double* in3, double* out);
 
+/* ADMM linear-solve kernel.  All of them run the same OSQP 0.6 iteration on the same
+ * block factor and agree to round-off; they differ in how the block-tridiagonal solve is
+ * mapped to the GPU.  PL_ADMM_AUTO picks by batch size;
+ * PL_ADMM_SWEEP: one wave per problem, node-by-node sweeps (large batches);
+ * PL_ADMM_SWEEP2: two waves per problem; PL_ADMM_CHAIN: reduced chain, one workgroup
+ * per problem (small batches).  Internal to osqp.solve() (optimization/ocp.py:401). */
+#define PL_ADMM_AUTO 0
+#define PL_ADMM_SWEEP 1
+#define PL_ADMM_SWEEP2 2
+#define PL_ADMM_CHAIN 3
+int pl_ocp_set_admm_kernel(pl_ocp* o, int kind);
+int pl_ocp_get_admm_kernel(const pl_ocp* o);
+
 /* Timing of the dominant kernel (ADMM sweeps) with HIP events on the handle's
  * stream: pl_ocp_profile(o, 1) clears and starts, pl_ocp_profile_read returns
  * [total_ms, launches, problem_iterations]. pl_ocp_sizes (out[12]): [n, m, nnz,

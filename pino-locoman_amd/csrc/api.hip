@@ -947,6 +947,30 @@ int upload(pl_ocp* o, T** p, const std::vector<T>& v) {
 
 }  // namespace
 
+// ADMM kernel selection (the three give the same iterates to round-off):
+//   sweep   k_admm: one wave per problem, node-by-node block sweeps (HBM-bound at B >= 1024)
+//   sweep2  k_admm2: two waves per problem
+//   chain   k_admm_rc: reduced chain, one workgroup of 8 waves per problem (small batches)
+// AUTO: chain up to PL_ADMM_CHAIN_MAX_B problems when supported, else sweep2 up to 512
+// problems (idle SIMDs below 4 x 256), else sweep.  The chain
+// buffers are allocated on first selection.
+#define PL_ADMM_CHAIN_MAX_B 0
+int admm_select(pl_ocp* o, int kind) {
+  PlOcpHandle& h = o->h;
+  if (kind == PL_ADMM_AUTO) {
+    if (h.B <= PL_ADMM_CHAIN_MAX_B && admm_rc_supported(&h)) kind = PL_ADMM_CHAIN;
+    else kind = (h.B <= 512 && admm2_supported(&h)) ? PL_ADMM_SWEEP2 : PL_ADMM_SWEEP;
+  }
+  if (kind == PL_ADMM_SWEEP2 && !admm2_supported(&h)) { pl_set_error("sweep2 ADMM kernel does not support this OCP"); return -1; }
+  if (kind == PL_ADMM_CHAIN && !admm_rc_supported(&h)) { pl_set_error("chain ADMM kernel does not support this OCP"); return -1; }
+  if (kind == PL_ADMM_CHAIN && o->on_device && !h.d.CH) {
+    if (dalloc(o, &h.d.CH, (size_t)h.B * h.ch_stride) || dalloc(o, &h.d.chv, (size_t)h.B * h.chv_stride)) return -2;
+  }
+  h.admm_rc = kind == PL_ADMM_CHAIN ? 1 : 0;
+  h.admm_waves = kind == PL_ADMM_SWEEP2 ? 2 : 1;
+  return 0;
+}
+
 extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int batch, int device, pl_ocp** out) {
   if (!model || !d || !out || batch <= 0) { pl_set_error("bad arguments"); return -1; }
   if (d->dynamics < 0 || d->dynamics > 4) { pl_set_error("Unknown dynamics type: %d", d->dynamics); return -1; }
@@ -1048,15 +1072,13 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   // Fatrop settings of the reference (ocp.py:254-262) + the restatement's constants
   // (oracle/ip_ref.py IP_SETTINGS)
   h.ip = PlIpSettings{1e-3, 1e-4, 1e-7, 1e-2, 1e-8, 1e-4, 10, 12, 2, 0};
-  // ADMM sweep kernel: one wave per problem (k_admm); PL_ADMM_WAVES=2 selects the
-  // two-waves-per-problem variant (k_admm2.hip; measured slower)
-  // ADMM sweep: one wave per problem fills every SIMD once B >= 1024 (256 CUs x 4); below
-  // that the two-waves-per-problem kernel uses the idle SIMDs (measured: B2 aba N=40 at
-  // B = 256 +20 %, one Go2 problem +32 %; at B = 1024 it is 7 % slower).  PL_ADMM_WAVES
-  // (1 or 2) overrides.
-  h.admm_waves = batch <= 512 ? 2 : 1;
-  if (const char* w = getenv("PL_ADMM_WAVES")) h.admm_waves = atoi(w) == 2 ? 2 : 1;
-  if (h.admm_waves == 2 && !admm2_supported(&h)) h.admm_waves = 1;
+  // ADMM kernel (admm_select below): PL_ADMM_KERNEL = sweep | sweep2 | chain | auto overrides
+  // the batch-size rule at creation, pl_ocp_set_admm_kernel afterwards.
+  h.admm_waves = 1;
+  h.admm_rc = 0;
+  h.rc_waves = 8;
+  h.ch_stride = rc_ch_stride(h.N, h.ndx);
+  h.chv_stride = rc_chv_stride(h.N, h.ndx);
   h.gait_type = d->gait_type;
   h.gait_period = d->gait_period;
   h.swing_period = d->gait_type == 0 ? 0.5 * d->gait_period : (d->gait_type == 1 ? 0.25 * d->gait_period : d->gait_period);
@@ -1151,6 +1173,15 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   D.dbg = nullptr;
   if (getenv("PL_ADMM_TIMING") && atoi(getenv("PL_ADMM_TIMING")) > 0) rc |= dalloc(o, &D.dbg, B * 32);
   if (rc) { pl_ocp_destroy(o); return -2; }
+  {
+    int kind = PL_ADMM_AUTO;
+    if (const char* k = getenv("PL_ADMM_KERNEL")) {
+      if (!strcmp(k, "sweep")) kind = PL_ADMM_SWEEP;
+      else if (!strcmp(k, "sweep2")) kind = PL_ADMM_SWEEP2;
+      else if (!strcmp(k, "chain")) kind = PL_ADMM_CHAIN;
+    }
+    if (admm_select(o, kind)) { pl_ocp_destroy(o); return -2; }
+  }
   if (hipMemcpy(D.model, &h.model, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(D.oc, &h.oc, sizeof(PlOcpConst), hipMemcpyHostToDevice) != hipSuccess) {
     pl_set_error("upload of model tables failed");
@@ -1323,6 +1354,18 @@ static int fetch_stats(pl_ocp* o, pl_stats* stats) {
 // optimization/ocp.py:382-383); k > 1 repeats eval -> osqp.update -> warm-started
 // osqp.solve -> line search from the accepted point.  Phase times are those of the
 // last iteration.
+extern "C" int pl_ocp_set_admm_kernel(pl_ocp* o, int kind) {
+  REQUIRE_DEVICE(o);
+  if (kind < PL_ADMM_AUTO || kind > PL_ADMM_CHAIN) { pl_set_error("ADMM kernel %d unknown", kind); return -1; }
+  PL_CHECK_HIP(hipStreamSynchronize(o->h.stream));
+  return admm_select(o, kind);
+}
+
+extern "C" int pl_ocp_get_admm_kernel(const pl_ocp* o) {
+  if (!o) { pl_set_error("null handle"); return -1; }
+  return o->h.admm_rc ? PL_ADMM_CHAIN : (o->h.admm_waves == 2 ? PL_ADMM_SWEEP2 : PL_ADMM_SWEEP);
+}
+
 extern "C" int pl_ocp_set_sqp_iters(pl_ocp* o, int sqp_iters) {
   if (!o) { pl_set_error("null handle"); return -1; }
   if (sqp_iters < 1 || sqp_iters > 1000) { pl_set_error("sqp_iters %d outside [1, 1000]", sqp_iters); return -1; }

@@ -845,7 +845,8 @@ void launch_admm(PlOcpHandle* h, int niter, int check, int it_base) {
   const AdmmCfg c = admm_config(h);
   const bool prof = h->profile && h->prof_n < 64;
   if (prof) hipEventRecord(h->prof_ev[h->prof_n][0], h->stream);
-  if (h->admm_waves == 2 && !h->d.dbg) launch_admm2(h, niter, check);
+  if (h->admm_rc) launch_admm_rc(h, niter, check);
+  else if (h->admm_waves == 2 && !h->d.dbg) launch_admm2(h, niter, check);
   else if (h->admm_asr <= 16) launch_admm_a<16>(h, niter, check, c);
   else launch_admm_a<32>(h, niter, check, c);
   if (prof) {

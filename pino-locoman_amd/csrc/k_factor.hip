@@ -572,4 +572,5 @@ void launch_factor(PlOcpHandle* h) {
     case 48: launch_factor_x<48>(h); break;
     default: break;
   }
+  if (h->admm_rc) launch_fred(h);  // chain blocks of the reduced-chain ADMM (k_admm_rc.hip)
 }

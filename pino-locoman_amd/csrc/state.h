@@ -166,6 +166,8 @@ struct PlDev {
   uint16_t* kfl;         // factor flush slots
   uint32_t* kcpl;        // factor coupling programs
   double* FS;            // factor scratch [B][fs_stride]: A', G, C^-1 per node
+  double* CH;            // reduced-chain blocks [B][ch_stride]: per node F_i^T | F_i | G_i (k_fred, k_admm_rc.hip)
+  double* chv;           // reduced-chain vectors [B][chv_stride] (k_admm_rc)
   uint32_t* ttab;        // lane-tile tables [64][PL_ADMM_KM] per distinct (T, K): (I << 24) | (J << 16) | cidx
   int2* jlist;           // k_eval_jac work list: (node, local column), tree-pass columns first (whole waves)
   // per problem [B][*]
@@ -234,6 +236,10 @@ struct PlOcpHandle {
   int admm_fwd_asb;                 // coupling rows too dense for registers: forward steps stage A in LDS
   int sqp_iters;                    // SQP iterations per solve (reference: 1, ocp.py:382-383)
   int admm_waves;                   // ADMM sweep kernel: 2 = k_admm2 (two waves per problem), 1 = k_admm
+  int admm_rc;                      // 1: reduced-chain ADMM (k_admm_rc.hip) instead of the sweeps
+  int rc_waves;                     // waves per problem of k_admm_rc (4 or 8)
+  long long ch_stride;              // doubles of chain blocks per problem
+  int chv_stride;                   // doubles of chain vectors per problem
   int jl_len;                       // k_eval_jac work-list entries (a multiple of 64 before the cheap part)
   int solver;                       // PL_SOLVER_OSQP (SQP + OSQP ADMM) or PL_SOLVER_IP (interior point)
   PlIpSettings ip;
@@ -272,6 +278,11 @@ void launch_admm_init(PlOcpHandle* h);
 void launch_admm(PlOcpHandle* h, int niter, int check, int it_base);
 bool admm2_supported(const PlOcpHandle* h);
 void launch_admm2(PlOcpHandle* h, int niter, int check);
+bool admm_rc_supported(const PlOcpHandle* h);
+void launch_admm_rc(PlOcpHandle* h, int niter, int check);
+void launch_fred(PlOcpHandle* h);
+long long rc_ch_stride(int N, int ndx);
+int rc_chv_stride(int N, int ndx);
 void launch_check(PlOcpHandle* h, int it, int final_check);
 void launch_unscale(PlOcpHandle* h);
 void launch_line_search(PlOcpHandle* h);

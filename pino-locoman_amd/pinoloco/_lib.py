@@ -72,6 +72,8 @@ EXPORTS = {
     "pl_ocp_solve": (C.c_int, [C.c_void_p, C.POINTER(Stats), _dp]),
     "pl_ocp_set_sqp_iters": (C.c_int, [C.c_void_p, C.c_int]),
     "pl_ocp_set_solver": (C.c_int, [C.c_void_p, C.c_int]),
+    "pl_ocp_set_admm_kernel": (C.c_int, [C.c_void_p, C.c_int]),
+    "pl_ocp_get_admm_kernel": (C.c_int, [C.c_void_p]),
     "pl_ocp_set_ip_settings": (C.c_int, [C.c_void_p, C.POINTER(IpSettings)]),
     "pl_ocp_ip_stats": (C.c_int, [C.c_void_p, C.POINTER(IpStats)]),
     "pl_ocp_get_lam": (C.c_int, [C.c_void_p, _dp]),

@@ -253,6 +253,21 @@ class BatchedOCP:
         """SQP iterations per solve / MPC step (reference: 1, ocp.py:382-383)."""
         _lib.check(_lib.lib().pl_ocp_set_sqp_iters(self.h, int(k)))
 
+    ADMM_KERNELS = {"auto": 0, "sweep": 1, "sweep2": 2, "chain": 3}
+
+    def set_admm_kernel(self, kind):
+        """GPU mapping of the ADMM linear solve inside osqp.solve() (ocp.py:401): "sweep"
+        (one wave per problem, node-by-node block sweeps), "sweep2" (two waves per problem),
+        "chain" (reduced chain, one workgroup per problem) or "auto" (by batch size).  All
+        run the same OSQP iteration on the same factor and agree to round-off."""
+        if kind not in self.ADMM_KERNELS:
+            raise ValueError(f"ADMM kernel {kind} unknown (choose from {sorted(self.ADMM_KERNELS)})")
+        _lib.check(_lib.lib().pl_ocp_set_admm_kernel(self.h, self.ADMM_KERNELS[kind]))
+
+    def admm_kernel(self):
+        code = _lib.lib().pl_ocp_get_admm_kernel(self.h)
+        return {v: k for k, v in self.ADMM_KERNELS.items()}[code]
+
     def set_solver(self, solver):
         """"osqp" (SQP + OSQP, ocp.py:265-313 / 375-422) or "fatrop" (the interior-point
         restatement of the Fatrop branch, ocp.py:248-263 / 360-373)."""
