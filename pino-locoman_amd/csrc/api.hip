@@ -954,7 +954,7 @@ int upload(pl_ocp* o, T** p, const std::vector<T>& v) {
 // AUTO: chain up to PL_ADMM_CHAIN_MAX_B problems when supported, else sweep2 up to 512
 // problems (idle SIMDs below 4 x 256), else sweep.  The chain
 // buffers are allocated on first selection.
-#define PL_ADMM_CHAIN_MAX_B 0
+#define PL_ADMM_CHAIN_MAX_B 256  // measured: profiles/r03b (B2 aba B=256 13.8 -> 5.3 ms per launch; B2G at 512 the sweep2 wins)
 int admm_select(pl_ocp* o, int kind) {
   PlOcpHandle& h = o->h;
   if (kind == PL_ADMM_AUTO) {

@@ -41,13 +41,37 @@ namespace {
 using namespace admm;
 
 struct RcLds {
-  int prog_dbl, per_wave;
+  int prog_dbl, chn, per_wave;  // programs | chain buffers [2][64] | per-wave regions
   int v, y, acc, trow, tcpl, bc, asb, asb_cap;
 };
 
 struct Sb {
   double2 s[KM][8];
 };
+
+// Lane map of the chains (k_admm_rc): RW rows per wave, each split over NS lanes of SG columns
+// (SG even: 16-byte loads); 2 RW NS <= 64 (forward: F and G rows side by side).  PD steps of
+// chain blocks in flight per lane, within a register budget (2 waves per SIMD at W = 8).
+constexpr int rc_pick_ns(int X, int RW) {
+  for (int ns = 8; ns >= 1; --ns)
+    if (X % ns == 0 && (X / ns) % 2 == 0 && 2 * RW * ns <= 64) return ns;
+  return 1;
+}
+template <int X, int W>
+struct RcChain {
+  static constexpr int RW = (X + W - 1) / W;
+  static constexpr int NS = rc_pick_ns(X, RW);
+  static constexpr int SG = X / NS;
+  static constexpr int PD = (W >= 8 ? 72 : 144) / SG < 2 ? 2 : ((W >= 8 ? 72 : 144) / SG > 10 ? 10 : (W >= 8 ? 72 : 144) / SG);
+};
+
+// Workgroup barrier that orders LDS only (lgkmcnt(0) + s_barrier): __syncthreads() would also
+// wait vmcnt(0) and drain the chain blocks kept in flight across the steps.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 }  // namespace
 
@@ -124,10 +148,11 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   }
   __syncthreads();
   constexpr int ndx = X;
+  typedef RcChain<X, W> CS;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint16_t* PG = reinterpret_cast<const uint16_t*>(lds);
-  double* Wr = lds + lm.prog_dbl + wv * lm.per_wave;
+  double* Wr = lds + lm.prog_dbl + 128 + wv * lm.per_wave;
   double* v = Wr + lm.v;        // mat-vec input, zero padded to 4 T
   double* y = Wr + lm.y;        // mat-vec output [0, nw) | e_{i+1} [nw, nw + ndx)
   double* acc = Wr + lm.acc;    // LDS f64-add accumulators (mat-vec, row sums, column sums)
@@ -273,15 +298,53 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
     const bool term = i == N;
     const uint16_t* P = PG + an[i].prog;
     const double* __restrict__ Ai = As + eo;
+    // every operand of the node is issued at once: the factor block (registers), the node's
+    // vectors, then the node's A values straight into LDS (global_load_lds, no VGPRs); one
+    // vmcnt(0) then covers them all (one memory latency per node)
     Sb R;
-    load_S(i, 0, R);  // the factor block streams in behind the gathers
-    for (int e = lane; e < min(ne, cap); e += 64) asb[e] = Ai[e];
-    auto A = [&](int e) __attribute__((always_inline)) { return e < cap ? asb[e] : Ai[e]; };
+    load_S(i, 0, R);
+    double rh[MV], xo[MV], qo[MV];
+#pragma unroll
+    for (int mm = 0; mm < MV; ++mm) {
+      const int c = x_off + min(lane + 64 * mm, nw - 1);
+      rh[mm] = rhs[c];
+      xo[mm] = mode ? xa[c] : 0.0;
+      qo[mm] = mode ? qs[c] : 0.0;
+    }
+    const int nrow = an[i].nrow, ro = an[i].row_off;
+    double lz[MR], ly[MR], lr[MR], ll[MR], lu[MR];
+    if (mode) {
+#pragma unroll
+      for (int mm = 0; mm < MR; ++mm) {
+        const int r = ro + min(lane + 64 * mm, max(nrow - 1, 0));
+        lz[mm] = za[r];
+        ly[mm] = ya[r];
+        lr[mm] = rho[r];
+        ll[mm] = ls[r];
+        lu[mm] = us[r];
+      }
+    }
+    const double dl = mode ? DL[i * ndx + rr] : 0.0;
+    const double ee = (mode && !term) ? EE[(i + 1) * ndx + rr] : 0.0;
+    const int na = min(ne, cap);
+    const int sh = (int)(((size_t)Ai >> 3) & 1);  // 16-byte alignment of the DMA source
+    {
+      typedef __attribute__((address_space(1))) const void* GP;
+      typedef __attribute__((address_space(3))) void* LP;
+      const double* g0 = Ai - sh;
+      const int n2 = (na + sh + 1) >> 1;
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the previous node's reads of the area are done
+      for (int j = 0; j * 64 < n2; ++j)
+        if (j * 64 + lane < n2) __builtin_amdgcn_global_load_lds((GP)(g0 + 2 * (j * 64 + lane)), (LP)(asb + 128 * j), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
+    const double* asbs = asb + sh;
+    auto A = [&](int e) __attribute__((always_inline)) { return e < na ? asbs[e] : Ai[e]; };
     if (mode == 0) {
 #pragma unroll
       for (int mm = 0; mm < MV; ++mm) {
         const int c = lane + 64 * mm;
-        if (c < nw) v[c] = rhs[x_off + c];
+        if (c < nw) v[c] = rh[mm];
         else if (c < T4) v[c] = 0.0;
       }
       if (lane < ndx) A2[(i + 1) * ndx + lane] = 0.0;
@@ -290,28 +353,8 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
       coupling_out(i, A);
       return;
     }
-    // ---- P3: operands
-    double rh[MV], xo[MV], qo[MV];
-#pragma unroll
-    for (int mm = 0; mm < MV; ++mm) {
-      const int c = x_off + min(lane + 64 * mm, nw - 1);
-      rh[mm] = rhs[c];
-      xo[mm] = xa[c];
-      qo[mm] = qs[c];
-    }
-    const int nrow = an[i].nrow, ro = an[i].row_off;
-    double lz[MR], ly[MR], lr[MR], ll[MR], lu[MR];
-#pragma unroll
-    for (int mm = 0; mm < MR; ++mm) {
-      const int r = ro + min(lane + 64 * mm, max(nrow - 1, 0));
-      lz[mm] = za[r];
-      ly[mm] = ya[r];
-      lr[mm] = rho[r];
-      ll[mm] = ls[r];
-      lu[mm] = us[r];
-    }
-    const double dl = DL[i * ndx + rr];
-    if (!term && lane < ndx) y[nw + lane] = EE[(i + 1) * ndx + lane];
+    // ---- P3
+    if (!term && lane < ndx) y[nw + lane] = ee;
     wsync();
     // t_s = rho_s a_s(dx_{i+1}) . e_{i+1}
     if (!term) {
@@ -456,128 +499,173 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
     coupling_out(i, A);
   };
 
-  // ---- C1: delta_{i+1} = (c'_i - F_i delta_i) - a2_i, lane r = chain row (wave 0).  Row r of
-  // F_{i+1} is streamed into the registers of row r of F_i as they are consumed (one step of
-  // latency cover, one register buffer).
+  // ---- The chains, spread over the whole workgroup: wave w owns rows [r0, r0 + nr) of the
+  // recurrence and every row is split over NS lanes (SG columns each), so a step is SG FMAs,
+  // an NS-lane reduction and one LDS barrier; PD steps of chain blocks are in flight per lane.
+  //   C1 (steps i = 0..N): lanes q < RW: d_{i+1}[r] = c'_i[r] - F_i[r] . delta_i,
+  //                          delta_{i+1}[r] = d_{i+1}[r] - a2_i[r];
+  //                        lanes RW <= q < 2 RW: w_i[r] = h'_i[r] - G_i[r] . delta_i
+  //   C2 (steps i = N-1..1): lanes q < RW: e_i[r] = w_i[r] - F_i^T[r] . e_{i+1}
+  // delta / e are double-buffered in LDS (read one buffer, write the other), so one barrier
+  // per step suffices.  Fixed lane -> (row, segment) map and a fixed-order reduction.
+  constexpr int RW = CS::RW, NS = CS::NS, SG = CS::SG, PD = CS::PD;
+  const int r0 = (X * wv) / W, nr = (X * (wv + 1)) / W - r0;
+  const int cq = lane / NS, cs = lane - cq * NS;
+  const bool cF = cq < RW;
+  const int cj = cF ? cq : cq - RW;
+  const bool cvalid = cj < nr && cq < 2 * RW;
+  const int crow = r0 + min(cj, nr - 1);
+  double* cbuf = lds + lm.chn;  // [2][64] shared by the workgroup
+
+  auto reduce_row = [&](double p) __attribute__((always_inline)) {
+    // sum of the NS partials of this lane's row, in segment order
+    double t = __shfl(p, cq * NS, 64);
+#pragma unroll
+    for (int k = 1; k < NS; ++k) t += __shfl(p, cq * NS + k, 64);
+    return t;
+  };
+
   auto chain_fwd = [&]() __attribute__((always_inline)) {
-    double2 fr[X / 2];
-    double cv, av;
-    auto rowp = [&](int i) __attribute__((always_inline)) {
-      return reinterpret_cast<const double2*>(CH + (size_t)min(i, N - 1) * 3 * X2 + rr * ndx);
+    double2 rg[PD][SG / 2];
+    double u1[PD], u2[PD];
+    // per-lane offsets (constant over the steps) from wave-uniform bases: saddr + voffset loads
+    const int boff = ((cF ? 0 : 2 * X2) + crow * X + cs * SG) / 2;
+    const int o1 = (cF ? 4 : 5) * L + crow, o2 = 3 * L + crow;
+    auto fetch = [&](int s, int i) __attribute__((always_inline)) {
+      const int ig = min(i, N);  // F rows are not used at step N (its block holds G_N only)
+      const double2* pp = reinterpret_cast<const double2*>(CH + (size_t)ig * 3 * X2);
+#pragma unroll
+      for (int k = 0; k < SG / 2; ++k) rg[s][k] = gld(pp, boff + k);
+      u1[s] = gld(DL + ig * X, o1);        // c'_i (F rows) / h'_i (G rows)
+      u2[s] = gld(DL + (ig + 1) * X, o2);  // a2_i
     };
-    {
-      const double2* fm = rowp(0);
+    int z0;  // an opaque 0: keeps the prologue's (iteration-invariant) addresses out of registers across phases
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z0));
 #pragma unroll
-      for (int k = 0; k < X / 2; ++k) fr[k] = fm[k];
-      cv = CP[rr];
-      av = A2[ndx + rr];
+    for (int s = 0; s < PD; ++s) fetch(s, s + z0);
+    if (wv == 0) {
+      cbuf[lane] = 0.0;  // delta_0
+      if (lane < X) DL[lane] = 0.0;
     }
-    if (lane < ndx) {
-      bc[lane] = 0.0;
-      DL[lane] = 0.0;
-    }
-    wsync();
-    for (int i = 0; i < N; ++i) {
-      const double2* fn = rowp(i + 1);
-      const double cvn = CP[min(i + 1, N - 1) * ndx + rr];
-      const double avn = A2[(min(i + 1, N - 1) + 1) * ndx + rr];
-      double a[4] = {0.0, 0.0, 0.0, 0.0};
-      const double2* b2 = reinterpret_cast<const double2*>(bc);
+    lds_barrier();
+    for (int i0 = 0; i0 <= N; i0 += PD) {
 #pragma unroll
-      for (int k = 0; k < X / 2; ++k) {
-        const double2 t = b2[k];
-        a[k & 3] += fr[k].x * t.x + fr[k].y * t.y;
-        fr[k] = fn[k];
+      for (int s = 0; s < PD; ++s) {
+        const int i = i0 + s;
+        if (i <= N) {
+          const double2* dc = reinterpret_cast<const double2*>(cbuf + (i & 1) * 64) + cs * (SG / 2);
+          double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+          for (int k = 0; k < SG / 2; ++k) {
+            const double2 t = dc[k];
+            if (k & 1) p1 += rg[s][k].x * t.x + rg[s][k].y * t.y;
+            else p0 += rg[s][k].x * t.x + rg[s][k].y * t.y;
+          }
+          const double v1 = u1[s], v2 = u2[s];
+          __builtin_amdgcn_sched_barrier(0);  // the slot is consumed before its refill is issued (one register set)
+          fetch(s, i + PD);
+          const double sum = reduce_row(p0 + p1);
+          if (cs == 0 && cvalid) {
+            if (cF) {
+              if (i < N) {
+                const double de = (v1 - sum) - v2;
+                cbuf[((i + 1) & 1) * 64 + crow] = de;
+                DL[(i + 1) * X + crow] = de;
+              }
+            } else {
+              WD[i * X + crow] = v1 - sum;
+            }
+          }
+          lds_barrier();
+        }
       }
-      const double de = (cv - ((a[0] + a[1]) + (a[2] + a[3]))) - av;
-      cv = cvn;
-      av = avn;
-      wsync();
-      bc[lane] = de;  // every lane (no branch for the compiler to sink the FMAs into)
-      if (lane < ndx) DL[(i + 1) * ndx + lane] = de;
-      wsync();
     }
   };
 
-  // ---- C2: e_i = w_i[dx] - F_i^T e_{i+1}, lane k = chain column (wave 0)
   auto chain_bwd = [&]() __attribute__((always_inline)) {
-    double2 fr[X / 2];
-    double wd;
-    auto rowp = [&](int i) __attribute__((always_inline)) {
-      return reinterpret_cast<const double2*>(CH + (size_t)max(i, 0) * 3 * X2 + X2 + rr * ndx);
+    double2 rg[PD][SG / 2];
+    double u1[PD];
+    const int boff = (X2 + crow * X + cs * SG) / 2;
+    auto fetch = [&](int s, int i) __attribute__((always_inline)) {
+      const int ic = max(i, 1);
+      const double2* pp = reinterpret_cast<const double2*>(CH + (size_t)ic * 3 * X2);
+#pragma unroll
+      for (int k = 0; k < SG / 2; ++k) rg[s][k] = gld(pp, boff + k);
+      u1[s] = gld(WD + ic * X, crow);
     };
-    {
-      const double2* fm = rowp(N - 1);
+    int z0;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z0));
 #pragma unroll
-      for (int r = 0; r < X / 2; ++r) fr[r] = fm[r];
-      wd = WD[(N - 1) * ndx + rr];
-      const double e = WD[N * ndx + rr];
-      if (lane < ndx) {
-        bc[lane] = e;
-        EE[N * ndx + lane] = e;
-      }
+    for (int s = 0; s < PD; ++s) fetch(s, N - 1 - s + z0);
+    if (cF && cs == 0 && cvalid) {
+      const double e = WD[N * X + crow];
+      cbuf[(N & 1) * 64 + crow] = e;
+      EE[N * X + crow] = e;
     }
-    wsync();
-    for (int i = N - 1; i >= 1; --i) {  // e_i for i = N-1 .. 1
-      const double2* fn = rowp(i - 1);
-      const double wdn = WD[max(i - 1, 0) * ndx + rr];
-      double a[4] = {0.0, 0.0, 0.0, 0.0};
-      const double2* b2 = reinterpret_cast<const double2*>(bc);
+    lds_barrier();
+    for (int j0 = 0; j0 < N - 1; j0 += PD) {
 #pragma unroll
-      for (int r = 0; r < X / 2; ++r) {
-        const double2 t = b2[r];
-        a[r & 3] += fr[r].x * t.x + fr[r].y * t.y;
-        fr[r] = fn[r];
+      for (int s = 0; s < PD; ++s) {
+        const int i = N - 1 - (j0 + s);  // e_i for i = N-1 .. 1
+        if (i >= 1) {
+          const double2* ec = reinterpret_cast<const double2*>(cbuf + ((i + 1) & 1) * 64) + cs * (SG / 2);
+          double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+          for (int k = 0; k < SG / 2; ++k) {
+            const double2 t = ec[k];
+            if (k & 1) p1 += rg[s][k].x * t.x + rg[s][k].y * t.y;
+            else p0 += rg[s][k].x * t.x + rg[s][k].y * t.y;
+          }
+          const double v1 = u1[s];
+          __builtin_amdgcn_sched_barrier(0);
+          fetch(s, i - PD);
+          const double sum = reduce_row(p0 + p1);
+          if (cF && cs == 0 && cvalid) {
+            const double e = v1 - sum;
+            cbuf[(i & 1) * 64 + crow] = e;
+            EE[i * X + crow] = e;
+          }
+          lds_barrier();
+        }
       }
-      const double e = wd - ((a[0] + a[1]) + (a[2] + a[3]));
-      wd = wdn;
-      wsync();
-      bc[lane] = e;
-      if (lane < ndx) EE[i * ndx + lane] = e;
-      wsync();
     }
   };
 
-  // ---- P2: w_i[dx] = h'_i - G_i delta_i
-  auto p2node = [&](int i) __attribute__((always_inline)) {
-    if (lane < ndx) bc[lane] = DL[i * ndx + lane];
-    const double h = HP[i * ndx + rr];
-    wsync();
-    const double2* G = reinterpret_cast<const double2*>(CH + (size_t)i * 3 * X2 + 2 * X2 + rr * ndx);
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
-    const double2* b2 = reinterpret_cast<const double2*>(bc);
-#pragma unroll
-    for (int k = 0; k < X / 2; ++k) {
-      const double2 t = b2[k], g = G[k];
-      a[k & 3] += g.x * t.x + g.y * t.y;
+  // optional phase timing (PL_ADMM_TIMING=1: s_memtime on wave 0, cycles into d.dbg[b][0..5]):
+  // P, C1, P2, C2, P3, barrier waits
+  const bool tim = d.dbg != nullptr;
+  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tl = 0;
+  auto T = [&](int slot) __attribute__((always_inline)) {
+    if (tim) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (slot >= 0) tacc[slot] += now - tl;
+      tl = now;
     }
-    if (lane < ndx) WD[i * ndx + lane] = h - ((a[0] + a[1]) + (a[2] + a[3]));
-    wsync();
   };
-
+  T(-1);
   if (wv == 0 && lane < ndx) A2[lane] = 0.0;  // a2_{-1}
-#ifndef RCX_NOP0
   for (int i = wv; i <= N; i += W) pnode(i, 0, false);
-#endif
+  T(0);
   __syncthreads();
+  T(5);
   for (int it = 0; it < niter; ++it) {
-#ifndef RCX_NOC1
-    if (wv == 0) chain_fwd();
-#endif
+    chain_fwd();  // C1 (+ w_i[dx], formerly P2)
+    T(1);
     __syncthreads();
-#ifndef RCX_NOP2
-    for (int i = wv; i <= N; i += W) p2node(i);
-#endif
+    T(5);
+    chain_bwd();  // C2
+    T(3);
     __syncthreads();
-#ifndef RCX_NOC2
-    if (wv == 0) chain_bwd();
-#endif
-    __syncthreads();
+    T(5);
     const bool lastit = it == niter - 1;
-#ifndef RCX_NOP3
     for (int i = wv; i <= N; i += W) pnode(i, lastit ? 2 : 1, check && lastit);
-#endif
+    T(4);
     __syncthreads();
+    T(5);
+  }
+  if (tim && wv == 0 && lane == 0) {
+    for (int k = 0; k < 6; ++k) d.dbg[(size_t)b * 16 + k] += (double)tacc[k];
+    d.dbg[(size_t)b * 16 + 6] += niter;
   }
   // the complete rhs for the next launch / kernel: rhs_i[dx] += a2_{i-1}
   for (int i = wv; i <= N; i += W) {
@@ -605,6 +693,7 @@ RcCfg rc_config(const PlOcpHandle* h, int w) {
   RcLds& lm = c.lm;
   auto up2 = [](int x) { return (x + 1) & ~1; };
   lm.prog_dbl = up2((h->aprog_len + 3) / 4);
+  lm.chn = lm.prog_dbl;
   const int T = h->ntile_max;
   int o = 0;
   lm.v = o;
@@ -622,11 +711,11 @@ RcCfg rc_config(const PlOcpHandle* h, int w) {
   lm.asb = o;
   c.w = w;
   const int budget = 160 * 1024 / 8;
-  int cap = ((budget - lm.prog_dbl) / w - o) & ~1;
+  int cap = ((budget - lm.prog_dbl - 128) / w - o - 2) & ~1;
   cap = std::max(0, std::min(up2(std::max(h->nent_max, 1)), cap));
   lm.asb_cap = cap;
-  lm.per_wave = o + cap;
-  c.lds = (size_t)(lm.prog_dbl + w * lm.per_wave) * sizeof(double);
+  lm.per_wave = o + cap + 2;  // + the 16-byte alignment shift of the A staging DMA
+  c.lds = (size_t)(lm.prog_dbl + 128 + w * lm.per_wave) * sizeof(double);
   return c;
 }
 

@@ -89,6 +89,38 @@ def test_chain_batch_invariance_and_repeatability():
     assert np.array_equal(x3[0], x1[3]) and it3[0] == it1[3]
 
 
+@pytest.mark.parametrize("kernel", ["sweep", "chain"])
+def test_bit_identical_across_batch_sizes_per_kernel(kernel):
+    """A problem gives the same bits alone and inside a batch of 1024 when the same ADMM
+    kernel runs both (the AUTO choice depends on the batch size; across kernels the sums
+    run in other orders and agree to round-off, test_kernels_agree)."""
+    from pinoloco.ocp import BatchedOCP
+    from pinoloco.synthetic import build_batch
+    R = make_robot("go2")
+    B = 1024
+    lay, P, X, XS, T0 = build_batch(R, "centroidal_vel", 20, B, 0)
+    out = []
+    for rows in (slice(0, B), slice(700, 701)):
+        bo = BatchedOCP(R, "centroidal_vel", 20, batch=rows.stop - rows.start, device=0)
+        bo.set_admm_kernel(kernel)
+        bo.set_params(P[rows])
+        bo.set_x(X[rows])
+        bo.init_solver()
+        st = bo.solve()
+        out.append((bo.get_x(), st["admm_iters"]))
+        bo.close()
+    assert np.array_equal(out[1][0][0], out[0][0][700]) and out[1][1][0] == out[0][1][700]
+
+
+def test_auto_kernel_choice():
+    from pinoloco.ocp import BatchedOCP
+    R = make_robot("b2")
+    for B, want in ((1, "chain"), (256, "chain"), (512, "sweep2"), (1024, "sweep")):
+        bo = BatchedOCP(R, "whole_body_aba", 10, batch=B, device=0)
+        assert bo.admm_kernel() == want, (B, bo.admm_kernel())
+        bo.close()
+
+
 @pytest.mark.parametrize("name,rname,dyn,N", [CONFIGS[0], CONFIGS[1], EDGE[0]])
 def test_chain_device_mpc_loop(name, rname, dyn, N):
     G = golden(f"sqp_{name}.npz")

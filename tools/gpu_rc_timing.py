@@ -1,0 +1,35 @@
+"""Phase timing of the reduced-chain ADMM kernel (k_admm_rc, s_memtime on wave 0).
+
+Run on the GPU box:  python tools/gpu_rc_timing.py robot dynamics N B
+"""
+import os
+import sys
+
+import numpy as np
+
+os.environ["PL_ADMM_TIMING"] = "1"
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "pino-locoman_amd"))
+from pinoloco import robots  # noqa: E402
+from pinoloco.ocp import BatchedOCP  # noqa: E402
+from pinoloco.synthetic import build_batch  # noqa: E402
+
+rob, dyn, N, B = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+R = robots.ROBOTS[rob]()
+R.set_gait_sequence("trot", 0.8)
+lay, P, X, XS, T0 = build_batch(R, dyn, N, B, 0)
+bo = BatchedOCP(R, dyn, N, batch=B, device=0)
+bo.set_admm_kernel("chain")
+bo.set_params(P)
+bo.set_x(X)
+bo.init_solver()
+st = bo.solve(timed=True)
+T = bo.debug("admm_t", B * 32)[:B * 16].reshape(B, 16)
+it = T[:, 6]
+names = ["P (first)", "C1 chain", "P2", "C2 chain", "P3 + P", "barrier waits"]
+per = T[:, :6] / it[:, None]
+print(f"{rob} {dyn} N={N} B={B}: phase_ms {st['phase_ms']}")
+for k, nm in enumerate(names):
+    print(f"{nm:14s} mean cycles/iteration {per[:, k].mean():10.1f}  p90 {np.percentile(per[:, k], 90):10.1f}")
+print(f"total cycles/iteration {per.sum(1).mean():.1f}; C1 cycles/step {per[:, 1].mean() / N:.1f}, "
+      f"C2 cycles/step {per[:, 3].mean() / (N - 1):.1f}")

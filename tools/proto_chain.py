@@ -76,6 +76,56 @@ def block_factor(K, bl, ndx):
     return S
 
 
+def gj_inv(M, equil=False):
+    """Gauss-Jordan inverse without pivoting (the sweep operator the GPU factor runs), optionally
+    on the symmetrically equilibrated matrix D M D, D = diag(M)^-1/2."""
+    M = np.array(M, dtype=float)
+    n = M.shape[0]
+    d = np.ones(n)
+    if equil:
+        d = 1.0 / np.sqrt(np.abs(np.diag(M)))
+        M = d[:, None] * M * d[None, :]
+    for k in range(n):
+        p = M[k, k]
+        rowk = M[k, :].copy()
+        colk = M[:, k].copy()
+        M -= np.outer(colk, rowk) / p
+        M[k, :] = rowk / p
+        M[:, k] = -colk / p
+        M[k, k] = 1.0 / p
+    M = -M  # sweep gives -M^-1 off the swept block convention; fix sign below
+    M = -M
+    return d[:, None] * M * d[None, :]
+
+
+def block_factor_two_stage(K, bl, ndx):
+    """The GPU factor's formulas (k_factor.hip): C^-1 of the u block, A' = A - B C^-1 B^T,
+    S_xx = (A' + E)^-1, S_ux = -G S_xx (G = C^-1 B^T), S_uu = C^-1 + G S_xx G^T, symmetrised."""
+    S = []
+    for i, (a, b) in enumerate(bl):
+        Kii = K[a:b, a:b].toarray()
+        Eb = np.zeros((ndx, ndx))
+        if i > 0:
+            pa, pb = bl[i - 1]
+            Ci = K[a:a + ndx, pa:pb].toarray()
+            Eb = -Ci @ S[-1] @ Ci.T
+        X = ndx
+        if b - a == X:
+            Si = INV(Kii + Eb)
+        else:
+            A_, B_, C_ = Kii[:X, :X], Kii[:X, X:], Kii[X:, X:]
+            inv = INV
+            Ci_ = inv(C_)
+            G = Ci_ @ B_.T
+            Ap = A_ - B_ @ G
+            Sxx = inv(Ap + Eb)
+            Sux = -G @ Sxx
+            Suu = Ci_ + G @ Sxx @ G.T
+            Si = np.block([[Sxx, Sux.T], [Sux, Suu]])
+        S.append(0.5 * (Si + Si.T))
+    return S
+
+
 def solve_sweep(K, S, bl, ndx, rhs):
     N1 = len(bl)
     w = [None] * N1
@@ -155,6 +205,10 @@ def admm(solve, P, qs, A, ls, us, rho, sigma, alpha, iters):
     return hist
 
 
+MODE = os.environ.get("PROTO_INV", "lu")
+INV = {"lu": np.linalg.inv, "gj": gj_inv, "gje": lambda M: gj_inv(M, True)}[MODE]
+
+
 def main():
     fix = sys.argv[1] if len(sys.argv) > 1 else "sqp_go2_rnea_n20"
     b = int(sys.argv[2]) if len(sys.argv) > 2 else 0
@@ -175,6 +229,8 @@ def main():
             pa, pb = bl[i - 1]
             assert abs(K[a + ndx:b_, pa:pb]).sum() == 0
     S = block_factor(K, bl, ndx)
+    if os.environ.get("PROTO_TWO_STAGE"):
+        S = block_factor_two_stage(K, bl, ndx)
     C, F, G = chain_setup(K, S, bl, ndx)
     lu = spla.splu(sp.bmat([[sp.diags(P + sigma), A.T], [A, sp.diags(-1.0 / rho)]], format="csc"))
     m = A.shape[0]
