@@ -173,6 +173,10 @@ int pl_ocp_set_solver(pl_ocp* o, int solver);
 int pl_ocp_set_ip_settings(pl_ocp* o, const pl_ip_settings* s);
 int pl_ocp_ip_stats(pl_ocp* o, pl_ip_stats* stats);   /* [batch] */
 int pl_ocp_get_lam(pl_ocp* o, double* lam);           /* [batch][m]: lam_g (ocp.py:373) */
+/* [batch][m] lam_g warm start of the next interior-point solves (the OCPs' warm_start:
+ * opti.set_initial(opti.lam_g, lam_g), ocp_whole_body_rnea.py:234-235); NULL = cold
+ * (lam = 0, the reference's first solve).  pl_mpc_step carries lam_g itself. */
+int pl_ocp_set_lam(pl_ocp* o, const double* lam);
 /* Parity aid: the interior point's Newton direction from a given state (x set with
  * pl_ocp_set_x; slacks, multipliers [batch][m], mu [batch]); read it back with
  * pl_debug_get("ip_dx" / "ip_dl" / "ip_ds") and the step bounds with pl_ocp_ip_stats

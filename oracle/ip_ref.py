@@ -29,8 +29,14 @@ Math. Prog. 106, 2006) -- is restated here, with these documented choices:
   path reuses its factor and sweep kernels; ``n_refine`` iterative-refinement solves
   on the KKT x-row residual follow the first solve;
 * initial point (warm_start_init_point): x from the warm start; slacks pushed into
-  the interior with bound_push / bound_frac; lam = 0 (the reference does not pass
-  lam_g back, ``run_mpc.py:58-59``); bound multipliers centred, z = mu_init / slack;
+  the interior with bound_push / bound_frac.  Cold (no lam_g yet, the reference's first
+  solve): lam = 0 and the slack-bound multipliers centred, z = mu_init / slack.  Warm
+  (``lam0`` given: the previous solve's lam_g, which the reference stores at ``ocp.py:373``
+  and passes back with ``opti.set_initial(opti.lam_g, lam_g)``,
+  ``ocp_whole_body_rnea.py:234-235``, ``ocp_whole_body_acc.py:164-165``): lam = lam0 and,
+  as IPOPT's warm_start_init_point does for the slack bounds, the multipliers split by the
+  sign of lam (stationarity in s: z_u - z_l = lam), z_l = max(-lam, 0), z_u = max(lam, 0),
+  each pushed up to warm_start_mult_bound_push (1e-7, ``ocp.py:260``);
 * barrier parameter: IPOPT's monotone rule mu <- max(tol / 10, min(kappa_mu mu,
   mu^theta_mu)) when E_mu <= kappa_eps mu (with tol 1e-3 and mu_init 1e-4 mu stays
   at 1e-4);
@@ -110,8 +116,9 @@ class IPRef:
     def _phi(self, f, sl, su, hl, hu, mu):
         return f - mu * (np.sum(np.log(sl[hl])) + np.sum(np.log(su[hu])))
 
-    def solve(self, x0, p, verbose=False):
-        """Returns x, lam, dict(status, iter, err, mu, f, alphas, trials)."""
+    def solve(self, x0, p, lam0=None, verbose=False):
+        """Returns x, lam, dict(status, iter, err, mu, f, alphas, trials).  lam0: the
+        multipliers of a previous solve (warm start, see the module docstring)."""
         o, st = self.o, self.s
         mu = st["mu_init"]
         tol = st["tol"]
@@ -125,11 +132,17 @@ class IPRef:
         ub = np.where(hu, ubg, 0.0)
         s = push_slacks(g, lbg, ubg, eq, hl, hu, st["bound_push"], st["bound_frac"])
         m = g.size
-        lam = np.zeros(m)
         sl = np.where(hl, s - lb, 1.0)
         su = np.where(hu, ub - s, 1.0)
-        zl = np.where(hl, mu / sl, 0.0)
-        zu = np.where(hu, mu / su, 0.0)
+        if lam0 is None:
+            lam = np.zeros(m)
+            zl = np.where(hl, mu / sl, 0.0)
+            zu = np.where(hu, mu / su, 0.0)
+        else:
+            lam = np.array(lam0, dtype=float, copy=True)
+            wp = st["warm_start_mult_bound_push"]
+            zl = np.where(hl, np.maximum(np.maximum(-lam, 0.0), wp), 0.0)
+            zu = np.where(hu, np.maximum(np.maximum(lam, 0.0), wp), 0.0)
         nb = int(hl.sum() + hu.sum())
         theta0 = float(np.sum(np.abs(self._c(g, s, lbg, eq))))
         theta_max = 1e4 * max(1.0, theta0)

@@ -1071,7 +1071,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   h.solver = PL_SOLVER_OSQP;
   // Fatrop settings of the reference (ocp.py:254-262) + the restatement's constants
   // (oracle/ip_ref.py IP_SETTINGS)
-  h.ip = PlIpSettings{1e-3, 1e-4, 1e-7, 1e-2, 1e-8, 1e-4, 10, 12, 2, 0};
+  h.ip = PlIpSettings{1e-3, 1e-4, 1e-7, 1e-2, 1e-8, 1e-4, 10, 12, 2, 0, 1e-7};
   // ADMM kernel (admm_select below): PL_ADMM_KERNEL = sweep | sweep2 | chain | auto overrides
   // the batch-size rule at creation, pl_ocp_set_admm_kernel afterwards.
   h.admm_waves = 1;
@@ -1150,6 +1150,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= dalloc(o, &D.us, B * m);
   rc |= dalloc(o, &D.rho, B * m);
   rc |= dalloc(o, &D.rhoc, B * (size_t)(h.N + 1) * std::max(h.ncpl_max, 1));
+  rc |= dalloc(o, &D.Acpl, B * (size_t)(h.N + 1) * PL_ACPL);
   rc |= dalloc(o, &D.D, B * n);
   rc |= dalloc(o, &D.E, B * m);
   rc |= dalloc(o, &D.cs, B);
@@ -1385,7 +1386,8 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
   PlOcpHandle* h = &o->h;
   if (solver == PL_SOLVER_IP && !h->d.ipinfo) {
     const size_t Bm = (size_t)h->B * h->m;
-    if (dalloc(o, &h->d.ip_s, Bm) || dalloc(o, &h->d.ip_lam, Bm) || dalloc(o, &h->d.ip_zl, Bm) ||
+    if (dalloc(o, &h->d.ip_s, Bm) || dalloc(o, &h->d.ip_lam, Bm) || dalloc(o, &h->d.ip_lam0, Bm) ||
+        dalloc(o, &h->d.ip_zl, Bm) ||
         dalloc(o, &h->d.ip_zu, Bm) || dalloc(o, &h->d.ip_rh, Bm) || dalloc(o, &h->d.ip_dl, Bm) ||
         dalloc(o, &h->d.ip_ds, Bm) || dalloc(o, &h->d.ip_jdx, Bm) || dalloc(o, &h->d.ip_dx, (size_t)h->B * h->n) ||
         dalloc(o, &h->d.ipinfo, (size_t)h->B))
@@ -1407,7 +1409,24 @@ extern "C" int pl_ocp_set_ip_settings(pl_ocp* o, const pl_ip_settings* s) {
     return -1;
   }
   o->h.ip = PlIpSettings{s->tol, s->mu_init, s->bound_push, s->bound_frac, s->delta_w, s->delta_c, s->max_iter,
-                         s->ls_max, s->n_refine, 0};
+                         s->ls_max, s->n_refine, 0, 1e-7};
+  return 0;
+}
+
+// lam_g warm start of the interior-point branch (opti.set_initial(opti.lam_g, lam_g),
+// ocp_whole_body_rnea.py:234-235 and the other OCPs' warm_start): lam = NULL returns to the
+// cold start (lam = 0).  Kept until changed, like an Opti initial value.
+extern "C" int pl_ocp_set_lam(pl_ocp* o, const double* lam) {
+  REQUIRE_DEVICE(o);
+  PlOcpHandle* h = &o->h;
+  if (!h->d.ip_lam0) { pl_set_error("no interior-point state (pl_ocp_set_solver(o, PL_SOLVER_IP) first)"); return -1; }
+  if (!lam) {
+    h->ip_lam_warm = 0;
+    return 0;
+  }
+  PL_CHECK_HIP(hipMemcpyAsync(h->d.ip_lam0, lam, (size_t)h->B * h->m * 8, hipMemcpyHostToDevice, h->stream));
+  PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+  h->ip_lam_warm = 1;
   return 0;
 }
 
@@ -1526,6 +1545,7 @@ extern "C" int pl_mpc_setup(pl_ocp* o, const double* x_state, const double* t0) 
   PL_CHECK_HIP(hipMemcpyAsync(h->d.xstate, x_state, (size_t)h->B * h->nx * 8, hipMemcpyHostToDevice, h->stream));
   PL_CHECK_HIP(hipMemcpyAsync(h->d.t0, t0, (size_t)h->B * 8, hipMemcpyHostToDevice, h->stream));
   PL_CHECK_HIP(hipStreamSynchronize(h->stream));
+  h->ip_lam_warm = 0;  // the loop's first solve has no lam_g yet (ocp.py:198)
   return 0;
 }
 
@@ -1533,8 +1553,13 @@ extern "C" int pl_mpc_step(pl_ocp* o, int k) {
   REQUIRE_DEVICE(o);
   if (o->h.profile && o->h.prof_n > 48) prof_collect(&o->h);
   launch_mpc_prepare(&o->h, k);
-  if (o->h.solver == PL_SOLVER_IP) enqueue_ip(&o->h);
-  else
+  if (o->h.solver == PL_SOLVER_IP) {
+    enqueue_ip(&o->h);
+    // warm_start() of the next step passes this solve's lam_g back (ocp.py:373, ocp_*.py warm_start)
+    PlOcpHandle* h = &o->h;
+    PL_CHECK_HIP(hipMemcpyAsync(h->d.ip_lam0, h->d.ip_lam, (size_t)h->B * h->m * 8, hipMemcpyDeviceToDevice, h->stream));
+    h->ip_lam_warm = 1;
+  } else
     for (int it = 0; it < o->h.sqp_iters; ++it) enqueue_solve(o, false);
   launch_mpc_finish(&o->h);
   PL_CHECK_HIP(hipGetLastError());
@@ -1661,6 +1686,7 @@ extern "C" int pl_debug_get(pl_ocp* o, const char* name, double* out, long long 
       {"rhs", h->d.rhs, B * h->n}, {"step", h->d.step, B * h->n},   {"grad", h->d.grad, B * h->n},
       {"g", h->d.g, B * h->m},     {"xstate", h->d.xstate, B * h->nx},
       {"ip_s", h->d.ip_s, h->d.ip_s ? B * h->m : 0},     {"ip_lam", h->d.ip_lam, h->d.ip_lam ? B * h->m : 0},
+      {"ip_lam0", h->d.ip_lam0, h->d.ip_lam0 ? B * h->m : 0},
       {"ip_zl", h->d.ip_zl, h->d.ip_zl ? B * h->m : 0},  {"ip_zu", h->d.ip_zu, h->d.ip_zu ? B * h->m : 0},
       {"ip_rh", h->d.ip_rh, h->d.ip_rh ? B * h->m : 0},  {"ip_dl", h->d.ip_dl, h->d.ip_dl ? B * h->m : 0},
       {"ip_ds", h->d.ip_ds, h->d.ip_ds ? B * h->m : 0},  {"ip_dx", h->d.ip_dx, h->d.ip_dx ? B * h->n : 0},

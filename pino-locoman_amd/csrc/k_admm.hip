@@ -118,6 +118,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   const double* __restrict__ As = d.As + (size_t)b * nnz;
   const double* __restrict__ rho = d.rho + (size_t)b * m;
   const double* __restrict__ rhoc = d.rhoc + (size_t)b * (N + 1) * cpl_stride;
+  const double* __restrict__ Acp = d.Acpl + (size_t)b * (N + 1) * PL_ACPL;
   const double* __restrict__ ls = d.ls + (size_t)b * m;
   const double* __restrict__ us = d.us + (size_t)b * m;
   const double* __restrict__ qs = d.qs + (size_t)b * n;
@@ -161,29 +162,16 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   };
   auto prefetch_E = [&](int kind1, int i1, Early& E) __attribute__((always_inline)) {
     const bool fw = kind1 == KFWD || kind1 == KTN;
-    const bool fr = fw && !fwd_asb;  // coupling A values through registers
     const int g = fw ? i1 - 1 : i1;
-    const uint16_t* P = PG + an[g].prog;
-    const int ncp = an[g].ncpl, eo = an[g].ent_off;
+    const int ncp = an[g].ncpl;
     const int s = min(lane, max(ncp - 1, 0));
-    {
-      const int q0 = P[an[g].cwptr + s], cnt = fr ? P[an[g].cwptr + s + 1] - q0 : 0;
-      const uint32_t* cw = reinterpret_cast<const uint32_t*>(P + an[g].cwp);
+    {  // coupling A values through registers, contiguous per node (d.Acpl, k_acpl)
+      const double* Ac = Acp + (size_t)g * PL_ACPL;
+      const int o1 = fw ? lane * CWM : 0, o2 = fw ? 64 * CWM + lane * XCM : 0;  // backward: unused, one line
 #pragma unroll
-      for (int k = 0; k < CWM; ++k) {
-        const int e = cnt > 0 ? (int)(cw[q0 + min(k, cnt - 1)] & 0xffff) : 0;
-        E.acw[k] = gld(As, eo + e);
-      }
-    }
-    {
-      const int c = min(lane, ndx - 1);
-      const int q0 = P[an[g].xcptr + c], cnt = fr ? P[an[g].xcptr + c + 1] - q0 : 0;
-      const uint32_t* xc = reinterpret_cast<const uint32_t*>(P + an[g].xcp);
+      for (int k = 0; k < CWM; ++k) E.acw[k] = gld(Ac, o1 + k);
 #pragma unroll
-      for (int k = 0; k < XCM; ++k) {
-        const int e = cnt > 0 ? (int)(xc[q0 + min(k, cnt - 1)] & 0xffff) : 0;
-        E.axc[k] = gld(As, eo + e);
-      }
+      for (int k = 0; k < XCM; ++k) E.axc[k] = gld(Ac, o2 + k);
     }
     E.rhoc = gld(rhoc, g * cpl_stride + s);
     E.tt = gld(reinterpret_cast<const uint4*>(d.ttab), max(an[i1].ttab, 0) / 4 + lane);
@@ -319,12 +307,15 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
         }
       }
     };
-    if (K <= KM && !reload) {
+    (void)reload;
+    if (K <= KM) {
       use_tt = true;
       pass(0, true);  // the common case, straight-line: the refill loads never force a wait
     } else {
+      // blocks with more than KM slots per lane: slots 0..KM-1 are already in R (the
+      // previous step's refill, as for every block); the rest load synchronously
       for (int kb = 0; kb < K; kb += KM) {
-        load_S(i, kb, R);  // blocks with more than KM slots per lane (synchronous)
+        if (kb > 0) load_S(i, kb, R);
         pass(kb, kb + KM >= K);
       }
     }
@@ -757,6 +748,39 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     if (lane == 0 && d.dbg)
       for (int k = 0; k < 10; ++k) d.dbg[(size_t)b * 16 + k] += (double)tacc[k];
   }
+}
+
+// Compact coupling A values of node i (one 64-lane block per (problem, node)), refreshed with
+// every factorisation: the forward step of the sweep gathers, per coupling row s, the A values
+// of its w part (cw list, PL_ADMM_CWM clamped slots) and, per dx_{i+1} column c, those of its
+// coupling entries (xc list, PL_ADMM_XCM slots).  Gathered from As they touch up to the
+// node's whole A slice (~56 lines of 128 B) for ~150 values; here they are 1.5 KB contiguous.
+__global__ __launch_bounds__(64) void k_acpl(PlDev d, int N, int nnz, int ndx) {
+  const int b = blockIdx.x / (N + 1), i = blockIdx.x - b * (N + 1);
+  const int lane = threadIdx.x;
+  const PlAdmmNode& a = d.anodes[i];
+  double* out = d.Acpl + ((size_t)b * (N + 1) + i) * PL_ACPL;
+  const double* As = d.As + (size_t)b * nnz + a.ent_off;
+  const uint16_t* P = d.aprog + a.prog;
+  const int ncp = a.ncpl;
+  {
+    const int s = min(lane, max(ncp - 1, 0));
+    const int q0 = ncp ? P[a.cwptr + s] : 0, cnt = ncp ? P[a.cwptr + s + 1] - q0 : 0;
+    const uint32_t* cw = reinterpret_cast<const uint32_t*>(P + a.cwp);
+    for (int k = 0; k < PL_ADMM_CWM; ++k)
+      out[lane * PL_ADMM_CWM + k] = cnt > 0 ? As[cw[q0 + min(k, cnt - 1)] & 0xffff] : 0.0;
+  }
+  {
+    const int c = min(lane, ndx - 1);
+    const int q0 = a.ncol ? P[a.xcptr + c] : 0, cnt = a.ncol ? P[a.xcptr + c + 1] - q0 : 0;
+    const uint32_t* xc = reinterpret_cast<const uint32_t*>(P + a.xcp);
+    for (int k = 0; k < PL_ADMM_XCM; ++k)
+      out[64 * PL_ADMM_CWM + lane * PL_ADMM_XCM + k] = cnt > 0 ? As[xc[q0 + min(k, cnt - 1)] & 0xffff] : 0.0;
+  }
+}
+
+void launch_acpl(PlOcpHandle* h) {
+  hipLaunchKernelGGL(k_acpl, dim3(h->B * (h->N + 1)), dim3(64), 0, h->stream, h->d, h->N, h->nnz, h->ndx);
 }
 
 namespace {

@@ -117,6 +117,7 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
   const double* __restrict__ As = d.As + (size_t)bb * nnz;
   const double* __restrict__ rho = d.rho + (size_t)bb * m;
   const double* __restrict__ rhoc = d.rhoc + (size_t)bb * (N + 1) * cpl_stride;
+  const double* __restrict__ Acp = d.Acpl + (size_t)bb * (N + 1) * PL_ACPL;
   const double* __restrict__ ls = d.ls + (size_t)bb * m;
   const double* __restrict__ us = d.us + (size_t)bb * m;
   const double* __restrict__ qs = d.qs + (size_t)bb * n;
@@ -154,29 +155,16 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
   };
   auto prefetch_E = [&](int kind1, int i1, Early2& E) __attribute__((always_inline)) {
     const bool fw = kind1 == KFWD || kind1 == KTN;
-    const bool fr = fw && !fwd_asb;
     const int g = fw ? i1 - 1 : i1;
-    const uint16_t* P = PG + an[g].prog;
-    const int ncp = an[g].ncpl, eo = an[g].ent_off;
+    const int ncp = an[g].ncpl;
     const int s = min(lane, max(ncp - 1, 0));
-    {
-      const int q0 = P[an[g].cwptr + s], cnt = fr ? P[an[g].cwptr + s + 1] - q0 : 0;
-      const uint32_t* cw = reinterpret_cast<const uint32_t*>(P + an[g].cwp);
+    {  // coupling A values, contiguous per node (d.Acpl, k_acpl)
+      const double* Ac = Acp + (size_t)g * PL_ACPL;
+      const int o1 = fw ? lane * CWM : 0, o2 = fw ? 64 * CWM + lane * XCM : 0;  // backward: unused, one line
 #pragma unroll
-      for (int k = 0; k < CWM; ++k) {
-        const int e = cnt > 0 ? (int)(cw[q0 + min(k, cnt - 1)] & 0xffff) : 0;
-        E.acw[k] = gld(As, eo + e);
-      }
-    }
-    {
-      const int c = min(lane, ndx - 1);
-      const int q0 = P[an[g].xcptr + c], cnt = fr ? P[an[g].xcptr + c + 1] - q0 : 0;
-      const uint32_t* xc = reinterpret_cast<const uint32_t*>(P + an[g].xcp);
+      for (int k = 0; k < CWM; ++k) E.acw[k] = gld(Ac, o1 + k);
 #pragma unroll
-      for (int k = 0; k < XCM; ++k) {
-        const int e = cnt > 0 ? (int)(xc[q0 + min(k, cnt - 1)] & 0xffff) : 0;
-        E.axc[k] = gld(As, eo + e);
-      }
+      for (int k = 0; k < XCM; ++k) E.axc[k] = gld(Ac, o2 + k);
     }
     E.rhoc = gld(rhoc, g * cpl_stride + s);
     {
@@ -321,12 +309,13 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
         }
       };
       const int nh = (K - h + 1) / 2;  // slots of this wave
-      if (K <= 2 * KH && !reload) {
+      (void)reload;
+      if (K <= 2 * KH) {
         use_tt = true;
         pass(0, true);
-      } else {
+      } else {  // slots of pass 0 are in R already (the previous step's refill)
         for (int j0 = 0; j0 < max(nh, 1); j0 += KH) {
-          load_S(i, j0, R);
+          if (j0 > 0) load_S(i, j0, R);
           pass(j0, j0 + KH >= nh);
         }
       }

@@ -566,6 +566,7 @@ void launch_factor_x(PlOcpHandle* h) {
 bool factor_supports_ndx(int ndx) { return ndx == 24 || ndx == 36 || ndx == 48; }
 
 void launch_factor(PlOcpHandle* h) {
+  launch_acpl(h);  // the sweep's compact coupling A values (k_admm.hip) for this As
   switch (h->ndx) {
     case 24: launch_factor_x<24>(h); break;
     case 36: launch_factor_x<36>(h); break;

@@ -97,7 +97,10 @@ __device__ __forceinline__ double next_mu(double mu, double tol) {
 // Initial point (warm_start_init_point): slacks pushed into the interior, lam = 0,
 // centred bound multipliers; theta_max / theta_min from theta(x0, s0).  Needs g, lbg,
 // ubg at d.x (k_eval_values).
-__global__ __launch_bounds__(256) void k_ip_init(PlDev d, int m, PlIpSettings st) {
+// warm: lam = lam0 (the previous solve's lam_g) and the slack-bound multipliers split by the
+// sign of lam (z_u - z_l = lam), pushed up to warm_push (oracle/ip_ref.py); cold: lam = 0,
+// z = mu / slack
+__global__ __launch_bounds__(256) void k_ip_init(PlDev d, int m, PlIpSettings st, int warm) {
   const int b = blockIdx.x;
   __shared__ double red[256];
   const double* g = d.g + (size_t)b * m;
@@ -125,12 +128,18 @@ __global__ __launch_bounds__(256) void k_ip_init(PlDev d, int m, PlIpSettings st
       sr = g[r];
       if (k.hl) sr = fmax(sr, l + pl);
       if (k.hu) sr = fmin(sr, u - pu);
-      if (k.hl) zlr = mu / (sr - l);
-      if (k.hu) zur = mu / (u - sr);
+      if (warm) {
+        const double lw = d.ip_lam0[(size_t)b * m + r];
+        if (k.hl) zlr = fmax(fmax(-lw, 0.0), st.warm_push);
+        if (k.hu) zur = fmax(fmax(lw, 0.0), st.warm_push);
+      } else {
+        if (k.hl) zlr = mu / (sr - l);
+        if (k.hu) zur = mu / (u - sr);
+      }
       th += fabs(g[r] - sr);
     }
     s[r] = sr;
-    lam[r] = 0.0;
+    lam[r] = warm ? d.ip_lam0[(size_t)b * m + r] : 0.0;
     zl[r] = zlr;
     zu[r] = zur;
   }
@@ -627,7 +636,7 @@ void enqueue_ip(PlOcpHandle* h) {
   const PlIpSettings st = h->ip;
   const PlSettings saved = h->set;
   launch_eval_values(h, h->d.x);
-  hipLaunchKernelGGL(k_ip_init, dim3(h->B), dim3(256), 0, h->stream, h->d, h->m, st);
+  hipLaunchKernelGGL(k_ip_init, dim3(h->B), dim3(256), 0, h->stream, h->d, h->m, st, h->ip_lam_warm);
   h->set.sigma = st.delta_w;  // factor: Ps + delta_w on the diagonal
   h->set.alpha = 1.0;         // ADMM sweep: x = x~, z = A x~
   for (int k = 0; k <= st.max_iter; ++k) {

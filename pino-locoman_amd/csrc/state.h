@@ -71,6 +71,7 @@ struct PlNode {
 #define PL_ADMM_MV 2        // columns per lane: nw <= 128
 #define PL_ADMM_MR 3        // rows per lane: nrow <= 192
 #define PL_ADMM_ASR_MAX 32  // A values per lane staged through registers (entries past 64 x ASR: global)
+#define PL_ACPL (64 * (PL_ADMM_CWM + PL_ADMM_XCM))  // coupling A values per node (d.Acpl)
 struct PlAdmmNode {
   int nw, nrow, ncol, ncpl, nent, nunit, ntile, ntl;  // nunit = K slots, ntile = T, ntl = tiles
   unsigned kmagic;  // ceil(2^32 / K): t / K == umulhi(t, kmagic) for the tile counts used
@@ -133,6 +134,7 @@ struct PlProbInfo {
 struct PlIpSettings {
   double tol, mu_init, bound_push, bound_frac, delta_w, delta_c;
   int max_iter, ls_max, n_refine, pad;
+  double warm_push;  // warm_start_mult_bound_push (1e-7, ocp.py:260)
 };
 struct PlIpInfo {
   double mu, theta_max, theta_min, err, f, alpha, alpha_z, viol_max;
@@ -186,6 +188,8 @@ struct PlDev {
   double* us;
   double* rho;
   double* rhoc;      // rho of the coupling rows, [N+1][ncpl_max] per problem (ADMM prefetch)
+  double* Acpl;      // scaled A of the coupling entries, [N+1][PL_ACPL] per problem, in the order the
+                     // sweep's forward step gathers them (k_acpl: [s][PL_ADMM_CWM] | [c][PL_ADMM_XCM])
   double* D;
   double* E;
   double* cs;        // cost scaling c (1 per problem)
@@ -210,6 +214,7 @@ struct PlDev {
   // interior point [B][m] (allocated by pl_ocp_set_solver(o, PL_SOLVER_IP))
   double* ip_s;      // slacks of the inequality rows
   double* ip_lam;    // constraint multipliers (lam_g)
+  double* ip_lam0;   // lam_g warm start (opti.set_initial(opti.lam_g, lam_g), ocp_whole_body_rnea.py:234-235)
   double* ip_zl;     // lower / upper bound multipliers of the slacks
   double* ip_zu;
   double* ip_rh;     // r^ of the reduced Newton system
@@ -242,6 +247,7 @@ struct PlOcpHandle {
   int chv_stride;                   // doubles of chain vectors per problem
   int jl_len;                       // k_eval_jac work-list entries (a multiple of 64 before the cheap part)
   int solver;                       // PL_SOLVER_OSQP (SQP + OSQP ADMM) or PL_SOLVER_IP (interior point)
+  int ip_lam_warm;                  // 1: the next interior-point solve starts from lam = ip_lam0
   PlIpSettings ip;
   long long fs_stride;              // factor scratch per problem (doubles)
   int nfgroup;                      // k_fnode launches: consecutive nodes with one program
@@ -281,6 +287,7 @@ void launch_admm2(PlOcpHandle* h, int niter, int check);
 bool admm_rc_supported(const PlOcpHandle* h);
 void launch_admm_rc(PlOcpHandle* h, int niter, int check);
 void launch_fred(PlOcpHandle* h);
+void launch_acpl(PlOcpHandle* h);
 long long rc_ch_stride(int N, int ndx);
 int rc_chv_stride(int N, int ndx);
 void launch_check(PlOcpHandle* h, int it, int final_check);

@@ -77,6 +77,7 @@ EXPORTS = {
     "pl_ocp_set_ip_settings": (C.c_int, [C.c_void_p, C.POINTER(IpSettings)]),
     "pl_ocp_ip_stats": (C.c_int, [C.c_void_p, C.POINTER(IpStats)]),
     "pl_ocp_get_lam": (C.c_int, [C.c_void_p, _dp]),
+    "pl_ocp_set_lam": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pl_debug_ip_direction": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),
     "pl_casadi_bind": (C.c_int, [C.c_void_p, C.c_int]),
     "pl_casadi_unbind": (None, []),

@@ -288,6 +288,15 @@ class BatchedOCP:
         _lib.check(_lib.lib().pl_ocp_ip_stats(self.h, stats))
         return {k: np.array([np.array(getattr(s, k)) for s in stats]) for k, _ in _lib.IpStats._fields_}
 
+    def set_lam(self, lam):
+        """lam_g warm start of the next interior-point solves ([batch][m] or None for the
+        cold start), the OCPs' opti.set_initial(opti.lam_g, lam_g) (ocp_whole_body_rnea.py:234-235)."""
+        if lam is None:
+            _lib.check(_lib.lib().pl_ocp_set_lam(self.h, None))
+            return
+        lam = np.ascontiguousarray(np.broadcast_to(np.asarray(lam, dtype=np.float64), (self.batch, self.m)))
+        _lib.check(_lib.lib().pl_ocp_set_lam(self.h, _lib.dptr(lam)))
+
     def get_lam(self):
         lam = np.zeros((self.batch, self.m))
         _lib.check(_lib.lib().pl_ocp_get_lam(self.h, _lib.dptr(lam)))
@@ -529,6 +538,8 @@ class OCP:
                         u = np.concatenate([u, u_prev[self.tau_idx:]])
                 o = L.x_off[i] + L.ndx
                 x[o:o + L.nu[i]] = u
+        if self.solver == "fatrop" and self.lam_g is not None:  # ocp_whole_body_rnea.py:234-235 (every OCP)
+            self._backend.set_lam(self.lam_g)
 
     # ------------------------------------------------------------------ solver
     def init_solver(self):

@@ -85,6 +85,14 @@ IP_CONFIGS = [
     ("ip_b2_aba_n40", "b2", "whole_body_aba", 40, [("syn", 0)], 0, "trot"),
     ("ip_b2g_acc_n50", "b2g", "whole_body_acc", 50, [("syn", 0)], 0, "trot"),
     ("ip_b2g_rnea_n50", "b2g", "whole_body_rnea", 50, [("syn", 0)], 0, "trot"),
+    # centroidal_vel from the feasible standing point (a well-conditioned trajectory beside the
+    # chaotic cold starts of ip_go2_cv_n20), and the variants without the base in u and
+    # centroidal_acc, each with a standing and a synthetic problem
+    ("ip_go2_cv_n20_stand", "go2", "centroidal_vel", 20, [("stand",), ("syn", 2)], 0, "stand"),
+    ("ip_go2_cv_nb_n20", "go2", "centroidal_vel", 20, [("stand",), ("syn", 2)], 0, "stand", {"include_base": False}),
+    ("ip_go2_ca_n20", "go2", "centroidal_acc", 20, [("stand",), ("syn", 0)], 0, "stand", {"include_base": True}),
+    ("ip_go2_acc_nb_n20", "go2", "whole_body_acc", 20, [("stand",), ("syn", 0)], 0, "stand",
+     {"include_base": False}),
 ]
 
 
@@ -114,12 +122,19 @@ def make_problem(R, lay, dyn, N, spec):
         Jb = np.stack([rbd.rnea_dynamics(M, frames, R.q0, z, z, np.eye(12)[k])[:6] - base[:6] for k in range(12)], 1)
         f = np.linalg.lstsq(Jb, -base[:6], rcond=None)[0]
         tau = rbd.rnea_dynamics(M, frames, R.q0, z, z, f)
-        assert dyn == "whole_body_rnea"
         x = np.zeros(lay.n)
         for i in range(N):
             o = lay.x_off[i] + lay.ndx
-            u = np.concatenate([np.zeros(R.nv), f] + ([tau[6:]] if i < lay.tau_nodes else []))
+            if dyn == "whole_body_rnea":
+                u = np.concatenate([np.zeros(R.nv), f] + ([tau[6:]] if i < lay.tau_nodes else []))
+            elif dyn == "whole_body_aba":  # u = [tau_j, f]
+                u = np.concatenate([tau[6:], f])
+            else:  # acc / centroidal families: zero accelerations / velocities, the same forces
+                u = np.concatenate([np.zeros(lay.f_idx), f])
             x[o:o + lay.nu[i]] = u
+        if dyn == "centroidal_vel":  # x = [h, q]: zero momentum
+            xs = np.concatenate([np.zeros(6), R.q0])
+            vals["x_init"] = xs
         return lay.pack(vals), x, xs, 0.0
     gidx = spec[1]
     vals, xs, t0 = problem_values(R, dyn, N, gidx, lay)
@@ -265,21 +280,23 @@ def sqp_fixture(name, rname, dyn, N, problems, loop_steps, gait, osqp, njac, kw=
           flush=True)
 
 
-def ip_fixture(name, rname, dyn, N, problems, loop_steps, gait):
+def ip_fixture(name, rname, dyn, N, problems, loop_steps, gait, kw=None):
     from oracle.ip_ref import IP_SETTINGS, IPRef
+    kw = kw or {}
     R = robots.ROBOTS[rname]()
     R.set_gait_sequence(gait, 0.8)
-    lay = Layout(R, dyn, N)
+    lay = Layout(R, dyn, N, **kw)
     B = len(problems)
     P, X, XS, T0 = (np.zeros((B, lay.np)), np.zeros((B, lay.n)), np.zeros((B, lay.nx)), np.zeros(B))
     for b, spec in enumerate(problems):
         P[b], X[b], XS[b], T0[b] = make_problem(R, lay, dyn, N, spec)
     mi = IP_SETTINGS["max_iter"]
-    rec = {"P": P, "X": X, "XS": XS, "T0": T0, "gait": np.array(gait), "kinds": np.array([s[0] for s in problems])}
+    rec = {"P": P, "X": X, "XS": XS, "T0": T0, "gait": np.array(gait), "kinds": np.array([s[0] for s in problems]),
+           "include_base": int(kw.get("include_base", True))}
     per = {k: [] for k in ("x_out", "lam", "s", "zl", "zu", "status", "iter", "err", "mu", "f", "alphas", "trials",
                            "viol_max")}
     for b in range(B):
-        o = OracleOCP(R, dyn, N)
+        o = OracleOCP(R, dyn, N, **kw)
         x, lam, st = IPRef(o).solve(X[b], P[b])
         g, lbg, ubg = o.eval_g(x, P[b])
         al = np.zeros(mi)
@@ -293,9 +310,10 @@ def ip_fixture(name, rname, dyn, N, problems, loop_steps, gait):
     # closed loop of problem 0 (run_mpc.py:115-143 with the Fatrop solver): warm start,
     # one interior-point solve, x <- integrate(x, DX[1])
     if loop_steps > 1:
-        o = OracleOCP(R, dyn, N)
+        o = OracleOCP(R, dyn, N, **kw)
         xs, x = XS[0].copy(), X[0].copy()
         states, stl = [], []
+        lam_prev = None
         for k in range(loop_steps):
             p = P[0].copy()
             contact, swing = R.gait_sequence.get_gait_schedule(T0[0] + k * DT_MIN, horizon_dts(DT_MIN, DT_MAX, N), N)
@@ -305,7 +323,8 @@ def ip_fixture(name, rname, dyn, N, problems, loop_steps, gait):
                 p[o_:o_ + s_] = lay.pack(vals)[o_:o_ + s_]
             if k > 0:
                 x = o.warm_start(x, p)
-            x, _, st = IPRef(o).solve(x, p)
+            # lam_g carried across solves (ocp_whole_body_rnea.py:234-235, ocp.py:373)
+            x, lam_prev, st = IPRef(o).solve(x, p, lam0=lam_prev)
             DX, _ = o.split(x)
             xs = o.integrate_state(xs, DX[1])
             states.append(xs)
