@@ -682,7 +682,7 @@ int build_admm_prog(pl_ocp* o) {
     h.admm_asr = nmax[dom] <= 16 * 64 ? 16 : PL_ADMM_ASR_MAX;
   }
   if (!factor_supports_ndx(ndx)) {
-    pl_set_error("state dimension ndx = %d is not supported by the factor kernel (24, 36, 48)", ndx);
+    pl_set_error("state dimension ndx = %d is not supported by the factor kernel (24, 30, 36, 48)", ndx);
     return -1;
   }
   if (h.nrow_max > 64 * PL_ADMM_MR || h.nw_max > 64 * PL_ADMM_MV || h.ncpl_max > 64) {

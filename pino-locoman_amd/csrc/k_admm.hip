@@ -307,15 +307,14 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
         }
       }
     };
-    (void)reload;
-    if (K <= KM) {
+    if (K <= KM && !reload) {
       use_tt = true;
       pass(0, true);  // the common case, straight-line: the refill loads never force a wait
     } else {
       // blocks with more than KM slots per lane: slots 0..KM-1 are already in R (the
-      // previous step's refill, as for every block); the rest load synchronously
+      // previous step's refill) unless `reload`; the rest load synchronously
       for (int kb = 0; kb < K; kb += KM) {
-        if (kb > 0) load_S(i, kb, R);
+        if (kb > 0 || reload) load_S(i, kb, R);
         pass(kb, kb + KM >= K);
       }
     }

@@ -309,13 +309,12 @@ __global__ __launch_bounds__(128 * PPW, 1) void k_admm2(PlDev d, int B, int N, i
         }
       };
       const int nh = (K - h + 1) / 2;  // slots of this wave
-      (void)reload;
-      if (K <= 2 * KH) {
+      if (K <= 2 * KH && !reload) {
         use_tt = true;
         pass(0, true);
-      } else {  // slots of pass 0 are in R already (the previous step's refill)
+      } else {  // slots of pass 0 are in R already (the previous step's refill) unless `reload`
         for (int j0 = 0; j0 < max(nh, 1); j0 += KH) {
-          if (j0 > 0) load_S(i, j0, R);
+          if (j0 > 0 || reload) load_S(i, j0, R);
           pass(j0, j0 + KH >= nh);
         }
       }

@@ -737,7 +737,7 @@ long long rc_ch_stride(int N, int ndx) { return (long long)(N + 1) * 3 * ndx * n
 int rc_chv_stride(int N, int ndx) { return 6 * (N + 2) * ndx; }
 
 bool admm_rc_supported(const PlOcpHandle* h) {
-  return (h->ndx == 24 || h->ndx == 36 || h->ndx == 48) && (h->rc_waves == 4 || h->rc_waves == 8) && h->nw_max <= 64 * MV && h->nrow_max <= 64 * MR && h->ncpl_max <= 64 &&
+  return (h->ndx == 24 || h->ndx == 30 || h->ndx == 36 || h->ndx == 48) && (h->rc_waves == 4 || h->rc_waves == 8) && h->nw_max <= 64 * MV && h->nrow_max <= 64 * MR && h->ncpl_max <= 64 &&
          rc_config(h, h->rc_waves).lds <= 160 * 1024;
 }
 
@@ -756,6 +756,8 @@ void launch_admm_rc(PlOcpHandle* h, int niter, int check) {
   const RcCfg c = rc_config(h, h->rc_waves);
   switch (h->ndx * 16 + h->rc_waves) {
     case 24 * 16 + 4: launch_rc_t<4, 24>(h, niter, check, c); break;
+    case 30 * 16 + 4: launch_rc_t<4, 30>(h, niter, check, c); break;
+    case 30 * 16 + 8: launch_rc_t<8, 30>(h, niter, check, c); break;
     case 36 * 16 + 4: launch_rc_t<4, 36>(h, niter, check, c); break;
     case 48 * 16 + 4: launch_rc_t<4, 48>(h, niter, check, c); break;
     case 24 * 16 + 8: launch_rc_t<8, 24>(h, niter, check, c); break;

@@ -373,18 +373,23 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
     __syncthreads();
     T(-1);
     if (w == 0) {
-      // ---- S_xx = (A' + E_i)^-1, one column per lane
-      double col[X];
+      // ---- S_xx = (A' + E_i)^-1, one column per lane.  The sweep runs on XS = X rounded up
+      // to 4 pivots: rows / columns X..XS-1 are an identity pad (their pivots are no-ops),
+      // e.g. X = 30 for B2G centroidal_vel (6 + nv).
+      constexpr int XS = (X + 3) & ~3;
+      double col[XS];
 #pragma unroll
-      for (int r = 0; r < X; ++r)
+      for (int r = 0; r < XS; ++r)
       {
-        // lanes >= X duplicate column X - 1: never pivots, never published, never stored
-        const int lc = min(l, X - 1);
-        col[r] = Ag[r * X + lc] + Eb[r >= lc ? r * X + lc : lc * X + r];
+        // lanes >= XS duplicate column XS - 1: never pivots, never published, never stored
+        const int lc = min(l, XS - 1);
+        const int rc = min(r, X - 1), cc = min(lc, X - 1);
+        const double v = Ag[rc * X + cc] + Eb[rc >= cc ? rc * X + cc : cc * X + rc];
+        col[r] = (r < X && lc < X) ? v : (r == lc ? 1.0 : 0.0);
       }
       unsigned long long ts0 = 0;
       if (TIMING) ts0 = __builtin_amdgcn_s_memtime();
-      sweep_rot<X, 0, X>(col, pb, 8 * 64, l, X / 4, true, true, true);
+      sweep_rot<XS, 0, XS>(col, pb, 8 * 64, l, XS / 4, true, true, true);
       if (TIMING) {
         const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
         if (l == 0) tacc[5] += ts1 - ts0;
@@ -423,7 +428,7 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
     // ---- S_ux = -G S_xx (U x X) and S_uu = C^-1 - G S_ux^T (U x U, lower) on the f64
     // MFMA: wave w owns the 16-row tile mt = w of both; K = X in steps of 4.
     {
-      constexpr int KX = X / 4;
+      constexpr int KX = (X + 3) / 4;  // K = X in steps of 4 (a partial last step is masked)
       constexpr int NX = (X + 15) / 16;
       const int mt = w;
       const bool act = 16 * mt < U;
@@ -431,8 +436,9 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
       double ga[KX];  // G[16 mt + (l & 15)][4 kk + (l >> 4)]
 #pragma unroll
       for (int kk = 0; kk < KX; ++kk) {
-        const double v = Ag[X * X + min(arow, max(U - 1, 0)) * X + 4 * kk + (l >> 4)];
-        ga[kk] = v * ((act && arow < U) ? 1.0 : 0.0);
+        const int kc = 4 * kk + (l >> 4);
+        const double v = Ag[X * X + min(arow, max(U - 1, 0)) * X + min(kc, X - 1)];
+        ga[kk] = v * ((act && arow < U && kc < X) ? 1.0 : 0.0);
       }
       if (act) {
 #pragma unroll
@@ -441,8 +447,9 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
           const int bc = 16 * nt + (l & 15);
 #pragma unroll
           for (int kk = 0; kk < KX; ++kk) {
-            const double bv0 = Sl[sidx(4 * kk + (l >> 4), min(bc, X - 1))];
-            const double bv = bv0 * (bc < X ? 1.0 : 0.0);
+            const int kc = 4 * kk + (l >> 4);
+            const double bv0 = Sl[sidx(min(kc, X - 1), min(bc, X - 1))];
+            const double bv = bv0 * ((bc < X && kc < X) ? 1.0 : 0.0);
             acc = mfma4(ga[kk], bv, acc);
           }
 #pragma unroll
@@ -467,8 +474,9 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
           }
 #pragma unroll
           for (int kk = 0; kk < KX; ++kk) {
-            const double bv0 = Sl[lidx(X + min(bu, U - 1), 4 * kk + (l >> 4))];
-            const double bv = bv0 * (bu < U ? 1.0 : 0.0);
+            const int kc = 4 * kk + (l >> 4);
+            const double bv0 = Sl[lidx(X + min(bu, U - 1), min(kc, X - 1))];
+            const double bv = bv0 * ((bu < U && kc < X) ? 1.0 : 0.0);
             acc = mfma4(ga[kk], bv, acc);
           }
 #pragma unroll
@@ -562,13 +570,15 @@ void launch_factor_x(PlOcpHandle* h) {
 }  // namespace
 
 // ndx values of the shipped models: 36 (Go2 / B2 whole body), 48 (B2G whole body),
-// 24 (Go2 / B2 centroidal_vel: 6 + nv); the handle refuses others.
-bool factor_supports_ndx(int ndx) { return ndx == 24 || ndx == 36 || ndx == 48; }
+// 24 (Go2 / B2 centroidal_vel: 6 + nv), 30 (B2G centroidal_vel, swept with a 2-row identity
+// pad); the handle refuses others.
+bool factor_supports_ndx(int ndx) { return ndx == 24 || ndx == 30 || ndx == 36 || ndx == 48; }
 
 void launch_factor(PlOcpHandle* h) {
   launch_acpl(h);  // the sweep's compact coupling A values (k_admm.hip) for this As
   switch (h->ndx) {
     case 24: launch_factor_x<24>(h); break;
+    case 30: launch_factor_x<30>(h); break;
     case 36: launch_factor_x<36>(h); break;
     case 48: launch_factor_x<48>(h); break;
     default: break;

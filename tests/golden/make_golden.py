@@ -74,6 +74,8 @@ SQP_CONFIGS = [
     # ocp_centroidal_vel.py:9-23, 119-129): v_b = A_b^-1 (m h - A_j v_j) inside the rows
     ("go2_cv_nb_n20", "go2", "centroidal_vel", 20, [("syn", k) for k in range(4)], 3, "trot", {}, 2,
      {"include_base": False}),
+    # B2G centroidal_vel (ndx = 30: the factor sweeps with a 2-row identity pad)
+    ("b2g_cv_n50", "b2g", "centroidal_vel", 50, [("syn", k) for k in range(4)], 3, "trot", {}, 1),
 ]
 
 # Interior-point (Fatrop branch) fixtures: name, robot, dynamics, N, problems, closed-loop

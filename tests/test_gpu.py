@@ -37,7 +37,9 @@ ACCF = [("go2_acc_nb_n20", "go2", "whole_body_acc", 20), ("go2_ca_n20", "go2", "
         ("go2_ca_nb_n20", "go2", "centroidal_acc", 20), ("b2g_ca_n50", "b2g", "centroidal_acc", 50),
         ("b2g_acc_nb_n50", "b2g", "whole_body_acc", 50),
         # centroidal_vel with include_base=False (v_b = A_b^-1 (m h - A_j v_j) in the rows)
-        ("go2_cv_nb_n20", "go2", "centroidal_vel", 20)]
+        ("go2_cv_nb_n20", "go2", "centroidal_vel", 20),
+        # B2G centroidal_vel: ndx = 6 + nv = 30, the factor sweeps with a 2-row identity pad
+        ("b2g_cv_n50", "b2g", "centroidal_vel", 50)]
 
 
 def _rel(a, b):
@@ -139,7 +141,7 @@ def test_fixture_coverage():
 
 
 @pytest.mark.parametrize("name,rname,dyn,N", [CONFIGS[0], CONFIGS[1], EDGE[0], EDGE[1], EDGE[4], ACCF[0], ACCF[1],
-                                               ACCF[5]])
+                                               ACCF[5], ACCF[6]])
 def test_device_mpc_loop_matches_oracle_loop(name, rname, dyn, N):
     """run_mpc.py:127-143 executed on the device (gait, x_init, warm start, solve,
     x <- integrate(x, DX[1])) vs the oracle's closed loop in the golden file: states

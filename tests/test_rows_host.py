@@ -59,6 +59,9 @@ def _consts(bo):
     # centroidal_vel without the base: v_b = A_b^-1 (m h - A_j v_j) inside the rows
     ("go2", "centroidal_vel", 20, [0, 1, 9, 19], {"include_base": False}),
     ("b2", "centroidal_vel", 20, [0, 10], {"include_base": False}),
+    # B2G (Z1 arm) centroidal_vel: ndx = 6 + nv = 30 (arm joints in the centroidal map)
+    ("b2g", "centroidal_vel", 50, [0, 1, 25, 49], {}),
+    ("b2g", "centroidal_vel", 50, [0, 30], {"include_base": False}),
 ])
 def test_node_rows_and_dual_jacobian(harness, rname, dyn, N, nodes_checked, kw):
     from pinoloco.ocp import BatchedOCP
