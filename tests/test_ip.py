@@ -53,7 +53,10 @@ CHAOTIC = {("ip_go2_cv_n20", 0), ("ip_go2_cv_n20", 1),
 # centroidal_vel start, whose reduced Newton systems at iterations 2 and 4 are
 # ill-conditioned: measured there dx 1e-8 / 9e-8 and dlam 6e-7 / 9e-7 against the oracle's
 # sparse LU, 1e-15 at its other 8 iterations (gpurun_out/ip_forced_ip_go2_cv_n20_0.json).
-TF_TOL = {("ip_go2_cv_n20", 0): 2e-6}
+TF_TOL = {("ip_go2_cv_n20", 0): 2e-6,
+          # iteration 2 of this infeasible start: dlam 8.1e-8, dx 9e-9 (ill-conditioned reduced
+          # system); 1e-13 at the other 9 iterations (profiles/r03e/ip_forced_ip_go2_acc_nb_n20_1.json)
+          ("ip_go2_acc_nb_n20", 1): 2e-7}
 # Fixtures whose every problem is chaotic: no trajectory test (it would check nothing); their
 # directions are teacher-forced, and ip_go2_cv_n20_stand checks a centroidal_vel trajectory.
 TRAJ_EXCLUDED = {"ip_go2_cv_n20"}
