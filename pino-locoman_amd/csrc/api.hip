@@ -1077,6 +1077,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   h.admm_waves = 1;
   h.admm_rc = 0;
   h.rc_waves = 8;
+  h.ruiz_fused = !(getenv("PL_RUIZ_FUSED") && atoi(getenv("PL_RUIZ_FUSED")) == 0);
   h.ch_stride = rc_ch_stride(h.N, h.ndx);
   h.chv_stride = rc_chv_stride(h.N, h.ndx);
   h.gait_type = d->gait_type;
@@ -1117,6 +1118,19 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= upload(o, &D.gr_ec, o->gr_ec);
   rc |= upload(o, &D.gc_ptr, o->gc_ptr);
   rc |= upload(o, &D.gc_er, o->gc_er);
+  if (h.n < 65536 && h.m < 65536) {  // entry coordinates of the fused Ruiz kernel (k_qp.hip)
+    std::vector<uint32_t> erc(h.nnz);
+    for (int i = 0; i < h.N; ++i) {
+      const PlNode& nd = o->nodes[i];
+      for (int e = 0; e < nd.nent; ++e) {
+        const int lc = o->entcol[nd.ent_off + e];
+        const int r = nd.row_off + o->rowidx[nd.ent_off + e];
+        const int j = lc < nd.nw ? nd.x_off + lc : o->nodes[i + 1].x_off + (lc - nd.nw);
+        erc[nd.ent_off + e] = ((uint32_t)r << 16) | (uint32_t)j;
+      }
+    }
+    rc |= upload(o, &D.erc, erc);
+  }
   rc |= upload(o, &D.anodes, o->anodes);
   rc |= upload(o, &D.aprog, o->aprog);
   rc |= upload(o, &D.fprog, o->fprog);

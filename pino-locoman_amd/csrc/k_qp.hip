@@ -202,6 +202,145 @@ __global__ __launch_bounds__(256) void k_ruiz_norms(PlDev d, int N, int n, int m
   }
 }
 
+// All passes of the equilibration in one launch, one 1024-thread workgroup per problem
+// (the same D, E and c bit for bit as k_ruiz_norms + k_ruiz_update: maxima are exact in
+// any order, D_j max(a, b) = max(D_j a, D_j b) under monotone rounding, and the cost sum
+// keeps k_ruiz_update's 256-thread order).  D and E live in LDS for the whole launch; a
+// pass reads the problem's A twice (column maxima with the old E, then row maxima with the
+// old D) in entry order, coalesced, into one LDS buffer of maxima (ds_max_u64 on the bit
+// patterns of the non-negative products; NaN products are skipped as fmax does).  With
+// one workgroup per CU the A slices of the resident problems (~0.36 MB each at the
+// headline size) stay in the Infinity Cache across the passes, so HBM sees A about once.
+namespace {
+__device__ __forceinline__ void lds_max_bits(unsigned long long* p, double v) {
+  if (v == v) __hip_atomic_fetch_max(p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+constexpr int RUIZ_NT = 1024, RUIZ_PER = 8;  // n, m <= RUIZ_NT x RUIZ_PER
+constexpr int RUIZ_U = 16;                   // entries per thread with loads in flight together
+
+// f(coordinates, |A_e|) over the problem's entries, RUIZ_U loads per thread issued together
+template <class F>
+__device__ __forceinline__ void ruiz_sweep(const double* A, const uint32_t* erc, int nnz, F f) {
+  const int tid = threadIdx.x;
+  for (int e0 = 0; e0 < nnz; e0 += RUIZ_U * RUIZ_NT) {
+    uint32_t w[RUIZ_U];
+    double a[RUIZ_U];
+#pragma unroll
+    for (int u = 0; u < RUIZ_U; ++u) {
+      const int e = min(e0 + u * RUIZ_NT + tid, nnz - 1);
+      w[u] = erc[e];
+      a[u] = A[e];
+    }
+#pragma unroll
+    for (int u = 0; u < RUIZ_U; ++u)
+      if (e0 + u * RUIZ_NT + tid < nnz) f(w[u], fabs(a[u]));
+  }
+}
+}  // namespace
+
+__global__ __launch_bounds__(RUIZ_NT) void k_ruiz_fused(PlDev d, int n, int m, int nnz, int passes) {
+  extern __shared__ double lds[];
+  __shared__ double red[256];
+  __shared__ double c_sh;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  double* Dl = lds;
+  double* El = Dl + ((n + 1) & ~1);
+  unsigned long long* mx = reinterpret_cast<unsigned long long*>(El + ((m + 1) & ~1));
+  const double* A = d.Araw + (size_t)b * nnz;
+  const double* P = d.P + (size_t)b * n;
+  const double* q = d.grad + (size_t)b * n;
+  const uint32_t* __restrict__ erc = d.erc;
+  for (int j = tid; j < n; j += RUIZ_NT) Dl[j] = 1.0;
+  for (int r = tid; r < m; r += RUIZ_NT) El[r] = 1.0;
+  double c = 1.0;
+  double Pa[RUIZ_PER];
+#pragma unroll
+  for (int k = 0; k < RUIZ_PER; ++k) {
+    const int j = tid + RUIZ_NT * k;
+    Pa[k] = j < n ? fabs(P[j]) : 0.0;
+  }
+  for (int pass = 0; pass < passes; ++pass) {
+    // ---- column maxima max_r |A_rj| E_r -> Dt_j
+    for (int j = tid; j < n; j += RUIZ_NT) mx[j] = 0ull;
+    __syncthreads();
+    ruiz_sweep(A, erc, nnz, [&](uint32_t w, double a) __attribute__((always_inline)) {
+      lds_max_bits(mx + (w & 0xffff), a * El[w >> 16]);
+    });
+    __syncthreads();
+    double dt[RUIZ_PER];
+#pragma unroll
+    for (int k = 0; k < RUIZ_PER; ++k) {
+      const int j = tid + RUIZ_NT * k;
+      dt[k] = 0.0;
+      if (j < n) {
+        const double dj = Dl[j];
+        dt[k] = fmax(c * dj * dj * Pa[k], dj * __longlong_as_double((long long)mx[j]));
+      }
+    }
+    __syncthreads();
+    // ---- row maxima max_j |A_rj| D_j -> Et_r
+    for (int r = tid; r < m; r += RUIZ_NT) mx[r] = 0ull;
+    __syncthreads();
+    ruiz_sweep(A, erc, nnz, [&](uint32_t w, double a) __attribute__((always_inline)) {
+      lds_max_bits(mx + (w >> 16), a * Dl[w & 0xffff]);
+    });
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RUIZ_PER; ++k) {
+      const int r = tid + RUIZ_NT * k;
+      if (r < m) El[r] *= 1.0 / sqrt(limit_scaling(El[r] * __longlong_as_double((long long)mx[r])));
+      const int j = tid + RUIZ_NT * k;
+      if (j < n) Dl[j] = Dl[j] * (1.0 / sqrt(limit_scaling(dt[k])));
+    }
+    __syncthreads();
+    // ---- cost normalisation (k_ruiz_update's order: 256 strided partial sums, then a tree)
+    double sum = 0.0, qmax = 0.0;
+    if (tid < 256) {
+      for (int j = tid; j < n; j += 256) {
+        const double dj = Dl[j];
+        sum += c * dj * dj * fabs(P[j]);
+        qmax = fmax(qmax, fabs(c * dj * q[j]));
+      }
+      red[tid] = sum;
+    }
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (tid < s) red[tid] += red[tid + s];
+      __syncthreads();
+    }
+    sum = red[0];
+    __syncthreads();
+    if (tid < 256) red[tid] = qmax;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (tid < s) red[tid] = fmax(red[tid], red[tid + s]);
+      __syncthreads();
+    }
+    if (tid == 0) {
+      double ct = fmax(sum / (double)n, limit_scaling(red[0]));
+      ct = limit_scaling(ct);
+      c_sh = c * (1.0 / ct);
+    }
+    __syncthreads();
+    c = c_sh;
+  }
+  double* D = d.D + (size_t)b * n;
+  double* E = d.E + (size_t)b * m;
+  for (int j = tid; j < n; j += RUIZ_NT) D[j] = Dl[j];
+  for (int r = tid; r < m; r += RUIZ_NT) E[r] = El[r];
+  if (tid == 0) d.cs[b] = c;
+}
+
+size_t ruiz_fused_lds(const PlOcpHandle* h) {
+  return (size_t)(((h->n + 1) & ~1) + ((h->m + 1) & ~1) + std::max(h->n, h->m)) * 8;
+}
+
+bool ruiz_fused_supported(const PlOcpHandle* h) {
+  return h->d.erc && h->n <= RUIZ_NT * RUIZ_PER && h->m <= RUIZ_NT * RUIZ_PER &&
+         ruiz_fused_lds(h) <= 156 * 1024;
+}
+
 __global__ __launch_bounds__(256) void k_ruiz_update(PlDev d, int n, int m) {
   const int b = blockIdx.x;
   __shared__ double red[256];
@@ -291,6 +430,18 @@ __global__ __launch_bounds__(256) void k_qp_finish(PlDev d, int N, int n, int m,
 
 void launch_qp_setup(PlOcpHandle* h) {
   const dim3 nodes_grid(h->B * (h->N + 1));
+  if (h->ruiz_fused && ruiz_fused_supported(h)) {
+    static bool fattr = false;
+    if (!fattr) {
+      hipFuncSetAttribute((const void*)k_ruiz_fused, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);  // + static
+      fattr = true;
+    }
+    hipLaunchKernelGGL(k_ruiz_fused, dim3(h->B), dim3(RUIZ_NT), ruiz_fused_lds(h), h->stream, h->d, h->n, h->m, h->nnz,
+                       h->set.scaling);
+    hipLaunchKernelGGL(k_qp_finish, nodes_grid, dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz,
+                       std::max(h->ncpl_max, 1), h->set);
+    return;
+  }
   hipLaunchKernelGGL(k_ruiz_init, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, h->m);
   const int nent_max = (std::max(h->nent_max, 1) + 1) & ~1, ncol_max = (std::max(h->ncol_max, h->nw_max) + 1) & ~1;
   const int nrow_max = (std::max(h->nrow_max, 1) + 1) & ~1, chunk_max = (std::max(h->chunk_max, 1) + 1) & ~1;

@@ -160,6 +160,7 @@ struct PlDev {
   int2* gr_ec;
   int* gc_ptr;       // global CSC of A: column j's (entry, row) pairs at gc_er[gc_ptr[j] ..)
   int2* gc_er;
+  uint32_t* erc;         // (global row << 16 | global column) of each entry, for k_ruiz_fused (n, m < 65536)
   PlAdmmNode* anodes;    // N + 1 node tables (ADMM and factor programs)
   uint16_t* aprog;       // distinct ADMM programs, concatenated
   uint16_t* fprog;       // distinct factor programs, concatenated
@@ -241,6 +242,7 @@ struct PlOcpHandle {
   int admm_fwd_asb;                 // coupling rows too dense for registers: forward steps stage A in LDS
   int sqp_iters;                    // SQP iterations per solve (reference: 1, ocp.py:382-383)
   int admm_waves;                   // ADMM sweep kernel: 2 = k_admm2 (two waves per problem), 1 = k_admm
+  int ruiz_fused;                   // 1: all equilibration passes in k_ruiz_fused (PL_RUIZ_FUSED=0: per-pass kernels)
   int admm_rc;                      // 1: reduced-chain ADMM (k_admm_rc.hip) instead of the sweeps
   int rc_waves;                     // waves per problem of k_admm_rc (4 or 8)
   long long ch_stride;              // doubles of chain blocks per problem

@@ -6,7 +6,8 @@ problem) run the same OSQP 0.6 iteration (osqp.solve(), optimization/ocp.py:401)
 same block factor; they differ only in summation order.  Bars:
 
 * every golden fixture with the chain kernel: the bars of test_gpu.py (solver outcome
-  exact, dx / new iterate <= 2e-7, violation metric <= 1e-10 at the returned point);
+  exact, dx / new iterate <= step_tol -- 1e-9 but for two named edge fixtures --,
+  violation metric <= 1e-10 at the returned point);
 * the kernels against each other on the BASELINE fixtures: outcome exact, dx <= 1e-9;
 * chain-kernel batch invariance and repeatability: bit-exact (a problem gives the same bits
   in any batch that runs this kernel; across kernels the order of the sums differs);
@@ -16,7 +17,7 @@ import numpy as np
 import pytest
 
 from conftest import golden, make_robot
-from test_gpu import ACCF, CONFIGS, EDGE, _batched, _rel
+from test_gpu import ACCF, CONFIGS, EDGE, _batched, _rel, step_tol
 
 pytestmark = pytest.mark.gpu
 
@@ -47,8 +48,8 @@ def test_chain_sqp_step_matches_golden(name, rname, dyn, N):
         if np.all(np.isnan(G["dx"][b])):
             assert np.all(np.isnan(dx[b])) and np.array_equal(xn[b], G["X"][b])
         else:
-            assert _rel(dx[b], G["dx"][b]) < 2e-7, b
-        assert _rel(xn[b], G["x_new"][b]) < 2e-7, b
+            assert _rel(dx[b], G["dx"][b]) < step_tol(name), b
+        assert _rel(xn[b], G["x_new"][b]) < step_tol(name), b
         g, l, u = o.eval_g(xn[b], G["P"][b])
         assert st["viol_max"][b] == pytest.approx(o.violation_max(g, l, u), rel=1e-10, abs=1e-14), b
 

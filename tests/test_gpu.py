@@ -6,14 +6,15 @@ oracle itself on the same seeded inputs.  Tolerances (fp64 throughout):
 * g, lbg/ubg, grad, f and the Jacobian values J_g:   <= 1e-12 relative to max |.|
   (lbg/ubg bit-exact);
 * one SQP iteration: OSQP status, ADMM iteration count, line-search branch,
-  trial count and step length exact; QP step dx and new iterate <= 2e-7
-  relative (inf-norm) -- the GPU factors the reduced system P + sigma I + A^T R A
-  with block inverses, the oracle (and the CPU baseline) the quasi-definite KKT
-  with LU / LDL^T.  The reduced matrix is ill-conditioned (sigma = 1e-6 against
-  rho_eq = 20 rows), so after 100 ADMM iterations the two differ by 1e-13 .. 9e-10
-  on the BASELINE configs, 5e-9 .. 1e-7 on the yawed / all-stance edge problems
-  (profiles/r02b_parity_errors.json); the oracle's own spread across LU orderings
-  is ~1e-12 and the CPU baseline's ~1e-11;
+  trial count and step length exact; QP step dx and new iterate <= 1e-9 relative
+  (inf-norm) on every fixture except the two named in STEP_TOL.  The GPU
+  factors the reduced system P + sigma I + A^T R A with block inverses, the oracle
+  (and the CPU baseline) the quasi-definite KKT with LU / LDL^T; the reduced matrix is
+  ill-conditioned (sigma = 1e-6 against rho_eq = 20 rows), so after up to 100 ADMM
+  iterations the two differ by 8e-14 .. 8.2e-10 on the BASELINE and acc-family
+  fixtures with every ADMM kernel, 5.4e-9 on the walking-gait problem and 1.0e-7 on
+  the all-stance problem (profiles/r03f/parity_errors.json, tools/parity_report.py);
+  the oracle's own spread across LU orderings is ~1e-12 and the CPU baseline's ~1e-11;
 * 4-step closed MPC loop on the device: states <= 1e-7 relative (SURVEY 8c);
 * batch invariance and repeatability: bit-exact.
 """
@@ -40,6 +41,15 @@ ACCF = [("go2_acc_nb_n20", "go2", "whole_body_acc", 20), ("go2_ca_n20", "go2", "
         ("go2_cv_nb_n20", "go2", "centroidal_vel", 20),
         # B2G centroidal_vel: ndx = 6 + nv = 30, the factor sweeps with a 2-row identity pad
         ("b2g_cv_n50", "b2g", "centroidal_vel", 50)]
+
+
+# step bars looser than 1e-9, with the error measured on them (all ADMM kernels)
+STEP_TOL = {"go2_rnea_n20_walk": 2e-8,    # measured 5.4e-9
+            "go2_rnea_n20_stand": 3e-7}   # measured 1.0e-7 (all four feet in stance)
+
+
+def step_tol(name):
+    return STEP_TOL.get(name, 1e-9)
 
 
 def _rel(a, b):
@@ -91,7 +101,7 @@ def test_eval_sqp_data_matches_golden(name, rname, dyn, N):
 
 @pytest.mark.parametrize("name,rname,dyn,N", CONFIGS + EDGE + ACCF)
 def test_sqp_step_matches_golden(name, rname, dyn, N):
-    """One SQP iteration per problem: solver outcome exact, step <= 1e-8; the max
+    """One SQP iteration per problem: solver outcome exact, step <= step_tol; the max
     violation at the returned point <= 1e-10 against the oracle's metric at the same
     point (and <= 1e-6 against the golden value, which sits at the oracle's own x)."""
     from oracle.ocp import OracleOCP
@@ -111,8 +121,8 @@ def test_sqp_step_matches_golden(name, rname, dyn, N):
         if np.all(np.isnan(G["dx"][b])):  # infeasible QP: NaN step, x unchanged (ocp.py:478-480)
             assert np.all(np.isnan(dx[b])) and np.array_equal(xn[b], G["X"][b])
         else:
-            assert _rel(dx[b], G["dx"][b]) < 2e-7, b
-        assert _rel(xn[b], G["x_new"][b]) < 2e-7, b
+            assert _rel(dx[b], G["dx"][b]) < step_tol(name), b
+        assert _rel(xn[b], G["x_new"][b]) < step_tol(name), b
         g, l, u = o.eval_g(xn[b], G["P"][b])
         assert st["viol_max"][b] == pytest.approx(o.violation_max(g, l, u), rel=1e-10, abs=1e-14), b
         assert st["viol_max"][b] == pytest.approx(float(G["viol_max"][b]), rel=1e-6, abs=1e-12), b
@@ -406,7 +416,7 @@ def test_make_ocp_centroidal_acc_surface():
     ocp.init_solver()
     x = ocp.solve()
     assert ocp.stats["status"] == int(G["status"][0])
-    assert _rel(x, G["x_new"][0]) <= 2e-7
+    assert _rel(x, G["x_new"][0]) <= step_tol("go2_ca_nb_n20")
     a0 = ocp.a_sol[0]
     assert a0.shape == (R.nv,)
     q0, v0 = ocp.q_sol[0], ocp.v_sol[0]
@@ -433,7 +443,7 @@ def test_make_ocp_centroidal_vel_nb_surface():
     ocp.init_solver()
     x = ocp.solve()
     assert ocp.stats["status"] == int(G["status"][0])
-    assert _rel(x, G["x_new"][0]) <= 2e-7
+    assert _rel(x, G["x_new"][0]) <= step_tol("go2_cv_nb_n20")
     M = rbd.ModelArrays(R.model)
     q0, v0, f0 = ocp.q_sol[0], ocp.v_sol[0], ocp.forces_sol[0]
     h0 = G["XS"][0][:6] + ocp.DX_prev[0][:6]
