@@ -161,9 +161,15 @@ typedef struct {
   double delta_c;      /* 1e-4  dual regularisation (equality rows weighted 1 / delta_c) */
   int max_iter;        /* 10    (ocp.py:256), at most 32 */
   int ls_max;          /* 12    line-search trials */
-  int n_refine;        /* 2     iterative-refinement solves of each Newton system */
-  int pad;
+  int n_refine;        /* 8     iterative-refinement solves of each Newton system (the Lagrangian
+                          Hessian makes the reduced systems stiffer: B2G rnea needs ~6 to
+                          reach the sparse LU's direction to 1e-9 with the block inverses) */
+  int hessian;         /* PL_IP_HESS_EXACT: the Lagrangian Hessian of f + lam^T g (CasADi's
+                          exact Hessian of the Opti/Fatrop solve, ocp.py:248-263) with the
+                          inertia correction; PL_IP_HESS_GN: the objective's diagonal only */
 } pl_ip_settings;
+#define PL_IP_HESS_EXACT 0
+#define PL_IP_HESS_GN 1
 typedef struct {
   int status, iter, ls_trials, nfilter;
   double err, mu, alpha, alpha_z, f, viol_max;
@@ -281,6 +287,7 @@ int pl_ocp_sizes(const pl_ocp* o, long long* out);
 
 /* Test / parity access to internal per-problem arrays and the node table. */
 int pl_debug_get(pl_ocp* o, const char* name, double* out, long long count);
+int pl_debug_set(pl_ocp* o, const char* name, const double* in, long long count);
 int pl_debug_nodes(const pl_ocp* o, int* out);
 int pl_debug_consts(const pl_ocp* o, void* model_out, void* oc_out, int* sizes);
 int pl_debug_admm(pl_ocp* o, int niter, int reset);

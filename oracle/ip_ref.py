@@ -13,9 +13,16 @@ Math. Prog. 106, 2006) -- is restated here, with these documented choices:
 
 * problem: min f(x) s.t. g_E(x) = lbg_E (rows with lbg == ubg) and
   lbg_I <= s = g_I(x) <= ubg_I (slacks on the other rows, bounds on s only);
-* Hessian: the constant objective Hessian diagonal (``ocp.py:293-296``), i.e. the
-  Gauss-Newton Lagrangian Hessian of the OSQP branch, + delta_w I; constraint
-  curvature is not included (Fatrop uses CasADi's exact Lagrangian Hessian);
+* Hessian (``hessian="exact"``, the default): the exact Lagrangian Hessian CasADi gives
+  the Opti/Fatrop solve (``expand=True``): the objective's constant diagonal
+  (``ocp.py:293-296``) + sum_r lam_r d^2 g_r / dx^2 (``OracleOCP.lag_hess``, block
+  diagonal over the w_i since the rows are linear in dx_{i+1}) + delta_w I, with IPOPT's
+  inertia correction (Waechter & Biegler 2006, Algorithm IC; Fatrop corrects the same way
+  when its Riccati recursion meets a block that is not positive definite): the reduced
+  matrix must be positive definite, else a shift delta I is added -- first 1e-4, or a
+  third of the last shift of this solve, then x100 while no shift has succeeded in this
+  solve, x8 after -- at most ``inertia_cap`` times.  ``hessian="gauss_newton"``: the
+  objective's diagonal only (the OSQP branch's Hessian);
 * Newton system: the slacks, bound multipliers and constraint multipliers are
   eliminated, leaving the reduced SPD system
       (H + J^T W J) dx = -(grad + J^T lam) - J^T W r^
@@ -61,7 +68,8 @@ import scipy.sparse.linalg as spla
 
 # ocp.py:254-262 (reference settings) + IPOPT / Fatrop defaults for the rest
 IP_SETTINGS = dict(max_iter=10, tol=1e-3, mu_init=1e-4, bound_push=1e-7, bound_frac=1e-2,
-                   warm_start_mult_bound_push=1e-7, delta_w=1e-8, delta_c=1e-4, ls_max=12, n_refine=2)
+                   warm_start_mult_bound_push=1e-7, delta_w=1e-8, delta_c=1e-4, ls_max=12, n_refine=8,
+                   hessian="exact", inertia_cap=8)
 KAPPA_EPS, KAPPA_MU, THETA_MU = 10.0, 0.2, 1.5
 TAU_MIN, S_MAX, KAPPA_SIGMA = 0.99, 100.0, 1e10
 GAMMA_THETA, GAMMA_PHI, DELTA, S_THETA, S_PHI, ETA_PHI = 1e-5, 1e-8, 1.0, 1.1, 2.3, 1e-8
@@ -91,6 +99,15 @@ def push_slacks(g, lbg, ubg, eq, hl, hu, push, frac):
     s = np.where(hl, np.maximum(s, lb + pl), s)
     s = np.where(hu, np.minimum(s, ub - pu), s)
     return np.where(eq, 0.0, s)
+
+
+def is_pd(K):
+    """Positive definiteness of the reduced Newton matrix (dense Cholesky)."""
+    try:
+        np.linalg.cholesky(K.toarray())
+    except np.linalg.LinAlgError:
+        return False
+    return True
 
 
 def frac_to_boundary(v, dv, tau, mask):
@@ -124,6 +141,8 @@ class IPRef:
         tol = st["tol"]
         dw, dc = st["delta_w"], st["delta_c"]
         H = o.compute_hess_diag(p) + dw
+        exact = st["hessian"] == "exact"
+        dw_last = 0.0  # the last nonzero inertia shift of this solve
         x = np.array(x0, dtype=float, copy=True)
         g, lbg, ubg = o.eval_g(x, p)
         eq, hl, hu = row_classes(lbg, ubg)
@@ -195,12 +214,26 @@ class IPRef:
             bs = np.where(iq, lam + np.where(hl, mu / sl, 0.0) - np.where(hu, mu / su, 0.0), 0.0)
             sig_safe = np.where(iq, sig, 1.0)
             rhat = np.where(eq, c, c - bs / sig_safe)
-            K = (sp.diags(H) + J.T @ sp.diags(W) @ J).tocsc()
+            Kb = sp.diags(H) + J.T @ sp.diags(W) @ J
+            Hl = o.lag_hess(x, p, lam) if exact else sp.csr_matrix((x.size, x.size))
+            Kb = (Kb + Hl).tocsc()
+            dw_before, dwi, tries = dw_last, 0.0, 0
+            while exact:  # inertia correction (module docstring)
+                if is_pd(Kb + dwi * sp.eye(x.size)):
+                    if dwi > 0.0:
+                        dw_last = dwi
+                    break
+                if tries >= st["inertia_cap"]:
+                    break
+                dwi = ((1e-4 if dw_last == 0.0 else max(1e-20, dw_last / 3.0)) if dwi == 0.0
+                       else dwi * (100.0 if dw_last == 0.0 else 8.0))
+                tries += 1
+            K = (Kb + dwi * sp.eye(x.size)).tocsc()
             rhs = -rx - J.T @ (W * rhat)
             lu = spla.splu(K)
             dx = lu.solve(rhs)
             for _ in range(st["n_refine"]):  # iterative refinement on the KKT x-row residual
-                res = -(grad + J.T @ (lam + W * (J @ dx + rhat))) - H * dx
+                res = -(grad + J.T @ (lam + W * (J @ dx + rhat))) - (H + dwi) * dx - Hl @ dx
                 dx = dx + lu.solve(res)
             dl = W * (J @ dx + rhat)
             ds = np.where(iq, (bs + dl) / sig_safe, 0.0)
@@ -213,7 +246,8 @@ class IPRef:
             amax = min(frac_to_boundary(sl, ds, tau, hl), frac_to_boundary(su, -ds, tau, hu))
             az = min(frac_to_boundary(zl, dzl, tau, hl), frac_to_boundary(zu, dzu, tau, hu))
             self.trace.append(dict(x=x.copy(), s=s.copy(), lam=lam.copy(), zl=zl.copy(), zu=zu.copy(), mu=mu, W=W,
-                                   rhat=rhat, rx=rx, rhs=rhs, dx=dx, dl=dl, ds=ds, jdx=J @ dx, amax=amax, az=az))
+                                   rhat=rhat, rx=rx, rhs=rhs, dx=dx, dl=dl, ds=ds, jdx=J @ dx, amax=amax, az=az,
+                                   dw_last=dw_before, dwi=dwi, tries=tries))
             theta = float(np.sum(np.abs(c)))
             phi = self._phi(f, sl, su, hl, hu, mu)
             dphi = float(grad @ dx + np.sum(np.where(hl, -mu / sl, 0.0) * ds + np.where(hu, mu / su, 0.0) * ds))

@@ -389,6 +389,57 @@ class OracleOCP:
             r0 += Jn.shape[0]
         return sp.csc_matrix((vals, (rows, cols)), shape=(r0, self.n))
 
+    def lag_hess(self, x, p, lam, delta=1e-3):
+        """Lagrangian Hessian sum_r lam_r d^2 g_r / dx^2 (csr, n x n) -- the constraint part of
+        the exact Hessian CasADi gives the reference's Opti/Fatrop solve (ocp.py:248-263).
+        The rows of node i are linear in dx_{i+1} (the integration rows), so it is block
+        diagonal over the w_i = [dx_i, u_i].  Entry (j, k) of block i: the complex-step
+        derivative of lam_i^T g_i along w_j, differentiated along w_k by the fourth-order
+        central difference [-f(+2d) + 8 f(+d) - 8 f(-d) + f(-2d)] / (12 d) (an independent
+        technique from the GPU's hyper-dual numbers; ~1e-12 relative).  The rnea tau_j
+        columns enter linearly and are skipped."""
+        P = self.unpack(p)
+        DX, U = self.split(x)
+        h = 1e-30
+        ndx = self.ndx
+        rows, cols, vals = [], [], []
+        r0 = ndx
+        for i in range(self.N):
+            nu = self.nu[i]
+            nw = ndx + nu
+            nr = self.node_row_count(i, P)
+            li = lam[r0:r0 + nr]
+            r0 += nr
+            lin = nw
+            if self.dynamics == "whole_body_rnea":
+                lin = ndx + self.na + self.nf
+            jj, kk = np.tril_indices(lin)  # j <= k pairs (kk >= jj after the swap below)
+            jj, kk = kk, jj
+            jj, kk = np.minimum(jj, kk), np.maximum(jj, kk)
+            base = np.concatenate([DX[i], U[i], DX[i + 1]])
+            npair = jj.size
+            steps = np.array([2.0, 1.0, -1.0, -2.0]) * delta
+            wts = np.array([-1.0, 8.0, -8.0, 1.0]) / (12.0 * delta)
+            pert = np.broadcast_to(base, (4, npair, base.size)).astype(complex).copy()
+            ar = np.arange(npair)
+            for s in range(4):
+                pert[s, ar, jj] += 1j * h
+                pert[s, ar, kk] += steps[s]
+            pert = pert.reshape(4 * npair, base.size)
+            out = self.node_rows(i, pert[:, :ndx], pert[:, ndx:nw], pert[:, nw:], P)
+            G = np.concatenate([np.broadcast_to(g, (4 * npair, g.shape[-1])) for g, _, _ in out], -1)
+            dphi = (G.imag @ li / h).reshape(4, npair)
+            Hjk = wts @ dphi
+            off = self.x_off[i]
+            rows.extend((off + kk).tolist())
+            cols.extend((off + jj).tolist())
+            vals.extend(Hjk.tolist())
+            low = jj != kk
+            rows.extend((off + jj[low]).tolist())
+            cols.extend((off + kk[low]).tolist())
+            vals.extend(Hjk[low].tolist())
+        return sp.csr_matrix((vals, (rows, cols)), shape=(self.n, self.n))
+
     def structural_pattern(self, p):
         """Jacobian pattern from randomised inputs (contacts toggled) -- superset of
         every numeric pattern the solve can produce.  Used as the OSQP A pattern."""

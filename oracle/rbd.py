@@ -46,11 +46,11 @@ def mtv(R, x):
 
 
 def mm(A, B):
-    return np.einsum("...ij,...jk->...ik", A, B)
+    return np.matmul(A, B)
 
 
 def mtm(A, B):
-    return np.einsum("...ji,...jk->...ik", A, B)
+    return np.matmul(np.swapaxes(A, -1, -2), B)
 
 
 # ---------------------------------------------------------------- spatial algebra

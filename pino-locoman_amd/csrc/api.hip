@@ -848,10 +848,11 @@ int build_factor_prog(pl_ocp* o) {
     f.fs_off = fs;
     fs += (long long)X * X + (long long)U * X + (long long)U * U;
     fs = (fs + 31) & ~31LL;
-    // k_fnode LDS: packed lower Kt (even) | max(A values x 2, G) | pivot buffer [2][128][4]
+    // k_fnode LDS: packed lower Kt (even) | A values x 2 (assembly), then the pivot buffer
+    // [2][512] (sweep), then G (after the sweep): the three share one region
     const int nK = (nslot + 1) & ~1;
-    const int r2 = (std::max(2 * (nd.nent + 1), U * X) + 1) & ~1;
-    lds_of[i] = (nK + r2 + 1024) * 8;
+    const int r2 = (std::max(std::max(2 * (nd.nent + 1), U * X), 1024) + 1) & ~1;
+    lds_of[i] = (nK + r2) * 8;
     um_of[i] = U <= 40 ? 40 : 64;
   }
   h.fs_stride = std::max(fs, 32LL);
@@ -870,13 +871,15 @@ int build_factor_prog(pl_ocp* o) {
   }
   for (int g = 0; g < h.nfgroup; ++g)
     if (h.fg_lds[g] > 160 * 1024) { pl_set_error("factor kernel: node needs %d bytes of LDS", h.fg_lds[g]); return -1; }
-  // k_fchain LDS: packed lower S (even) | Y / transpose buffer | E | pivot buffer |
-  // staged coupling values (ncw + 2 X) | timing stamps
+  // k_fchain LDS: packed lower S (even) | Y / transpose buffer, the pivot buffer during the
+  // sweep | E (packed lower) | staged coupling values (ncw + 2 X) | timing stamps (84 KB for
+  // B2G rnea, one chain per CU: the chain is latency-bound, 81 k cycles per node)
   const int nS = (h.nw_max * (h.nw_max + 1) / 2 + 1) & ~1;
-  const int ny = (std::max(npc_max * X, X * (X + 1)) + 1) & ~1;
+  const int ny = (std::max(std::max(npc_max * X, X * (X + 1)), 1024) + 1) & ~1;
+  const int nE = (X * (X + 1) / 2 + 1) & ~1;
   h.fchain_ny = ny;
   h.fchain_ncw = (ncw_max + 1) & ~1;
-  h.fchain_lds = (nS + ny + X * X + 1024 + h.fchain_ncw + 2 * X + 10) * 8;  // + timing stamps
+  h.fchain_lds = (nS + ny + nE + h.fchain_ncw + 2 * X + 10) * 8;  // + timing stamps
   if (h.fchain_lds > 160 * 1024) { pl_set_error("factor kernel: chain needs %d bytes of LDS", h.fchain_lds); return -1; }
   if (o->kasm.empty()) o->kasm.assign(NT, 0);
   if (o->kcpl.empty()) o->kcpl.assign(4, 0);
@@ -1071,7 +1074,8 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   h.solver = PL_SOLVER_OSQP;
   // Fatrop settings of the reference (ocp.py:254-262) + the restatement's constants
   // (oracle/ip_ref.py IP_SETTINGS)
-  h.ip = PlIpSettings{1e-3, 1e-4, 1e-7, 1e-2, 1e-8, 1e-4, 10, 12, 2, 0, 1e-7};
+  h.ip = PlIpSettings{1e-3, 1e-4, 1e-7, 1e-2, 1e-8, 1e-4, 10, 12, 8, 0, 1e-7};
+  h.ip_hess = PL_IP_HESS_EXACT;  // the Lagrangian Hessian (pl_ip_settings.hessian)
   // ADMM kernel (admm_select below): PL_ADMM_KERNEL = sweep | sweep2 | chain | auto overrides
   // the batch-size rule at creation, pl_ocp_set_admm_kernel afterwards.
   h.admm_waves = 1;
@@ -1404,7 +1408,32 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
         dalloc(o, &h->d.ip_zl, Bm) ||
         dalloc(o, &h->d.ip_zu, Bm) || dalloc(o, &h->d.ip_rh, Bm) || dalloc(o, &h->d.ip_dl, Bm) ||
         dalloc(o, &h->d.ip_ds, Bm) || dalloc(o, &h->d.ip_jdx, Bm) || dalloc(o, &h->d.ip_dx, (size_t)h->B * h->n) ||
-        dalloc(o, &h->d.ipinfo, (size_t)h->B))
+        dalloc(o, &h->d.ipinfo, (size_t)h->B) || dalloc(o, &h->d.ip_dwi, (size_t)2 * h->B) ||
+        dalloc(o, &h->d.ip_iflag, (size_t)4 * h->B))
+      return -2;
+    // Lagrangian Hessian work list (k_hess.hip): column pairs j <= k of every w_i block,
+    // without the rnea tau_j columns (the rows are linear in them); node blocks packed lower
+    std::vector<int2> hl;
+    std::vector<int> hoff;
+    long long off = 0;
+    const PlOcpConst& O = h->oc;
+    for (int i = 0; i <= h->N; ++i) {
+      const int nw = o->nodes[i].nw;
+      hoff.push_back((int)off);
+      off += (long long)nw * (nw + 1) / 2;
+      if (i == h->N) break;  // no rows on the last node
+      for (int k = 0; k < nw; ++k) {
+        const bool tk = O.dyn == PL_DYN_RNEA && k >= O.ndx + O.na + O.nf;
+        for (int j = 0; j <= k && !tk; ++j) {
+          if (O.dyn == PL_DYN_RNEA && j >= O.ndx + O.na + O.nf) continue;
+          hl.push_back(make_int2(i, j | (k << 16)));
+        }
+      }
+    }
+    h->hl_len = (int)hl.size();
+    h->hl_stride = (off + 1) & ~1LL;
+    if (upload(o, &h->d.hlist, hl) || upload(o, &h->d.hoff, hoff) ||
+        dalloc(o, &h->d.Hlag, (size_t)h->B * h->hl_stride))
       return -2;
   }
   h->solver = solver;
@@ -1422,8 +1451,13 @@ extern "C" int pl_ocp_set_ip_settings(pl_ocp* o, const pl_ip_settings* s) {
     pl_set_error("invalid interior-point settings");
     return -1;
   }
+  if (s->hessian != PL_IP_HESS_EXACT && s->hessian != PL_IP_HESS_GN) {
+    pl_set_error("ip hessian %d unknown (PL_IP_HESS_EXACT = 0, PL_IP_HESS_GN = 1)", s->hessian);
+    return -1;
+  }
   o->h.ip = PlIpSettings{s->tol, s->mu_init, s->bound_push, s->bound_frac, s->delta_w, s->delta_c, s->max_iter,
                          s->ls_max, s->n_refine, 0, 1e-7};
+  o->h.ip_hess = s->hessian;
   return 0;
 }
 
@@ -1687,11 +1721,12 @@ extern "C" int pl_ocp_sizes(const pl_ocp* o, long long* out) {
 }
 
 // Debug / parity access to internal per-problem arrays (tests only).
-extern "C" int pl_debug_get(pl_ocp* o, const char* name, double* out, long long count) {
-  REQUIRE_DEVICE(o);
+static int debug_rw(pl_ocp* o, const char* name, double* out, const double* in, long long count) {
   PlOcpHandle* h = &o->h;
   const size_t B = h->B;
   struct Item { const char* n; double* p; size_t len; } items[] = {
+      {"Hlag", h->d.Hlag, h->d.Hlag ? B * (size_t)h->hl_stride : 0},
+      {"ip_dwi", h->d.ip_dwi, h->d.ip_dwi ? 2 * B : 0},
       {"As", h->d.As, B * h->nnz}, {"Araw", h->d.Araw, B * h->nnz}, {"qs", h->d.qs, B * h->n},
       {"ls", h->d.ls, B * h->m},   {"us", h->d.us, B * h->m},       {"rho", h->d.rho, B * h->m},
       {"D", h->d.D, B * h->n},     {"E", h->d.E, B * h->m},         {"cs", h->d.cs, B},
@@ -1708,13 +1743,28 @@ extern "C" int pl_debug_get(pl_ocp* o, const char* name, double* out, long long 
   for (auto& it : items) {
     if (strcmp(it.n, name) == 0) {
       if ((size_t)count < it.len) { pl_set_error("buffer too small for %s (%zu)", name, it.len); return -1; }
-      PL_CHECK_HIP(hipMemcpyAsync(out, it.p, it.len * 8, hipMemcpyDeviceToHost, h->stream));
+      if (out) PL_CHECK_HIP(hipMemcpyAsync(out, it.p, it.len * 8, hipMemcpyDeviceToHost, h->stream));
+      else PL_CHECK_HIP(hipMemcpyAsync(it.p, in, it.len * 8, hipMemcpyHostToDevice, h->stream));
       PL_CHECK_HIP(hipStreamSynchronize(h->stream));
       return (int)0;
     }
   }
   pl_set_error("unknown array %s", name);
   return -1;
+}
+
+extern "C" int pl_debug_get(pl_ocp* o, const char* name, double* out, long long count) {
+  REQUIRE_DEVICE(o);
+  if (!out) { pl_set_error("null argument"); return -1; }
+  return debug_rw(o, name, out, nullptr, count);
+}
+
+// Overwrite an internal array (tests: e.g. "ip_dwi", the inertia state of a teacher-forced
+// interior-point direction).
+extern "C" int pl_debug_set(pl_ocp* o, const char* name, const double* in, long long count) {
+  REQUIRE_DEVICE(o);
+  if (!in) { pl_set_error("null argument"); return -1; }
+  return debug_rw(o, name, nullptr, in, count);
 }
 
 // Node table (tests): per node [nw, nu, x_off, row_off, nrow, ncol, ent_off, nent, ntile, nunit, s_off, ncpl]

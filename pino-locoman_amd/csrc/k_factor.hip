@@ -85,9 +85,11 @@ __device__ __forceinline__ f64x4 mfma4(double a, double b, f64x4 c) {
 // and lane l + R, so row (r + k) needs no modulo.  pb: 2 x [2 R_pub][4] doubles.
 // kSync: 0 = one wave (wave-scope fence), 1 = workgroup barrier (publisher and
 // readers are different waves; every wave of the group must call).
-template <int R, int kSync, int kBatch>
+// kTrack: pmin <- min(pmin, every pivot) (the positive-definiteness test of the
+// interior-point inertia correction; pivots are wave-uniform)
+template <int R, int kSync, int kBatch, bool kTrack = false>
 __device__ __forceinline__ void sweep_rot(double (&col)[R], double* pb, int pbstride, int l, int nblocks,
-                                          bool publish, bool active, bool pivcols) {
+                                          bool publish, bool active, bool pivcols, double* pmin = nullptr) {
 #pragma unroll 1
   for (int B = 0; B < nblocks; ++B) {
     const int k = 4 * B;
@@ -114,6 +116,7 @@ __device__ __forceinline__ void sweep_rot(double (&col)[R], double* pb, int pbst
       // m <- -M_PP^-1 (4-pivot sweep, wave-uniform values)
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
+        if constexpr (kTrack) *pmin = fmin(*pmin, m[p][p]) + (m[p][p] == m[p][p] ? 0.0 : -1.0);  // NaN: fails
         const double pinv = rcp_nr(m[p][p]);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -174,24 +177,28 @@ typedef const __attribute__((address_space(4))) double* CF64;
 
 // ---------------------------------------------------------------------------------
 // Stage 1: per (problem, node).  X = ndx, UM >= nu (register columns of the sweep).
-template <int X, int UM>
+// HL: the interior point's exact-Hessian system -- Kt_ii += H_i (d.Hlag), pivots <= 0
+// reported in d.ip_iflag, and (fac_only) only the problems flagged for a refactor
+template <int X, int UM, bool HL>
 __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, int i0, int ni, long long fs_stride,
-                                              double sigma) {
+                                              double sigma, long long hl_stride, int fac_only) {
   const int task = blockIdx.x;
   const int b = task / ni;
   const int i = i0 + (task - b * ni);
+  if constexpr (HL) {
+    if (fac_only && !d.ip_iflag[4 * b + 1]) return;
+  }
   const int tid = threadIdx.x, l = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
   CFac fn = (CFac)d.fnodes + i;
   const int nw = fn->nw, U = fn->nu, nent = fn->nent;
   const int nK = (nw * (nw + 1) / 2 + 1) & ~1;
-  const int r2 = (max(2 * (nent + 1), U * X) + 1) & ~1;
   extern __shared__ double lds[];
   double* K = lds;         // packed lower Kt_ii
-  double* Ar = K + nK;     // rho-scaled A values (nent + 1, the last one zero)
+  double* Ar = K + nK;     // rho-scaled A values (nent + 1, the last one zero), during the assembly
   double* Av = Ar + nent + 1;
+  double* pb = K + nK;     // pivot block rows [2][512] during the sweep
   double* Gs = K + nK;     // after the sweep: G (U x X), row-major
-  double* pb = K + nK + r2;
 
   const double* __restrict__ As = d.As + (size_t)b * nnz + fn->ent_off;
   const double* __restrict__ rho = d.rho + (size_t)b * m + fn->row_off;
@@ -225,6 +232,11 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
     const double* __restrict__ Ps = d.Ps + (size_t)b * n + fn->x_off;
     for (int c = tid; c < nw; c += NT) K[lidx(c, c)] += Ps[c] + sigma;
   }
+  if constexpr (HL) {
+    __syncthreads();
+    const double* __restrict__ Hb = d.Hlag + (size_t)b * hl_stride + d.hoff[i];
+    for (int k = tid; k < nw * (nw + 1) / 2; k += NT) K[k] += Hb[k];
+  }
   __syncthreads();
   double* FS = d.FS + (size_t)b * fs_stride + fn->fs_off;
   double* Ag = FS;
@@ -250,7 +262,11 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
     }
     // pivots k >= U meet an identity pad (wave 0) and zero rows (wave 1): no-ops;
     // the rotation is back to the identity once all UM / 4 blocks are swept
-    sweep_rot<UM, 1, 8>(col, pb, 8 * 64, l, UM / 4, w == 0, w < 2, w == 0);
+    double pmin = 1.0;
+    sweep_rot<UM, 1, 8, HL>(col, pb, 8 * 64, l, UM / 4, w == 0, w < 2, w == 0, &pmin);
+    if constexpr (HL) {
+      if (w == 0 && l == 0 && !(pmin > 0.0)) d.ip_iflag[4 * b] = 1;
+    }
     if (w == 0 && l < U) {
 #pragma unroll
       for (int r = 0; r < UM; ++r)
@@ -304,11 +320,12 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
 //
 // Store S_i in the ADMM lane-tile layout (state.h): 4x4 tile t = K l + k of lane l,
 // pair j at s_off + ((k * 8 + j) * 64 + l) * 2 (coalesced over o).  Threads [t0, t0 + nt).
-__device__ __forceinline__ void store_tiles(const PlDev& d, CFac fn, const double* Sl, double* Sg, int t0, int nt) {
+__device__ __forceinline__ void store_tiles(const PlDev& d, CFac fn, const double* Sl, double* Sg, int t0, int nt,
+                                            int tid) {
   double* Sn = Sg + fn->s_off;
   const int nunit = fn->nunit, ntl = fn->ntl, nw = fn->nw;
   const int total = nunit * 64 * 16;
-  for (int o = (int)threadIdx.x - t0; o < total; o += nt) {
+  for (int o = tid - t0; o < total; o += nt) {
     const int slot = o & 1, ln = (o >> 1) & 63, j = (o >> 7) & 7, k = o >> 10;
     const int t = nunit * ln + k;
     double val = 0.0;
@@ -324,19 +341,23 @@ __device__ __forceinline__ void store_tiles(const PlDev& d, CFac fn, const doubl
   }
 }
 
-template <int X>
+template <int X, bool HL>
 __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, int S_stride, long long fs_stride,
-                                               int nwm, int ny, int ncw) {
+                                               int nwm, int ny, int ncw, int fac_only) {
   const int b = blockIdx.x;
+  if constexpr (HL) {
+    if (fac_only && !d.ip_iflag[4 * b + 1]) return;
+  }
   const int tid = threadIdx.x, l = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
   extern __shared__ double lds[];
   const int nS = (nwm * (nwm + 1) / 2 + 1) & ~1;
+  constexpr int nE = (X * (X + 1) / 2 + 1) & ~1;
   double* Sl = lds;       // packed lower S_i
   double* Yb = Sl + nS;   // transpose buffer [X][X + 1], then Y [npc][X]
-  double* Eb = Yb + ny;   // E_i [X][X]
-  double* pb = Eb + X * X;  // pivot block rows [2][128][4]
-  double* Acw = pb + 1024;  // A values of the coupling rows' w parts (ncw)
+  double* pb = Yb;        // pivot block rows [2][128][4] during the sweep (Yb is free then; ny >= 1024)
+  double* Eb = Yb + ny;   // E_i, packed lower
+  double* Acw = Eb + nE;  // A values of the coupling rows' w parts (ncw)
   double* cv = Acw + ncw;   // rho_a A_{e_a} (X)
   double* ev = cv + X;      // A_{e_a} (X)
   // optional phase timing (thread 0, s_memtime): 8 accumulators + last stamp in LDS
@@ -352,7 +373,7 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
       }
     }
   };
-  for (int k = tid; k < X * X; k += NT) Eb[k] = 0.0;
+  for (int k = tid; k < nE; k += NT) Eb[k] = 0.0;
   double* Sg = d.S + (size_t)b * S_stride;
   const double* __restrict__ FSb = d.FS + (size_t)b * fs_stride;
   for (int i = 0; i <= N; ++i) {
@@ -384,12 +405,16 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
         // lanes >= XS duplicate column XS - 1: never pivots, never published, never stored
         const int lc = min(l, XS - 1);
         const int rc = min(r, X - 1), cc = min(lc, X - 1);
-        const double v = Ag[rc * X + cc] + Eb[rc >= cc ? rc * X + cc : cc * X + rc];
+        const double v = Ag[rc * X + cc] + Eb[sidx(rc, cc)];
         col[r] = (r < X && lc < X) ? v : (r == lc ? 1.0 : 0.0);
       }
       unsigned long long ts0 = 0;
       if (TIMING) ts0 = __builtin_amdgcn_s_memtime();
-      sweep_rot<XS, 0, XS>(col, pb, 8 * 64, l, XS / 4, true, true, true);
+      double pmin = 1.0;
+      sweep_rot<XS, 0, XS, HL>(col, pb, 8 * 64, l, XS / 4, true, true, true, &pmin);
+      if constexpr (HL) {
+        if (l == 0 && !(pmin > 0.0)) d.ip_iflag[4 * b] = 1;
+      }
       if (TIMING) {
         const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
         if (l == 0) tacc[5] += ts1 - ts0;
@@ -407,7 +432,7 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
       // ---- waves 1-3, while wave 0 sweeps: store S_{i-1}, stage node i's coupling values
       unsigned long long ts0 = 0;
       if (TIMING) ts0 = __builtin_amdgcn_s_memtime();
-      if (i > 0) store_tiles(d, (CFac)d.fnodes + (i - 1), Sl, Sg, 64, NT - 64);
+      if (i > 0) store_tiles(d, (CFac)d.fnodes + (i - 1), Sl, Sg, 64, NT - 64, tid);
       if (i < N) {
         const int ncwi = (int)cwptr[X];
         for (int q = tid - 64; q < ncwi; q += NT - 64) Acw[q] = Asb[cwl[q] & 0xffff];
@@ -516,17 +541,18 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
     T(3);
     if (l < X) {
       const double cb = cv[l];
-      for (int a = w; a < X; a += 4) {
+      for (int a = w; a < X; a += 4) {  // lower triangle (l <= a) only: E is symmetric
+        if (l > a) continue;
         const double ca = cv[a];
         double acc = 0.0;
         for (int q = (int)cwptr[a]; q < (int)cwptr[a + 1]; ++q)
           acc = fma(Acw[q], Yb[(cwl[q] >> 24) * X + l], acc);
-        Eb[a * X + l] = (a == l ? ca * ev[a] : 0.0) - ca * cb * acc;
+        Eb[lidx(a, l)] = (a == l ? ca * ev[a] : 0.0) - ca * cb * acc;
       }
     }
     T(4);
   }
-  store_tiles(d, (CFac)d.fnodes + N, Sl, Sg, 0, NT);
+  store_tiles(d, (CFac)d.fnodes + N, Sl, Sg, 0, NT, tid);
   T(6);
   if (TIMING) {
     if (tid == 0)
@@ -536,35 +562,41 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
 
 namespace {
 
-template <int X, int UM>
+template <int X, int UM, bool HL>
 void launch_fnode(PlOcpHandle* h, int g) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)k_fnode<X, UM>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_fnode<X, UM, HL>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((k_fnode<X, UM>), dim3(h->B * h->fg_n[g]), dim3(NT), h->fg_lds[g], h->stream, h->d, h->n, h->m,
-                     h->nnz, h->fg_i0[g], h->fg_n[g], h->fs_stride, h->set.sigma);
+  hipLaunchKernelGGL((k_fnode<X, UM, HL>), dim3(h->B * h->fg_n[g]), dim3(NT), h->fg_lds[g], h->stream, h->d, h->n,
+                     h->m, h->nnz, h->fg_i0[g], h->fg_n[g], h->fs_stride, h->set.sigma, h->hl_stride, h->fac_only);
 }
 
-template <int X>
+template <int X, bool HL>
 void launch_fchain(PlOcpHandle* h) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)k_fchain<X>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_fchain<X, HL>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((k_fchain<X>), dim3(h->B), dim3(NT), h->fchain_lds, h->stream, h->d, h->N, h->m, h->nnz,
-                     h->S_stride, h->fs_stride, h->nw_max, h->fchain_ny, h->fchain_ncw);
+  hipLaunchKernelGGL((k_fchain<X, HL>), dim3(h->B), dim3(NT), h->fchain_lds, h->stream, h->d, h->N, h->m, h->nnz,
+                     h->S_stride, h->fs_stride, h->nw_max, h->fchain_ny, h->fchain_ncw, h->fac_only);
+}
+
+template <int X, bool HL>
+void launch_factor_xh(PlOcpHandle* h) {
+  for (int g = 0; g < h->nfgroup; ++g) {
+    if (h->fg_um[g] <= 40) launch_fnode<X, 40, HL>(h, g);
+    else launch_fnode<X, 64, HL>(h, g);
+  }
+  launch_fchain<X, HL>(h);
 }
 
 template <int X>
 void launch_factor_x(PlOcpHandle* h) {
-  for (int g = 0; g < h->nfgroup; ++g) {
-    if (h->fg_um[g] <= 40) launch_fnode<X, 40>(h, g);
-    else launch_fnode<X, 64>(h, g);
-  }
-  launch_fchain<X>(h);
+  if (h->fac_hlag) launch_factor_xh<X, true>(h);
+  else launch_factor_xh<X, false>(h);
 }
 
 }  // namespace
@@ -574,8 +606,11 @@ void launch_factor_x(PlOcpHandle* h) {
 // pad); the handle refuses others.
 bool factor_supports_ndx(int ndx) { return ndx == 24 || ndx == 30 || ndx == 36 || ndx == 48; }
 
-void launch_factor(PlOcpHandle* h) {
+void launch_factor_pre(PlOcpHandle* h) {
   launch_acpl(h);  // the sweep's compact coupling A values (k_admm.hip) for this As
+}
+
+void launch_factor_core(PlOcpHandle* h) {
   switch (h->ndx) {
     case 24: launch_factor_x<24>(h); break;
     case 30: launch_factor_x<30>(h); break;
@@ -583,5 +618,14 @@ void launch_factor(PlOcpHandle* h) {
     case 48: launch_factor_x<48>(h); break;
     default: break;
   }
+}
+
+void launch_factor_post(PlOcpHandle* h) {
   if (h->admm_rc) launch_fred(h);  // chain blocks of the reduced-chain ADMM (k_admm_rc.hip)
+}
+
+void launch_factor(PlOcpHandle* h) {
+  launch_factor_pre(h);
+  launch_factor_core(h);
+  launch_factor_post(h);
 }

@@ -103,6 +103,7 @@ __device__ __forceinline__ double next_mu(double mu, double tol) {
 __global__ __launch_bounds__(256) void k_ip_init(PlDev d, int m, PlIpSettings st, int warm) {
   const int b = blockIdx.x;
   __shared__ double red[256];
+  if (threadIdx.x == 0 && d.ip_dwi) d.ip_dwi[2 * b + 1] = 0.0;  // no inertia shift used yet in this solve
   const double* g = d.g + (size_t)b * m;
   const double* lbg = d.lbg + (size_t)b * m;
   const double* ubg = d.ubg + (size_t)b * m;
@@ -342,6 +343,10 @@ __global__ __launch_bounds__(256) void k_ip_kkt(PlDev d, int N, int n, int m, in
     d.ip_dx[(size_t)b * n + j] = 0.0;
   }
   for (int r = threadIdx.x; r < m; r += 256) d.ip_jdx[(size_t)b * m + r] = 0.0;
+  if (threadIdx.x == 0 && d.ip_dwi) {  // inertia correction of this Newton system starts at 0
+    d.ip_dwi[2 * b] = 0.0;
+    for (int q = 0; q < 4; ++q) d.ip_iflag[4 * b + q] = 0;
+  }
   __syncthreads();
   // rho of the coupling rows, contiguous for the ADMM prefetch (as k_qp_finish)
   for (int i = 0; i <= N; ++i) {
@@ -359,7 +364,8 @@ __global__ __launch_bounds__(256) void k_ip_kkt(PlDev d, int N, int n, int m, in
 // W_E = 1 / delta_c = 1e4 one block-inverse solve agrees with the oracle's sparse LU to
 // ~1e-12 and the refinement keeps the step at that level as the multipliers grow
 // (at W_E = 1e6 the explicit inverses lose ~5 digits and the refinement diverges).
-__global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int n, int m, int nnz, double delta_w) {
+__global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int n, int m, int nnz, double delta_w, int hlag,
+                                                   long long hl_stride) {
   const int b = blockIdx.x;
   if (!d.ipinfo[b].active) return;
   const double* A = d.Araw + (size_t)b * nnz;
@@ -367,7 +373,7 @@ __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int n, int m, int nn
   const double* rh = d.ip_rh + (size_t)b * m;
   const double* lam = d.ip_lam + (size_t)b * m;
   const double* grad = d.grad + (size_t)b * n;
-  const double* P = d.P + (size_t)b * n;
+  const double* Ps = d.Ps + (size_t)b * n;  // P + the inertia shift (k_ip_kkt, k_ip_inertia)
   double* xa = d.xa + (size_t)b * n;
   double* za = d.za + (size_t)b * m;
   double* ya = d.ya + (size_t)b * m;
@@ -383,17 +389,77 @@ __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int n, int m, int nn
     ya[r] = 0.0;
   }
   __syncthreads();
+  for (int j = threadIdx.x; j < n; j += 256) dx[j] += xa[j];
+  __syncthreads();
+  const double* Hb = hlag ? d.Hlag + (size_t)b * hl_stride : nullptr;
   for (int j = threadIdx.x; j < n; j += 256) {
-    const double dj = dx[j] + xa[j];
-    dx[j] = dj;
-    double acc = grad[j] + (P[j] + delta_w) * dj;
+    const double dj = dx[j];
+    double acc = grad[j] + (Ps[j] + delta_w) * dj;
+    if (Hb) {  // + H_i dx_{w_i}, node i's packed-lower block (k_lag_hess)
+      const int i = d.colnode[j];
+      const PlNode nd = d.nodes[i];
+      const int lc = j - nd.x_off;
+      const double* Hi = Hb + d.hoff[i];
+      for (int c = 0; c < nd.nw; ++c) {
+        const int r0 = max(lc, c), c0 = min(lc, c);
+        acc = fma(Hi[r0 * (r0 + 1) / 2 + c0], dx[nd.x_off + c], acc);
+      }
+    }
     for (int q = d.gc_ptr[j]; q < d.gc_ptr[j + 1]; ++q) {
       const int2 er = d.gc_er[q];
       acc += A[er.x] * t[er.y];
     }
     qs[j] = acc;  // rhs = -qs = r
-    xa[j] = 0.0;
   }
+  __syncthreads();
+  for (int j = threadIdx.x; j < n; j += 256) xa[j] = 0.0;
+}
+
+// Inertia correction of the Newton system (IPOPT Algorithm IC, Waechter & Biegler 2006,
+// sec. 3.1; Fatrop corrects the same way when its Riccati recursion meets a block that is
+// not positive definite).  The reduced matrix H_L + Ps + delta_w I + J^T W J is positive
+// definite iff every pivot of the factor's block elimination is (k_fnode / k_fchain report
+// a pivot <= 0 in ip_iflag[0]).  Per round: a clean factor resolves the system (and
+// records a nonzero shift as the last one); otherwise the shift grows -- first
+// 1e-4, or a third of the last one, then x100 while no shift has succeeded in this solve,
+// x8 after -- and the problem is refactored (ip_iflag[1]).  After `cap` shifts the system
+// is taken as it is.  oracle/ip_ref.py restates the same rule.
+__global__ __launch_bounds__(256) void k_ip_inertia(PlDev d, int n, int cap) {
+  const int b = blockIdx.x;
+  if (!d.ipinfo[b].active) return;
+  int* F = d.ip_iflag + 4 * b;
+  double* dw = d.ip_dwi + 2 * b;
+  __shared__ double s_new;
+  __shared__ int s_act;
+  if (threadIdx.x == 0) {
+    s_act = 0;
+    if (F[2]) {
+      F[1] = 0;
+    } else if (!F[0]) {
+      F[2] = 1;
+      F[1] = 0;
+      if (dw[0] > 0.0) dw[1] = dw[0];
+    } else if (F[3] >= cap) {
+      F[0] = 0;
+      F[1] = 0;
+      F[2] = 1;
+    } else {
+      F[0] = 0;
+      const double nd = dw[0] == 0.0 ? (dw[1] == 0.0 ? 1e-4 : fmax(1e-20, dw[1] / 3.0))
+                                     : dw[0] * (dw[1] == 0.0 ? 100.0 : 8.0);
+      dw[0] = nd;
+      F[1] = 1;
+      F[3] += 1;
+      s_new = nd;
+      s_act = 1;
+    }
+  }
+  __syncthreads();
+  if (!s_act) return;
+  const double* P = d.P + (size_t)b * n;
+  double* Ps = d.Ps + (size_t)b * n;
+  const double sh = s_new;
+  for (int j = threadIdx.x; j < n; j += 256) Ps[j] = P[j] + sh;
 }
 
 // ---------------------------------------------------------------------------------
@@ -630,6 +696,35 @@ __global__ void k_ip_finish(PlDev d, int B) {
     default: hipLaunchKernelGGL(KERNEL<PL_DYN_ABA>, __VA_ARGS__); break;           \
   }
 
+#define PL_IP_INERTIA_CAP 8  // shifts per Newton system (1e-4 x 100^7 = 1e10 from a clean start)
+
+// Factor the Newton system, with the inertia correction when the Lagrangian Hessian is in
+// it (the Gauss-Newton system is positive definite by construction).
+static void ip_factor(PlOcpHandle* h) {
+  const bool exact = h->ip_hess == PL_IP_HESS_EXACT;
+  h->fac_hlag = exact ? 1 : 0;
+  if (!exact) {
+    launch_factor(h);
+    return;
+  }
+  launch_factor_pre(h);
+  launch_factor_core(h);
+  for (int r = 0; r <= PL_IP_INERTIA_CAP; ++r) {
+    hipLaunchKernelGGL(k_ip_inertia, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, PL_IP_INERTIA_CAP);
+    if (r == PL_IP_INERTIA_CAP) break;
+    h->fac_only = 1;
+    launch_factor_core(h);
+    h->fac_only = 0;
+  }
+  launch_factor_post(h);
+  h->fac_hlag = 0;
+}
+
+static void ip_refine(PlOcpHandle* h, const PlIpSettings& st) {
+  hipLaunchKernelGGL(k_ip_refine, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, h->m, h->nnz, st.delta_w,
+                     h->ip_hess == PL_IP_HESS_EXACT ? 1 : 0, h->hl_stride);
+}
+
 // One interior-point solve of every problem from d.x (the warm start), enqueued on the
 // handle's stream.  Kernels of terminated problems return at once.
 void enqueue_ip(PlOcpHandle* h) {
@@ -646,11 +741,12 @@ void enqueue_ip(PlOcpHandle* h) {
     hipLaunchKernelGGL(k_ip_kkt, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz,
                        std::max(h->ncpl_max, 1), k, st);
     if (k == st.max_iter) break;
-    launch_factor(h);
+    if (h->ip_hess == PL_IP_HESS_EXACT) launch_lag_hess(h);
+    ip_factor(h);
     launch_admm_init(h);
     launch_admm(h, 1, 0, 0);
     for (int r = 0; r < st.n_refine; ++r) {
-      hipLaunchKernelGGL(k_ip_refine, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, h->m, h->nnz, st.delta_w);
+      ip_refine(h, st);
       launch_admm_init(h);
       launch_admm(h, 1, 0, 0);
     }
@@ -674,11 +770,12 @@ void enqueue_ip_direction(PlOcpHandle* h) {
   launch_eval_jac(h);
   hipLaunchKernelGGL(k_ip_kkt, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz,
                      std::max(h->ncpl_max, 1), -1, st);
-  launch_factor(h);
+  if (h->ip_hess == PL_IP_HESS_EXACT) launch_lag_hess(h);
+  ip_factor(h);
   launch_admm_init(h);
   launch_admm(h, 1, 0, 0);
   for (int r = 0; r < st.n_refine; ++r) {
-    hipLaunchKernelGGL(k_ip_refine, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, h->m, h->nnz, st.delta_w);
+    ip_refine(h, st);
     launch_admm_init(h);
     launch_admm(h, 1, 0, 0);
   }

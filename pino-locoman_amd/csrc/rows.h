@@ -73,11 +73,27 @@ template <> struct VecIn<Dual> {
   int seed;
   PL_HD Dual operator[](int k) const { return Dual(x[k], k == seed ? 1.0 : 0.0); }
 };
+// two seeds: the e1 / e2 parts of column seed / seed2 (the Lagrangian Hessian, k_lag_hess)
+template <> struct VecIn<HDual> {
+  const double* x;
+  const double* step;
+  double alpha;
+  int seed, seed2;
+  PL_HD HDual operator[](int k) const { return HDual(x[k], k == seed ? 1.0 : 0.0, k == seed2 ? 1.0 : 0.0, 0.0); }
+};
 template <class S> PL_HD VecIn<S> sub_in(const VecIn<S>& a, int off) {
   VecIn<S> r = a;
   r.x = a.x + off;
   if (a.step) r.step = a.step + off;
   r.seed = a.seed - off;
+  if constexpr (std::is_same<S, HDual>::value) r.seed2 = a.seed2 - off;
+  return r;
+}
+// a seed of the input in [lo, hi) (for HDual: either seed -- a pass whose outputs do not
+// depend on one seed's column has zero mixed second derivatives)
+template <class S> PL_HD bool seeded(const VecIn<S>& a, int lo, int hi) {
+  bool r = a.seed >= lo && a.seed < hi;
+  if constexpr (std::is_same<S, HDual>::value) r = r || (a.seed2 >= lo && a.seed2 < hi);
   return r;
 }
 
@@ -141,7 +157,7 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
   S vnb[CVNB ? PL_MAXV : 1], hdot_nb[CVNB ? 6 : 1];
   if constexpr (CVNB) {
     bool run = true;
-    if constexpr (!std::is_same<S, double>::value) run = !(dxn.seed >= 0 && dxn.seed < O.ndx);
+    if constexpr (!std::is_same<S, double>::value) run = !seeded(dxn, 0, O.ndx);
     if (run) {
       S hj[6], ci[9], hcur[6], R0[9];
       centroidal_pass<S>(M, O, qb, qrev, ZeroBaseAcc<S>{u}, sub_in(u, nj), true, true, hj, hdot_nb, ci,
@@ -195,11 +211,11 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
   // centroidal pass reads the forces but not h.
   bool tree = true, cen = CV;
   if constexpr (!std::is_same<S, double>::value) {
-    const bool seed_dxn = dxn.seed >= 0 && dxn.seed < O.ndx;
-    const bool seed_tau = DYN == PL_DYN_RNEA && u.seed >= O.na + O.nf && u.seed < O.na + O.nf + nj;
+    const bool seed_dxn = seeded(dxn, 0, O.ndx);
+    const bool seed_tau = DYN == PL_DYN_RNEA && seeded(u, O.na + O.nf, O.na + O.nf + nj);
     // (without the base, h enters the kinematics through v_b; its centroidal pass ran above)
-    const bool seed_h = DYN == PL_DYN_CV && dx.seed >= 0 && dx.seed < 6;
-    const bool seed_f = CV && u.seed >= f_off && u.seed < f_off + O.nf;
+    const bool seed_h = DYN == PL_DYN_CV && seeded(dx, 0, 6);
+    const bool seed_f = CV && seeded(u, f_off, f_off + O.nf);
     tree = !(seed_dxn || seed_tau || seed_h || seed_f);
     cen = DYN == PL_DYN_CV && !(seed_dxn || seed_h);
   }

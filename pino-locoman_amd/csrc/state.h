@@ -63,6 +63,10 @@ struct PlNode {
 #define PL_CHUNK 6
 // ADMM sweep kernel limits (one wave per problem, k_admm.hip)
 #ifndef PL_ADMM_ATOMIC
+#ifndef PL_IP_HESS_EXACT  // include/pinoloco.h (pl_ip_settings.hessian)
+#define PL_IP_HESS_EXACT 0
+#define PL_IP_HESS_GN 1
+#endif
 #define PL_ADMM_ATOMIC 1  // k_admm mat-vec: accumulate y with LDS f64 atomics (0: segment sums)
 #endif
 #define PL_ADMM_KM 4        // factor tile slots per lane held in registers (more: extra passes)
@@ -216,6 +220,12 @@ struct PlDev {
   double* ip_s;      // slacks of the inequality rows
   double* ip_lam;    // constraint multipliers (lam_g)
   double* ip_lam0;   // lam_g warm start (opti.set_initial(opti.lam_g, lam_g), ocp_whole_body_rnea.py:234-235)
+  // exact Lagrangian Hessian (k_hess.hip) and its inertia correction (k_ip.hip)
+  int2* hlist;       // (node, j | k << 16) column pairs of the w_i blocks
+  int* hoff;         // packed-lower offset of node i's block
+  double* Hlag;      // [B][hl_stride] sum_r lam_r d^2 g_r / dw_i^2, packed lower per node
+  double* ip_dwi;    // [B][2]: the inertia shift of this Newton system, the last nonzero one
+  int* ip_iflag;     // [B][4]: not-SPD seen by the factor, refactor, resolved, tries
   double* ip_zl;     // lower / upper bound multipliers of the slacks
   double* ip_zu;
   double* ip_rh;     // r^ of the reduced Newton system
@@ -250,6 +260,11 @@ struct PlOcpHandle {
   int jl_len;                       // k_eval_jac work-list entries (a multiple of 64 before the cheap part)
   int solver;                       // PL_SOLVER_OSQP (SQP + OSQP ADMM) or PL_SOLVER_IP (interior point)
   int ip_lam_warm;                  // 1: the next interior-point solve starts from lam = ip_lam0
+  int ip_hess;                      // interior point: PL_IP_HESS_EXACT (Lagrangian) or PL_IP_HESS_GN
+  int hl_len;                       // Lagrangian Hessian work list (k_lag_hess)
+  long long hl_stride;              // doubles per problem of d.Hlag
+  int fac_hlag;                     // 1: k_fnode adds d.Hlag to Kt_ii and both factor kernels report pivots <= 0
+  int fac_only;                     // 1: the factor kernels skip problems whose d.ip_iflag refactor flag is clear
   PlIpSettings ip;
   long long fs_stride;              // factor scratch per problem (doubles)
   int nfgroup;                      // k_fnode launches: consecutive nodes with one program
@@ -281,6 +296,9 @@ void launch_objective(PlOcpHandle* h);
 void launch_hess(PlOcpHandle* h);
 void launch_qp_setup(PlOcpHandle* h);
 void launch_factor(PlOcpHandle* h);
+void launch_factor_pre(PlOcpHandle* h);   // launch_factor = pre + core + post
+void launch_factor_core(PlOcpHandle* h);
+void launch_factor_post(PlOcpHandle* h);
 bool factor_supports_ndx(int ndx);
 void launch_admm_init(PlOcpHandle* h);
 void launch_admm(PlOcpHandle* h, int niter, int check, int it_base);
@@ -288,6 +306,7 @@ bool admm2_supported(const PlOcpHandle* h);
 void launch_admm2(PlOcpHandle* h, int niter, int check);
 bool admm_rc_supported(const PlOcpHandle* h);
 void launch_admm_rc(PlOcpHandle* h, int niter, int check);
+void launch_lag_hess(PlOcpHandle* h);
 void launch_fred(PlOcpHandle* h);
 void launch_acpl(PlOcpHandle* h);
 long long rc_ch_stride(int N, int ndx);

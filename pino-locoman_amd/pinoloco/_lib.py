@@ -46,7 +46,7 @@ class Stats(C.Structure):
 class IpSettings(C.Structure):
     _fields_ = [("tol", C.c_double), ("mu_init", C.c_double), ("bound_push", C.c_double), ("bound_frac", C.c_double),
                 ("delta_w", C.c_double), ("delta_c", C.c_double), ("max_iter", C.c_int), ("ls_max", C.c_int),
-                ("n_refine", C.c_int), ("pad", C.c_int)]
+                ("n_refine", C.c_int), ("hessian", C.c_int)]
 
 
 class IpStats(C.Structure):
@@ -97,6 +97,7 @@ EXPORTS = {
     "pl_ocp_sizes": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong)]),
     "pl_debug_consts": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, _ip]),
     "pl_debug_get": (C.c_int, [C.c_void_p, C.c_char_p, _dp, C.c_longlong]),
+    "pl_debug_set": (C.c_int, [C.c_void_p, C.c_char_p, _dp, C.c_longlong]),
     "pl_debug_nodes": (C.c_int, [C.c_void_p, _ip]),
     "pl_debug_admm": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "pl_dyn_create": (C.c_int, [C.c_void_p, _ip, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),

@@ -31,8 +31,10 @@ OSQP_SETTINGS = dict(max_iter=100, alpha=1.4, rho=2e-2, warm_start=True, adaptiv
 
 # ocp.py:254-262 (the reference's Fatrop options) plus the restatement's constants
 # (oracle/ip_ref.py IP_SETTINGS: bound_frac, regularisation, line-search trials)
+# hessian: 0 = the exact Lagrangian Hessian (CasADi / Fatrop), 1 = the objective's diagonal
 FATROP_SETTINGS = dict(max_iter=10, tol=1e-3, mu_init=1e-4, bound_push=1e-7, bound_frac=1e-2, delta_w=1e-8,
-                       delta_c=1e-4, ls_max=12, n_refine=2, pad=0)
+                       delta_c=1e-4, ls_max=12, n_refine=8, hessian=0)
+IP_HESSIAN = {"exact": 0, "gauss_newton": 1}
 
 # ocp_args.py:2-19
 OCP_ARGS = {
@@ -280,6 +282,8 @@ class BatchedOCP:
         """Interior-point settings (defaults: FATROP_SETTINGS, the reference's ocp.py:254-262)."""
         s = dict(FATROP_SETTINGS)
         s.update(kw)
+        if isinstance(s["hessian"], str):
+            s["hessian"] = IP_HESSIAN[s["hessian"]]
         st = _lib.IpSettings(**{k: s[k] for k, _ in _lib.IpSettings._fields_})
         _lib.check(_lib.lib().pl_ocp_set_ip_settings(self.h, C.byref(st)))
 
@@ -340,6 +344,35 @@ class BatchedOCP:
     def debug(self, name, length):
         out = np.zeros(length)
         _lib.check(_lib.lib().pl_debug_get(self.h, name.encode(), _lib.dptr(out), length))
+        return out
+
+    def debug_set(self, name, values):
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.float64).ravel())
+        _lib.check(_lib.lib().pl_debug_set(self.h, name.encode(), _lib.dptr(v), v.size))
+
+    def lag_hess(self):
+        """The interior point's Lagrangian Hessian blocks of the last Newton system (tests):
+        [batch] list of csr n x n matrices (k_lag_hess, packed lower per node)."""
+        import scipy.sparse as sp
+        nodes = self.node_table()
+        B = self.batch
+        offs, o = [], 0
+        for nd in nodes:
+            offs.append(o)
+            o += nd[0] * (nd[0] + 1) // 2
+        stride = (o + 1) & ~1
+        raw = self.debug("Hlag", B * stride).reshape(B, stride)
+        out = []
+        for b in range(B):
+            rows, cols, vals = [], [], []
+            for i, nd in enumerate(nodes):
+                nw, xo = nd[0], nd[2]
+                kk, jj = np.tril_indices(nw)
+                v = raw[b, offs[i] + kk * (kk + 1) // 2 + jj]
+                rows += (xo + kk).tolist() + (xo + jj[kk != jj]).tolist()
+                cols += (xo + jj).tolist() + (xo + kk[kk != jj]).tolist()
+                vals += v.tolist() + v[kk != jj].tolist()
+            out.append(sp.csr_matrix((vals, (rows, cols)), shape=(self.n, self.n)))
         return out
 
     # ---------------------------------------------------------------- MPC

@@ -282,6 +282,13 @@ def sqp_fixture(name, rname, dyn, N, problems, loop_steps, gait, osqp, njac, kw=
           flush=True)
 
 
+# (fixture, problem) whose per-iteration oracle states and Newton directions are stored for
+# the GPU's teacher-forced directions (tests/test_ip.py); problems of ip_go2_rnea_n20 also
+# get a lam_g warm-started solve from their own solution
+IP_TF = {("ip_go2_cv_n20", 0), ("ip_go2_cv_n20", 1), ("ip_go2_rnea_n20", 0), ("ip_go2_acc_nb_n20", 1)}
+IP_WARM = {"ip_go2_rnea_n20": 2}
+
+
 def ip_fixture(name, rname, dyn, N, problems, loop_steps, gait, kw=None):
     from oracle.ip_ref import IP_SETTINGS, IPRef
     kw = kw or {}
@@ -299,7 +306,20 @@ def ip_fixture(name, rname, dyn, N, problems, loop_steps, gait, kw=None):
                            "viol_max")}
     for b in range(B):
         o = OracleOCP(R, dyn, N, **kw)
-        x, lam, st = IPRef(o).solve(X[b], P[b])
+        ip = IPRef(o)
+        x, lam, st = ip.solve(X[b], P[b])
+        if (name, b) in IP_TF:
+            for key in ("x", "s", "lam", "zl", "zu", "dx", "dl", "ds"):
+                rec[f"tf{b}_{key}"] = np.array([t[key] for t in ip.trace])
+            for key in ("mu", "amax", "az", "dw_last", "dwi"):
+                rec[f"tf{b}_{key}"] = np.array([float(t[key]) for t in ip.trace])
+        if b == 0:  # the Lagrangian Hessian at the solution (GPU k_lag_hess vs OracleOCP.lag_hess)
+            Hl = o.lag_hess(x, P[b], lam).tocsr()
+            rec["hess_data"], rec["hess_indices"], rec["hess_indptr"] = Hl.data, Hl.indices, Hl.indptr
+        if b < IP_WARM.get(name, 0):
+            xw, lw, sw = IPRef(o).solve(x, P[b], lam0=lam)
+            for key, v in (("warm_x", xw), ("warm_lam", lw), ("warm_status", sw["status"]), ("warm_iter", sw["iter"])):
+                rec.setdefault(key, []).append(v)
         g, lbg, ubg = o.eval_g(x, P[b])
         al = np.zeros(mi)
         al[:len(st["alphas"])] = st["alphas"]
@@ -309,6 +329,9 @@ def ip_fixture(name, rname, dyn, N, problems, loop_steps, gait, kw=None):
                      ("viol_max", o.violation_max(g, lbg, ubg))):
             per[k].append(v)
     rec.update({k: np.array(v) for k, v in per.items()})
+    for key in ("warm_x", "warm_lam", "warm_status", "warm_iter"):
+        if key in rec:
+            rec[key] = np.array(rec[key])
     # closed loop of problem 0 (run_mpc.py:115-143 with the Fatrop solver): warm start,
     # one interior-point solve, x <- integrate(x, DX[1])
     if loop_steps > 1:
