@@ -98,6 +98,25 @@ def _cpu_model():
     return "unknown"
 
 
+def _cgroup_cpu_quota():
+    """CPUs granted by the cgroup CPU controller (v2 ``cpu.max`` or v1 cfs quota / period),
+    or None when no quota is set: evidence for ``cores`` beside OMP_NUM_THREADS."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else int(quota) / int(period)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            quota = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            period = int(f.read())
+        return None if quota <= 0 else quota / period
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(robot, dynamics, N, per_core=4, n_steps=2):
     """The compiled C++ restatement of the reference's CPU path (oracle/cpu/sqp_cpu.cpp:
     rows + dual Jacobians, OSQP 0.6 with the QDLDL LDL^T on the quasi-definite KKT,
@@ -124,7 +143,8 @@ def cpu_baseline(robot, dynamics, N, per_core=4, n_steps=2):
             "sample": f"{B} problems x {n_steps} MPC steps of the same workload (seeds 0..{B - 1}) on {threads} OpenMP "
                       f"threads; compiled C++ restatement of the reference CPU path (oracle/cpu/sqp_cpu.cpp: OSQP 0.6 "
                       f"+ QDLDL LDL^T, Armijo/filter line search), g++ -O3 -march=x86-64-v3",
-            "single_core_ms_per_solve": w1 / n_steps * 1e3, "cpu_model": _cpu_model(), "host_cpus_visible": avail}
+            "single_core_ms_per_solve": w1 / n_steps * 1e3, "cpu_model": _cpu_model(), "host_cpus_visible": avail,
+            "omp_num_threads_env": env, "cgroup_cpu_quota": _cgroup_cpu_quota()}
 
 
 def _free_port():

@@ -19,12 +19,12 @@
 // the workgroup, and waves of terminated or padding problems keep hitting the same
 // barriers without doing work.
 //
-// Measured (B2G whole_body_rnea N=50, B=1024, same box, r02c): 26.75 ms per launch vs
-// 24.99 ms for k_admm, parity suite green.  The per-step time of k_admm is issue plus
-// latency of a few dependent chains (≈1600 VALU instructions per step and wave, SQ
-// counters); splitting the work across two waves leaves the chain depth of the
-// gathers / reductions unchanged, adds 7-9 barriers per step, and the two waves of a
-// SIMD compete for the same VALU issue.  Kept as an opt-in (PL_ADMM_WAVES=2) for A/B.
+// Selection (api.hip::admm_select, AUTO): the reduced-chain kernel k_admm_rc up to
+// B = 256 problems where it supports the OCP, this kernel for B <= 512, k_admm above.
+// Measured: at B = 1024 this kernel is slower than k_admm (26.3 vs 25.2 ms per launch,
+// r02e; the two waves of a SIMD compete for the same VALU issue and the 7-9 barriers per
+// step add latency), at B = 512 it is faster (15.2 vs 18.5 ms: k_admm leaves half the
+// SIMDs idle there).  PL_ADMM_KERNEL=sweep2 / pl_ocp_set_admm_kernel force it.
 #include <algorithm>
 #include <type_traits>
 
