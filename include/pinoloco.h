@@ -80,7 +80,7 @@ typedef struct {
   int dynamics;                /* PL_DYN_* */
   int nodes;                   /* N */
   int tau_nodes;               /* OCP_ARGS["whole_body_rnea"]["tau_nodes"] (ocp_args.py:16) */
-  int include_acc;             /* must be 1 (ocp_args.py:17) */
+  int include_acc;             /* rnea: 1 = a in u (ocp_args.py:17), 0 = a = (v_{i+1} - v_i) / dt (ocp_whole_body_rnea.py:183-191; OSQP branch only) */
   int include_base;            /* acc / centroidal_acc / centroidal_vel: 1 = base in u (ocp_args.py:5-11);
                                   0 = base acceleration / velocity from the dynamics
                                   (ocp_whole_body_acc.py:124-135, ocp_centroidal_vel.py:119-129) */

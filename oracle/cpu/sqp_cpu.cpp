@@ -186,7 +186,7 @@ double objective(const Problem& pr, const double* p, const double* x, const doub
       const double e = xj - pl::u_des(pr.M, O, p, k);
       f += e * (R[k] * e);
       gj = 2.0 * R[k] * e;
-      if (O.dyn == PL_DYN_RNEA && i == 0 && k >= O.na + O.nf) {
+      if (PL_IS_RNEA(O.dyn) && i == 0 && k >= O.na + O.nf) {
         const int t = k - O.na - O.nf;
         const double W = p[O.P.W_diag + t], et = xj - p[O.P.tau_prev + t];
         f += et * (W * et);
@@ -577,7 +577,7 @@ void hess_diag(const Problem& pr, const double* p, double* Pd) {
     } else {
       const int k = lc - O.ndx;
       h = 2.0 * p[O.P.R_diag + k];
-      if (O.dyn == PL_DYN_RNEA && i == 0 && k >= O.na + O.nf) h += 2.0 * p[O.P.W_diag + k - O.na - O.nf];
+      if (PL_IS_RNEA(O.dyn) && i == 0 && k >= O.na + O.nf) h += 2.0 * p[O.P.W_diag + k - O.na - O.nf];
     }
     Pd[j] = h;
   }
@@ -762,6 +762,7 @@ extern "C" double cpu_mpc_batch(void* h, int B, const double* P, const double* X
         case PL_DYN_CA: run_problem<PL_DYN_CA>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
         case PL_DYN_ACCNB: run_problem<PL_DYN_ACCNB>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
         case PL_DYN_CVNB: run_problem<PL_DYN_CVNB>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
+        case PL_DYN_RNEAFD: run_problem<PL_DYN_RNEAFD>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
         default: run_problem<PL_DYN_CV>(pr, w, Pb, Xb, XSb, T0[b], steps, xs_out + (size_t)b * nx, sb); break;
       }
     }
@@ -789,6 +790,7 @@ extern "C" int cpu_sqp_step(void* h, const double* p, double* x, double* dx, int
     case PL_DYN_CA: s = sqp_step<PL_DYN_CA>(pr, w, st, p, Pd.data(), x); break;
     case PL_DYN_ACCNB: s = sqp_step<PL_DYN_ACCNB>(pr, w, st, p, Pd.data(), x); break;
     case PL_DYN_CVNB: s = sqp_step<PL_DYN_CVNB>(pr, w, st, p, Pd.data(), x); break;
+    case PL_DYN_RNEAFD: s = sqp_step<PL_DYN_RNEAFD>(pr, w, st, p, Pd.data(), x); break;
     default: s = sqp_step<PL_DYN_CV>(pr, w, st, p, Pd.data(), x); break;
   }
   for (int j = 0; j < pr.n; ++j) dx[j] = w.step[j];

@@ -77,13 +77,13 @@ class CpuOCP:
     """One (robot, dynamics, N) OCP on the CPU baseline; structure from the product's
     host-only handle (layout and Jacobian pattern, pl_ocp_pattern / pl_debug_consts)."""
 
-    def __init__(self, robot, dynamics, nodes, osqp_settings=None, gait_type="trot", gait_period=0.8):
+    def __init__(self, robot, dynamics, nodes, osqp_settings=None, gait_type="trot", gait_period=0.8, **kw):
         from pinoloco import _lib as plib
         from pinoloco.ocp import GAIT_CODES, OSQP_SETTINGS, BatchedOCP
         s = dict(OSQP_SETTINGS)
         s.update(osqp_settings or {})
         bo = BatchedOCP(robot, dynamics, nodes, batch=1, device=-1, osqp_settings=s, gait_type=gait_type,
-                        gait_period=gait_period)
+                        gait_period=gait_period, **kw)  # kw: include_base / include_acc
         sizes = (C.c_int * 2)()
         plib.check(plib.lib().pl_debug_consts(bo.h, None, None, sizes))
         mb, ob = C.create_string_buffer(sizes[0]), C.create_string_buffer(sizes[1])

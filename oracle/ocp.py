@@ -253,11 +253,15 @@ class OracleOCP:
         else:
             q, v = self.state(dx, P)
         if dyn == "whole_body_rnea":
-            a = u[..., :nv]
             forces = u[..., self.na:self.na + nf]
             tau_j = u[..., self.na + nf:]
             add(dx_next[..., :nv] - (dx[..., :nv] + v * dt), 0, 0)
-            add(dx_next[..., nv:] - (dx[..., nv:] + a * dt), 0, 0)
+            if self.include_acc:
+                a = u[..., :nv]
+                add(dx_next[..., nv:] - (dx[..., nv:] + a * dt), 0, 0)
+            else:  # get_a: finite difference, no dv row (ocp_whole_body_rnea.py:157-159, 183-191)
+                _, v_next = self.state(dx_next, P)
+                a = (v_next - v) / dt
             tau = rbd.rnea_dynamics(self.M, self.ee_frames, q, v, a, forces)
             add(tau[..., :6], 0, 0)
             if i < self.tau_nodes:

@@ -154,7 +154,7 @@ void build_blocks(PlOcpConst& O, bool has_ext, bool has_arm) {
   for (int type = 0; type < 3; ++type) {
     O.nblk[type] = 0;
     const bool first = (type == 0);
-    const bool tau = (O.dyn == PL_DYN_RNEA) && (type == 1 || (type == 0 && O.tau_nodes > 0));
+    const bool tau = PL_IS_RNEA(O.dyn) && (type == 1 || (type == 0 && O.tau_nodes > 0));
     const bool cv = PL_IS_CV(O.dyn);
     // centroidal_vel keeps the state rows at node 0 (ocp.py:137-140, 170-173)
     const bool state = !first || cv;
@@ -165,9 +165,10 @@ void build_blocks(PlOcpConst& O, bool has_ext, bool has_arm) {
       if (O.dyn == PL_DYN_CV) add_block(O, type, PL_RB_CV_GAP, 6);  // include_base only
     } else {
       add_block(O, type, PL_RB_DYNQ, O.nv);
-      add_block(O, type, PL_RB_DYNV, O.nv);
+      // include_acc = False: "a inherently uses this finite difference" (ocp_whole_body_rnea.py:157-159)
+      if (O.dyn != PL_DYN_RNEAFD) add_block(O, type, PL_RB_DYNV, O.nv);
     }
-    if (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC) add_block(O, type, PL_RB_RNEA_BASE, 6);
+    if (PL_IS_RNEA(O.dyn) || O.dyn == PL_DYN_ACC) add_block(O, type, PL_RB_RNEA_BASE, 6);
     if (O.dyn == PL_DYN_CA) add_block(O, type, PL_RB_CA_GAP, 6);
     if (tau) {
       add_block(O, type, PL_RB_TAU_EQ, O.nj);
@@ -225,13 +226,15 @@ std::vector<std::vector<int>> node_row_deps(const PlModel& M, const PlOcpConst& 
   };
   auto DXN = [&](int k) { return nw + k; };
   const bool accf = O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA || O.dyn == PL_DYN_ACCNB;
-  const int f_off = (O.dyn == PL_DYN_RNEA || accf) ? O.na : (O.dyn == PL_DYN_CV ? nv : nj);
+  const int f_off = (PL_IS_RNEA(O.dyn) || accf) ? O.na : (O.dyn == PL_DYN_CV ? nv : nj);
   auto F = [&](int k) { return U(f_off + k); };
   std::vector<int> dynset;  // dependency set of the RNEA / ABA / base-solve outputs
   for (int k = 3; k < nv; ++k) dynset.push_back(DQ(k));
   for (int k = 0; k < nv; ++k) dynset.push_back(DV(k));
   if (O.dyn == PL_DYN_ABA || O.dyn == PL_DYN_ACCNB) {
     for (int k = 0; k < nj; ++k) dynset.push_back(U(k));
+  } else if (O.dyn == PL_DYN_RNEAFD) {  // a = (v_{i+1} - v_i) / dt
+    for (int k = 0; k < nv; ++k) dynset.push_back(DXN(nv + k));
   } else {
     for (int k = 0; k < nv; ++k) dynset.push_back(U(k));
   }
@@ -724,7 +727,21 @@ int build_factor_prog(pl_ocp* o) {
   };
   long long fs = 0;
   std::vector<int> lds_of(N + 1), um_of(N + 1);
-  int npc_max = 1, ncw_max = 2;
+  int npc_max = 1, ncw_max = 2, nc_max = 1, nxc_max = 2;
+  // General coupling (h.fac_gc) when some node's rows touch a dx_{i+1} column more than once
+  // or one row touches several (whole_body_rnea include_acc = False: the RNEA rows read
+  // a = (v_{i+1} - v_i) / dt); otherwise every dx_{i+1} column has exactly one coupling row.
+  h.fac_gc = 0;
+  for (int i = 0; i < N; ++i) {
+    const PlNode& nd = o->nodes[i];
+    const int* cp = o->colptr.data() + nd.colptr_off;
+    const int* rid = o->rowidx.data() + nd.ent_off;
+    std::vector<int> seen(nd.nrow, 0);
+    for (int a = 0; a < X; ++a) {
+      const int c = nd.nw + a;
+      if (cp[c + 1] - cp[c] != 1 || seen[rid[cp[c]]]++) h.fac_gc = 1;
+    }
+  }
   for (int i = 0; i <= N; ++i) {
     const PlNode& nd = o->nodes[i];
     PlFacNode& f = o->fnodes[i];
@@ -798,7 +815,55 @@ int build_factor_prog(pl_ocp* o) {
     }
     // ---- coupling program (i < N)
     std::vector<uint32_t> C;
-    if (i < N) {
+    if (i < N && h.fac_gc) {
+      // general form: coupling rows s (rows with a dx_{i+1} entry), Z = R - R Vc S Vc^T R over
+      // them and E_{i+1} = Wc^T Z Wc.  Words: crow[nc] | cwptr[nc + 1] | pcl[npc] |
+      // cw (e | col << 16 | pc << 24)[ncw] | xcptr[X + 1] | xc (e | s << 16)[nxc]
+      const int* cpl = o->cplrow.data() + nd.cpl_off;
+      const int nc = nd.ncpl;
+      std::vector<int> sidx_of(nd.nrow, -1);
+      for (int q = 0; q < nc; ++q) sidx_of[cpl[q]] = q;
+      std::vector<int> used(nw, 0);
+      std::vector<std::vector<std::pair<int, int>>> cw(nc);
+      for (int q = 0; q < nc; ++q)
+        for (int t = rp[cpl[q]]; t < rp[cpl[q] + 1]; ++t) {
+          const int e = re[t], c = ecol[e];
+          if (c < nw) { cw[q].push_back({e, c}); used[c] = 1; }
+        }
+      std::vector<int> pcl, pcof(nw, -1);
+      for (int c = 0; c < nw; ++c)
+        if (used[c]) { pcof[c] = (int)pcl.size(); pcl.push_back(c); }
+      if (nw > 255 || pcl.size() > 255 || nc > 64) { pl_set_error("factor kernel: node too wide"); return -1; }
+      for (int q = 0; q < nc; ++q) C.push_back((uint32_t)cpl[q]);
+      uint32_t acc = 0;
+      for (int q = 0; q <= nc; ++q) {
+        C.push_back(acc);
+        if (q < nc) acc += (uint32_t)cw[q].size();
+      }
+      for (int c : pcl) C.push_back((uint32_t)c);
+      for (int q = 0; q < nc; ++q)
+        for (auto& pr : cw[q])
+          C.push_back((uint32_t)pr.first | ((uint32_t)pr.second << 16) | ((uint32_t)pcof[pr.second] << 24));
+      uint32_t nx = 0;
+      std::vector<uint32_t> xl;
+      for (int a = 0; a <= X; ++a) {
+        C.push_back(nx);
+        if (a == X) break;
+        for (int e = cp[nw + a]; e < cp[nw + a + 1]; ++e) {
+          if (sidx_of[rid[e]] < 0) { pl_set_error("factor kernel: dx_{i+1} entry outside a coupling row"); return -1; }
+          xl.push_back((uint32_t)e | ((uint32_t)sidx_of[rid[e]] << 16));
+          ++nx;
+        }
+      }
+      C.insert(C.end(), xl.begin(), xl.end());
+      f.npc = (int)pcl.size();
+      f.nc = nc;
+      npc_max = std::max(npc_max, f.npc);
+      ncw_max = std::max(ncw_max, (int)acc);
+      nc_max = std::max(nc_max, nc);
+      nxc_max = std::max(nxc_max, (int)nx);
+      f.cp_off = intern32(cpls, cpl_offs, o->kcpl, C);
+    } else if (i < N) {
       std::vector<int> crow(X), cent(X);
       std::vector<int> owner(nd.nrow, -1);
       for (int a = 0; a < X; ++a) {
@@ -874,12 +939,19 @@ int build_factor_prog(pl_ocp* o) {
   // k_fchain LDS: packed lower S (even) | Y / transpose buffer, the pivot buffer during the
   // sweep | E (packed lower) | staged coupling values (ncw + 2 X) | timing stamps (84 KB for
   // B2G rnea, one chain per CU: the chain is latency-bound, 81 k cycles per node)
+  // (general coupling: Y [npc][nc], then T = Z Wc [nc][X] in the Y buffer, and behind the
+  // stamps Z [nc][nc], the staged dx_{i+1} values [nxc] and rho of the coupling rows [nc])
   const int nS = (h.nw_max * (h.nw_max + 1) / 2 + 1) & ~1;
-  const int ny = (std::max(std::max(npc_max * X, X * (X + 1)), 1024) + 1) & ~1;
+  int ny = std::max(std::max(npc_max * X, X * (X + 1)), 1024);
+  if (h.fac_gc) ny = std::max(ny, std::max(npc_max, X) * nc_max);
+  ny = (ny + 1) & ~1;
   const int nE = (X * (X + 1) / 2 + 1) & ~1;
   h.fchain_ny = ny;
   h.fchain_ncw = (ncw_max + 1) & ~1;
-  h.fchain_lds = (nS + ny + nE + h.fchain_ncw + 2 * X + 10) * 8;  // + timing stamps
+  h.fchain_nc = h.fac_gc ? nc_max : 0;
+  h.fchain_nxc = h.fac_gc ? (nxc_max + 1) & ~1 : 0;
+  const int ngc = h.fac_gc ? ((nc_max * nc_max + h.fchain_nxc + nc_max + 1) & ~1) : 0;
+  h.fchain_lds = (nS + ny + nE + h.fchain_ncw + 2 * X + 10 + ngc) * 8;  // + timing stamps
   if (h.fchain_lds > 160 * 1024) { pl_set_error("factor kernel: chain needs %d bytes of LDS", h.fchain_lds); return -1; }
   if (o->kasm.empty()) o->kasm.assign(NT, 0);
   if (o->kcpl.empty()) o->kcpl.assign(4, 0);
@@ -916,12 +988,12 @@ int build_jac_list(pl_ocp* o, std::vector<int2>& list) {
       if (cp[lc] == cp[lc + 1]) continue;
       bool cheap;
       if (lc >= nd.nw) {
-        cheap = true;
+        cheap = !(O.dyn == PL_DYN_RNEAFD && lc - nd.nw >= O.nv);  // FD: dv_{i+1} enters the RNEA
       } else if (lc < O.ndx) {
         cheap = O.dyn == PL_DYN_CV && lc < 6;  // (without the base, h enters v_b: not cheap)
       } else {
         const int k = lc - O.ndx;
-        cheap = O.dyn == PL_DYN_RNEA && k >= O.na + O.nf;
+        cheap = PL_IS_RNEA(O.dyn) && k >= O.na + O.nf;
       }
       (cheap ? ch : ex).push_back(make_int2(i, lc));
     }
@@ -977,13 +1049,6 @@ int admm_select(pl_ocp* o, int kind) {
 extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int batch, int device, pl_ocp** out) {
   if (!model || !d || !out || batch <= 0) { pl_set_error("bad arguments"); return -1; }
   if (d->dynamics < 0 || d->dynamics > 4) { pl_set_error("Unknown dynamics type: %d", d->dynamics); return -1; }
-  if (d->dynamics == PL_DYN_WHOLE_BODY_RNEA && !d->include_acc) {
-    // a = (v_{i+1} - v_i) / dt (ocp_whole_body_rnea.py:183-191) couples the RNEA rows of
-    // node i to dv_{i+1}: not the stage-wise structure the block factor needs
-    pl_set_error("whole_body_rnea requires include_acc=True on this path (finite-difference accelerations "
-                 "couple the RNEA rows to the next node; the reference notes the same for Fatrop)");
-    return -1;
-  }
   if (d->nodes < 2 || d->n_feet != 4) { pl_set_error("need nodes >= 2 and 4 feet"); return -1; }
   pl_ocp* o = new pl_ocp();
   PlOcpHandle& h = o->h;
@@ -997,6 +1062,10 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   if ((O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA) && !d->include_base) O.dyn = PL_DYN_ACCNB;
   // centroidal_vel without the base velocity in u (the class default, ocp_centroidal_vel.py:9-23)
   if (O.dyn == PL_DYN_CV && !d->include_base) O.dyn = PL_DYN_CVNB;
+  // whole_body_rnea with finite-difference accelerations (include_acc = False,
+  // ocp_whole_body_rnea.py:21-26, 183-191): u = [f | tau_j], no dv_{i+1} rows; the RNEA rows
+  // of node i read dv_{i+1}, so the factor takes the general coupling program (fac_gc)
+  if (O.dyn == PL_DYN_RNEA && !d->include_acc) O.dyn = PL_DYN_RNEAFD;
   O.N = d->nodes;
   O.nq = M.nq;
   O.nv = M.nv;
@@ -1011,7 +1080,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   O.ndx = cv ? 6 + M.nv : 2 * M.nv;
   O.na = (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA) ? M.nv
          : (O.dyn == PL_DYN_ACCNB ? M.nq - 7 : 0);
-  O.tau_nodes = (O.dyn == PL_DYN_RNEA) ? d->tau_nodes : 0;
+  O.tau_nodes = PL_IS_RNEA(O.dyn) ? d->tau_nodes : 0;
   O.mu = d->mu;
   for (int k = 0; k < 4; ++k) O.feet[k] = frame_ref(model, d->foot_frames[k]);
   O.ext = frame_ref(model, d->ext_force_frame);
@@ -1044,7 +1113,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   O.P.base_vel_des = take(6);
   O.P.ext_force_des = take(3);
   O.P.arm_vel_des = take(3);
-  if (O.dyn == PL_DYN_RNEA) {
+  if (PL_IS_RNEA(O.dyn)) {
     O.P.tau_prev = take(O.nj);
     O.P.W_diag = take(O.nj);
   } else {
@@ -1402,6 +1471,12 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
     return -1;
   }
   PlOcpHandle* h = &o->h;
+  if (solver == PL_SOLVER_IP && h->oc.dyn == PL_DYN_RNEAFD) {
+    // the reference keeps the accelerations in u for its Fatrop branch ("necessary for Fatrop
+    // solver", ocp_whole_body_rnea.py:21); the Lagrangian Hessian here is block diagonal over w_i
+    pl_set_error("the interior-point solver needs include_acc=True (ocp_whole_body_rnea.py:21)");
+    return -1;
+  }
   if (solver == PL_SOLVER_IP && !h->d.ipinfo) {
     const size_t Bm = (size_t)h->B * h->m;
     if (dalloc(o, &h->d.ip_s, Bm) || dalloc(o, &h->d.ip_lam, Bm) || dalloc(o, &h->d.ip_lam0, Bm) ||
@@ -1873,7 +1948,7 @@ int cas_ready() {
 // (nf), joint torques (nt: u's tau block for rnea, RNEA / u's tau_j for the others)
 void cas_u_split(const pl_ocp* o, int& na, int& nf, int& nt) {
   const PlOcpConst& O = o->h.oc;
-  if (O.dyn == PL_DYN_RNEA) { na = O.na; nf = O.nf; nt = O.nj; }
+  if (PL_IS_RNEA(O.dyn)) { na = O.na; nf = O.nf; nt = O.nj; }
   else if (O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA || O.dyn == PL_DYN_ACCNB) { na = O.na; nf = O.nf; nt = O.nj; }
   else if (O.dyn == PL_DYN_CV) { na = O.nv; nf = O.nf; nt = O.nj; }
   else if (O.dyn == PL_DYN_CVNB) { na = O.nj; nf = O.nf; nt = O.nj; }
@@ -1959,10 +2034,11 @@ extern "C" int pl_casadi_bind(pl_ocp* o, int retract_steps) {
   }
   c.sp_q = dense_sp(retract_steps, h.oc.nq);
   c.sp_v = dense_sp(retract_steps, h.oc.nv);
-  c.sp_a = dense_sp(retract_steps, h.oc.nv);  // a: inputs (rnea / acc), ABA (aba), FD + dccrba (cv)
+  // a: inputs (rnea / acc; none for rnea include_acc = False, u_sol[:0]), ABA (aba), FD + dccrba (cv)
+  c.sp_a = dense_sp(retract_steps, h.oc.dyn == PL_DYN_RNEAFD ? 0 : h.oc.nv);
   c.sp_f = dense_sp(retract_steps, nf);
   int ntau = nt;
-  if (h.oc.dyn == PL_DYN_RNEA)
+  if (PL_IS_RNEA(h.oc.dyn))
     for (int i = 0; i < retract_steps; ++i)
       if (o->nodes[i].nu - na - nf < ntau) ntau = o->nodes[i].nu - na - nf;
   c.sp_tau = dense_sp(retract_steps, std::max(ntau, 0));
@@ -2212,12 +2288,12 @@ extern "C" int retract_solution(const double** arg, double** res, casadi_int*, d
     // CasADi dense matrices are column-major: element (row i, col k) at k * S + i
     if (res[0]) for (int k = 0; k < nq; ++k) res[0][k * S + i] = q[k];
     if (res[1]) for (int k = 0; k < nv; ++k) res[1][k * S + i] = v[k];
-    if (res[2]) for (int k = 0; k < nv; ++k) res[2][k * S + i] = a[k];
+    if (res[2] && O.dyn != PL_DYN_RNEAFD) for (int k = 0; k < nv; ++k) res[2][k * S + i] = a[k];
     if (res[3]) for (int k = 0; k < nf; ++k) res[3][k * S + i] = f[k];
     if (res[4]) {
       for (int k = 0; k < ntau; ++k) {
         double t;
-        if (O.dyn == PL_DYN_RNEA) t = u[na + nf + k];
+        if (PL_IS_RNEA(O.dyn)) t = u[na + nf + k];
         else if (O.dyn == PL_DYN_ABA) t = u[k];
         else t = tau[6 + k];
         res[4][k * S + i] = t;

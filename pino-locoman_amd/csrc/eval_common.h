@@ -34,7 +34,7 @@ __device__ inline double objective_wg(const PlDev& d, int b, int N, int n, int n
       double e = xj - pl::u_des(M, O, p, k);
       acc += e * (R[k] * e);
       gj = 2.0 * R[k] * e;
-      if (O.dyn == PL_DYN_RNEA && i == 0 && k >= O.na + O.nf) {
+      if (PL_IS_RNEA(O.dyn) && i == 0 && k >= O.na + O.nf) {
         int t = k - O.na - O.nf;
         double W = p[O.P.W_diag + t];
         double et = xj - p[O.P.tau_prev + t];

@@ -737,7 +737,8 @@ long long rc_ch_stride(int N, int ndx) { return (long long)(N + 1) * 3 * ndx * n
 int rc_chv_stride(int N, int ndx) { return 6 * (N + 2) * ndx; }
 
 bool admm_rc_supported(const PlOcpHandle* h) {
-  return (h->ndx == 24 || h->ndx == 30 || h->ndx == 36 || h->ndx == 48) && (h->rc_waves == 4 || h->rc_waves == 8) && h->nw_max <= 64 * MV && h->nrow_max <= 64 * MR && h->ncpl_max <= 64 &&
+  // the chain blocks F_i = C_i S_i[:, dx] assume one coupling row per dx_{i+1} column
+  return !h->fac_gc && (h->ndx == 24 || h->ndx == 30 || h->ndx == 36 || h->ndx == 48) && (h->rc_waves == 4 || h->rc_waves == 8) && h->nw_max <= 64 * MV && h->nrow_max <= 64 * MR && h->ncpl_max <= 64 &&
          rc_config(h, h->rc_waves).lds <= 160 * 1024;
 }
 

@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void k_hess(PlDev d, int N, int n, int np) {
     } else {
       int k = lc - O.ndx;
       h = 2.0 * p[O.P.R_diag + k];
-      if (O.dyn == PL_DYN_RNEA && i == 0 && k >= O.na + O.nf) h += 2.0 * p[O.P.W_diag + k - O.na - O.nf];
+      if (PL_IS_RNEA(O.dyn) && i == 0 && k >= O.na + O.nf) h += 2.0 * p[O.P.W_diag + k - O.na - O.nf];
     }
     P[j] = h;
   }
@@ -170,6 +170,7 @@ __global__ __launch_bounds__(256) void k_hess(PlDev d, int N, int n, int np) {
     case PL_DYN_CA: hipLaunchKernelGGL(KERNEL<PL_DYN_CA>, __VA_ARGS__); break;     \
     case PL_DYN_ACCNB: hipLaunchKernelGGL(KERNEL<PL_DYN_ACCNB>, __VA_ARGS__); break; \
     case PL_DYN_CVNB: hipLaunchKernelGGL(KERNEL<PL_DYN_CVNB>, __VA_ARGS__); break;   \
+    case PL_DYN_RNEAFD: hipLaunchKernelGGL(KERNEL<PL_DYN_RNEAFD>, __VA_ARGS__); break; \
     default: hipLaunchKernelGGL(KERNEL<PL_DYN_ABA>, __VA_ARGS__); break;           \
   }
 

@@ -343,7 +343,7 @@ __device__ __forceinline__ void store_tiles(const PlDev& d, CFac fn, const doubl
 
 template <int X, bool HL>
 __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, int S_stride, long long fs_stride,
-                                               int nwm, int ny, int ncw, int fac_only) {
+                                               int nwm, int ny, int ncw, int fac_only, int gc, int ncm, int nxcm) {
   const int b = blockIdx.x;
   if constexpr (HL) {
     if (fac_only && !d.ip_iflag[4 * b + 1]) return;
@@ -362,6 +362,10 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
   double* ev = cv + X;      // A_{e_a} (X)
   // optional phase timing (thread 0, s_memtime): 8 accumulators + last stamp in LDS
   unsigned long long* tacc = reinterpret_cast<unsigned long long*>(ev + X);
+  // general coupling (gc): Z [ncm][ncm], staged dx_{i+1} values of the coupling rows, their rho
+  double* Zb = ev + X + 10;
+  double* Axc = Zb + ncm * ncm;
+  double* rcl = Axc + nxcm;
   const bool TIMING = d.dbg != nullptr;  // optional phase timing (PL_ADMM_TIMING=1)
   if (TIMING && tid < 9) tacc[tid] = 0;
   auto T = [&](int slot) {
@@ -389,6 +393,14 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
     CU32 pcl = cp + 3 * X + 1;
     const int npc = fn->npc;
     CU32 cwl = pcl + npc;
+    // general coupling program (api.hip build_factor_prog): crow[nc] | cwptr[nc + 1] | pcl[npc] |
+    // cw[ncw] | xcptr[X + 1] | xc[nxc]
+    const int nc = gc ? fn->nc : 0;
+    CU32 gcwptr = cp + nc;
+    CU32 gpcl = gcwptr + nc + 1;
+    CU32 gcwl = gpcl + npc;
+    CU32 gxcptr = gcwl + (gc && i < N ? (int)gcwptr[nc] : 0);
+    CU32 gxcl = gxcptr + X + 1;
     const double* __restrict__ Asb = d.As + (size_t)b * nnz + fn->ent_off;
     const double* __restrict__ rhob = d.rho + (size_t)b * m + fn->row_off;
     __syncthreads();
@@ -433,7 +445,12 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
       unsigned long long ts0 = 0;
       if (TIMING) ts0 = __builtin_amdgcn_s_memtime();
       if (i > 0) store_tiles(d, (CFac)d.fnodes + (i - 1), Sl, Sg, 64, NT - 64, tid);
-      if (i < N) {
+      if (i < N && gc) {
+        const int ncwi = (int)gcwptr[nc], nxci = (int)gxcptr[X];
+        for (int q = tid - 64; q < ncwi; q += NT - 64) Acw[q] = Asb[gcwl[q] & 0xffff];
+        for (int q = tid - 64; q < nxci; q += NT - 64) Axc[q] = Asb[gxcl[q] & 0xffff];
+        for (int q = tid - 64; q < nc; q += NT - 64) rcl[q] = rhob[crow[q]];
+      } else if (i < N) {
         const int ncwi = (int)cwptr[X];
         for (int q = tid - 64; q < ncwi; q += NT - 64) Acw[q] = Asb[cwl[q] & 0xffff];
         for (int a = tid - 64; a < X; a += NT - 64) {
@@ -515,6 +532,59 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
     __syncthreads();
     T(2);
     if (i == N) break;
+    if (gc) {
+      // ---- general coupling: E_{i+1} = Wc^T Z Wc with Z = R - R Vc S Vc^T R over the nc
+      // coupling rows (Vc: their w_i parts, Wc: their dx_{i+1} parts)
+      // Y[pc][s] = (S Vc_s^T)[pcl[pc]]
+      if (l < nc) {
+        const int q0 = (int)gcwptr[l], q1 = (int)gcwptr[l + 1];
+        for (int pc = w; pc < npc; pc += 4) {
+          const int p = (int)gpcl[pc];
+          double acc = 0.0;
+          for (int q = q0; q < q1; ++q) acc = fma(Acw[q], Sl[sidx(p, (gcwl[q] >> 16) & 0xff)], acc);
+          Yb[pc * nc + l] = acc;
+        }
+      }
+      __syncthreads();
+      T(3);
+      // Z[s][t] = rho_s d_st - rho_s rho_t Vc_s . Y[:, t]  (lower, mirrored)
+      if (l < nc) {
+        const double rt = rcl[l];
+        for (int s2 = w; s2 < nc; s2 += 4) {
+          if (l > s2) continue;
+          double acc = 0.0;
+          for (int q = (int)gcwptr[s2]; q < (int)gcwptr[s2 + 1]; ++q)
+            acc = fma(Acw[q], Yb[(gcwl[q] >> 24) * nc + l], acc);
+          const double rs = rcl[s2];
+          const double z = (s2 == l ? rs : 0.0) - rs * rt * acc;
+          Zb[s2 * nc + l] = z;
+          Zb[l * nc + s2] = z;
+        }
+      }
+      __syncthreads();
+      // T[s][b] = sum_t Z[s][t] Wc[t][b]  (into the Y buffer)
+      if (l < X) {
+        const int q0 = (int)gxcptr[l], q1 = (int)gxcptr[l + 1];
+        for (int s2 = w; s2 < nc; s2 += 4) {
+          double acc = 0.0;
+          for (int q = q0; q < q1; ++q) acc = fma(Axc[q], Zb[s2 * nc + (gxcl[q] >> 16)], acc);
+          Yb[s2 * X + l] = acc;
+        }
+      }
+      __syncthreads();
+      // E[a][b] = sum_s Wc[s][a] T[s][b]  (lower)
+      if (l < X) {
+        for (int a = w; a < X; a += 4) {
+          if (l > a) continue;
+          double acc = 0.0;
+          for (int q = (int)gxcptr[a]; q < (int)gxcptr[a + 1]; ++q)
+            acc = fma(Axc[q], Yb[(gxcl[q] >> 16) * X + l], acc);
+          Eb[lidx(a, l)] = acc;
+        }
+      }
+      T(4);
+      continue;
+    }
     // ---- E_{i+1} = D - Kc S Kc^T, Kc row a = rho_a A_{e_a} w_{s_a}^T (one coupling row per column)
     // Y[pc][bb] = (S w_{s_bb})[pcl[pc]]: thread (w, l) -> bb = l, pc = w (mod 4)
     if (l < X) {
@@ -581,7 +651,8 @@ void launch_fchain(PlOcpHandle* h) {
     attr = true;
   }
   hipLaunchKernelGGL((k_fchain<X, HL>), dim3(h->B), dim3(NT), h->fchain_lds, h->stream, h->d, h->N, h->m, h->nnz,
-                     h->S_stride, h->fs_stride, h->nw_max, h->fchain_ny, h->fchain_ncw, h->fac_only);
+                     h->S_stride, h->fs_stride, h->nw_max, h->fchain_ny, h->fchain_ncw, h->fac_only, h->fac_gc,
+                     h->fchain_nc, h->fchain_nxc);
 }
 
 template <int X, bool HL>

@@ -54,11 +54,16 @@ struct PlFrameRef {
 // true); PL_DYN_ACCNB is internal: whole_body_acc and centroidal_acc with
 // include_base = False (u = [a_j | f], the base acceleration solved from the 6 base
 // equations), which share their rows; PL_DYN_CVNB is internal too: centroidal_vel with
-// include_base = False (u = [v_j | f], the base velocity v_b = A_b^-1 (m h - A_j v_j)).
+// include_base = False (u = [v_j | f], the base velocity v_b = A_b^-1 (m h - A_j v_j));
+// PL_DYN_RNEAFD is whole_body_rnea with include_acc = False (u = [f | tau_j], the RNEA
+// acceleration a_i = (v_{i+1} - v_i) / dt_i by finite difference, ocp_whole_body_rnea.py:183-191,
+// no dv_{i+1} rows).
 enum { PL_DYN_RNEA = 0, PL_DYN_ACC = 1, PL_DYN_ABA = 2, PL_DYN_CV = 3, PL_DYN_CA = 4, PL_DYN_ACCNB = 5,
-       PL_DYN_CVNB = 6 };
+       PL_DYN_CVNB = 6, PL_DYN_RNEAFD = 7 };
 // centroidal_vel in either form: x = [h, q], dx = [dh, dq]
 #define PL_IS_CV(d) ((d) == PL_DYN_CV || (d) == PL_DYN_CVNB)
+// whole_body_rnea in either form: u = [a | f | tau_j] (tau_j on the first tau_nodes nodes), na = 0 for FD
+#define PL_IS_RNEA(d) ((d) == PL_DYN_RNEA || (d) == PL_DYN_RNEAFD)
 
 // Row-block kinds, emitted per node in the reference's subject_to order
 // (optimization/ocp.py:103-190 + setup_dynamics_constraints of each subclass).

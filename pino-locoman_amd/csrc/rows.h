@@ -40,7 +40,7 @@ PL_HD double spline_vel_z(double phase, double period, double h_max, double v_lo
 
 PL_HD int node_type(const PlOcpConst& O, int i) { return i == 0 ? 0 : (i < O.tau_nodes ? 1 : 2); }
 PL_HD int node_nu(const PlOcpConst& O, int i) {
-  if (O.dyn == PL_DYN_RNEA) return O.na + O.nf + (i < O.tau_nodes ? O.nj : 0);
+  if (PL_IS_RNEA(O.dyn)) return O.na + O.nf + (i < O.tau_nodes ? O.nj : 0);
   if (O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA || O.dyn == PL_DYN_ACCNB) return O.na + O.nf;
   if (O.dyn == PL_DYN_CV) return O.nv + O.nf;
   return O.nj + O.nf;  // aba: [tau_j | f]; centroidal_vel without the base: [v_j | f]
@@ -99,6 +99,15 @@ template <class S> PL_HD bool seeded(const VecIn<S>& a, int lo, int hi) {
 
 // Acceleration input of the tree pass for the include_base = False variants: the base
 // acceleration zeroed (the base rows at a_b = 0 give the right-hand side of the base solve).
+// whole_body_rnea with include_acc = False: a = (v_{i+1} - v_i) / dt with v = x_init.v + dv
+// (get_a, ocp_whole_body_rnea.py:183-191), in the oracle's operation order.
+template <class S> struct FdAcc {
+  const double* xv;
+  VecIn<S> dv, dvn;
+  double dt;
+  PL_HD S operator[](int k) const { return ((xv[k] + dvn[k]) - (xv[k] + dv[k])) / dt; }
+};
+
 template <class S> struct ZeroBaseAcc {
   VecIn<S> aj;
   PL_HD S operator[](int k) const { return k < 6 ? S(0.0) : aj[k - 6]; }
@@ -179,10 +188,12 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
   constexpr bool ACCF = (DYN == PL_DYN_ACC || DYN == PL_DYN_CA || DYN == PL_DYN_ACCNB);
   constexpr bool NB = (DYN == PL_DYN_ACCNB);
   constexpr bool COMP = (DYN == PL_DYN_CA || DYN == PL_DYN_ACCNB);
-  const int f_off = (DYN == PL_DYN_RNEA || ACCF) ? O.na : (DYN == PL_DYN_CV ? nv : nj);
+  constexpr bool FD = (DYN == PL_DYN_RNEAFD);
+  const int f_off = (PL_IS_RNEA(DYN) || ACCF) ? O.na : (DYN == PL_DYN_CV ? nv : nj);
   const VecIn<S> a = u;                                   // rnea / acc: a = u[0:nv]
+  const FdAcc<S> afd{xi + nq, sub_in(dx, nv), sub_in(dxn, nv), dt};  // rnea, include_acc = False
   const VecIn<S> forces = sub_in(u, f_off);
-  const VecIn<S> tau_j = sub_in(u, DYN == PL_DYN_RNEA ? O.na + O.nf : 0);
+  const VecIn<S> tau_j = sub_in(u, PL_IS_RNEA(DYN) ? O.na + O.nf : 0);
   // centroidal_vel keeps the state rows at node 0 (ocp.py:137-140, 170-173)
   const bool state_rows = CV || (type != 0);
   NodeKin<S> kin;
@@ -203,7 +214,7 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
     kin.store = kstore;
     kin.stride = kstride;
   }
-  constexpr bool want_tau = (DYN == PL_DYN_RNEA || ACCF);
+  constexpr bool want_tau = (PL_IS_RNEA(DYN) || ACCF);
   // A Jacobian column seeded on dx_{i+1}, or (rnea) on tau_j, has a zero tangent in the
   // tree pass and the ABA: every row that reads them then has a zero derivative, so
   // the pass is skipped (its values are not emitted for such a column's pattern).
@@ -211,8 +222,9 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
   // centroidal pass reads the forces but not h.
   bool tree = true, cen = CV;
   if constexpr (!std::is_same<S, double>::value) {
-    const bool seed_dxn = seeded(dxn, 0, O.ndx);
-    const bool seed_tau = DYN == PL_DYN_RNEA && seeded(u, O.na + O.nf, O.na + O.nf + nj);
+    // (FD: dv_{i+1} enters the pass through a)
+    const bool seed_dxn = seeded(dxn, 0, FD ? nv : O.ndx);
+    const bool seed_tau = PL_IS_RNEA(DYN) && seeded(u, O.na + O.nf, O.na + O.nf + nj);
     // (without the base, h enters the kinematics through v_b; its centroidal pass ran above)
     const bool seed_h = DYN == PL_DYN_CV && seeded(dx, 0, 6);
     const bool seed_f = CV && seeded(u, f_off, f_off + O.nf);
@@ -249,6 +261,8 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
       tree_pass<S>(M, O, qb, qrev, vel, ZeroBaseAcc<S>{a}, forces, want_tau, state_rows, kin, comp, std::true_type{});
     } else if constexpr (COMP) {
       tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin, comp, std::true_type{});
+    } else if constexpr (FD) {
+      tree_pass<S>(M, O, qb, qrev, vel, afd, forces, want_tau, state_rows, kin);
     } else {
       tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin);
     }

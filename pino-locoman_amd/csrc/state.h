@@ -104,6 +104,7 @@ struct PlFacNode {
   int nw, nu, nrow, nent, ent_off, row_off, x_off, s_off, nunit, ntl;
   int asm_off, asm_len, fl_off, fl_len;
   int cp_off, npc;
+  int nc;            // coupling rows (general coupling program, PlOcpHandle::fac_gc)
   long long fs_off;  // doubles: A' (X x X, full) | G (U x X) | C^-1 (U x U), row-major
 };
 #define PL_FAC_NT 256
@@ -271,6 +272,9 @@ struct PlOcpHandle {
   int fg_i0[PL_FAC_MAXGROUPS], fg_n[PL_FAC_MAXGROUPS], fg_lds[PL_FAC_MAXGROUPS], fg_um[PL_FAC_MAXGROUPS];
   int fchain_lds;                   // k_fchain LDS bytes
   int fchain_ny, fchain_ncw;        // k_fchain Y buffer and staged coupling values (doubles)
+  int fac_gc;                       // 1: general coupling (rows of node i touch several dx_{i+1} columns:
+                                    //    whole_body_rnea include_acc = False), E_{i+1} = Wc^T Z Wc in k_fchain
+  int fchain_nc, fchain_nxc;        // general coupling: max coupling rows, max dx_{i+1} entries per node
   PlSettings set;
   PlModel model;
   PlOcpConst oc;

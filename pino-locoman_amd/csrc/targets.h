@@ -39,7 +39,7 @@ PL_HD double f_des_comp(const PlModel& M, const PlOcpConst& O, const double* p, 
 
 // Offset of the forces inside u for the dynamics kind.
 PL_HD int u_force_off(const PlOcpConst& O) {
-  if (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA || O.dyn == PL_DYN_ACCNB) return O.na;
+  if (PL_IS_RNEA(O.dyn) || O.dyn == PL_DYN_ACC || O.dyn == PL_DYN_CA || O.dyn == PL_DYN_ACCNB) return O.na;
   return O.dyn == PL_DYN_CV ? O.nv : O.nj;
 }
 

@@ -53,9 +53,10 @@ STATUS_NAMES = {1: "solved", 2: "solved inaccurate", -2: "maximum iterations rea
 class Layout:
     """Variable / parameter bookkeeping (setup_variables / setup_parameters)."""
 
-    def __init__(self, robot, dynamics, nodes, tau_nodes=3, include_base=True):
+    def __init__(self, robot, dynamics, nodes, tau_nodes=3, include_base=True, include_acc=True):
         self.dynamics = dynamics
         self.include_base = include_base
+        self.include_acc = include_acc
         self.N = nodes
         self.nq, self.nv, self.nj, self.nf = robot.nq, robot.nv, robot.nj, robot.nf
         self.nx = self.nq + self.nv
@@ -71,10 +72,11 @@ class Layout:
             self.nu = [self.nv_opt + nf] * nodes
             self.f_idx, self.tau_idx = self.nv_opt, None
         elif dynamics == "whole_body_rnea":
+            # na_opt = nv, or 0 with finite-difference accelerations (ocp_whole_body_rnea.py:21-26, 69-76)
             self.tau_nodes = tau_nodes
-            self.na = nv
-            self.nu = [nv + nf + nj] * tau_nodes + [nv + nf] * (nodes - tau_nodes)
-            self.f_idx, self.tau_idx = nv, nv + nf
+            self.na = nv if include_acc else 0
+            self.nu = [self.na + nf + nj] * tau_nodes + [self.na + nf] * (nodes - tau_nodes)
+            self.f_idx, self.tau_idx = self.na, self.na + nf
         elif dynamics in ("whole_body_acc", "centroidal_acc"):
             # u = [a | f] or, without the base, [a_j | f] (ocp_whole_body_acc.py:56-63,
             # ocp_centroidal_acc.py:15-19, 57-59)
@@ -161,7 +163,7 @@ class BatchedOCP:
         self.robot = robot
         self.dynamics = dynamics
         self.batch = batch
-        self.layout = Layout(robot, dynamics, nodes, tau_nodes, include_base)
+        self.layout = Layout(robot, dynamics, nodes, tau_nodes, include_base, include_acc)
         self.model_h = ModelCache.get(robot.model)
         s = dict(OSQP_SETTINGS)
         if osqp_settings:
@@ -456,7 +458,7 @@ class OCP:
         self.mass = robot.mass
         self.dynamics = dynamics
         self.dyn = DYNAMICS_CLASSES[dynamics](robot, device=device)
-        self.layout = Layout(robot, dynamics, nodes, tau_nodes, include_base)
+        self.layout = Layout(robot, dynamics, nodes, tau_nodes, include_base, include_acc)
         L = self.layout
         self.nx, self.ndx_opt, self.nu_opt = L.nx, L.ndx, L.nu
         self.f_idx, self.tau_idx = L.f_idx, L.tau_idx

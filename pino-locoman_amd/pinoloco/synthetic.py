@@ -87,9 +87,9 @@ def initial_guess(robot, lay, n_contacts):
     return x
 
 
-def build_batch(robot, dynamics, N, B, first=0, include_base=True):
+def build_batch(robot, dynamics, N, B, first=0, include_base=True, include_acc=True):
     """Parameters P [B][np], initial guesses X [B][n], states XS [B][nx], gait offsets T0 [B]."""
-    lay = Layout(robot, dynamics, N, include_base=include_base)
+    lay = Layout(robot, dynamics, N, include_base=include_base, include_acc=include_acc)
     P = np.zeros((B, lay.np))
     X = np.zeros((B, lay.n))
     XS = np.zeros((B, lay.nx))

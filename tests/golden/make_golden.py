@@ -76,6 +76,12 @@ SQP_CONFIGS = [
      {"include_base": False}),
     # B2G centroidal_vel (ndx = 30: the factor sweeps with a 2-row identity pad)
     ("b2g_cv_n50", "b2g", "centroidal_vel", 50, [("syn", k) for k in range(4)], 3, "trot", {}, 1),
+    # whole_body_rnea with finite-difference accelerations (include_acc = False,
+    # ocp_whole_body_rnea.py:21-26, 157-159, 183-191): the RNEA rows of node i read dv_{i+1}
+    ("go2_rnea_fd_n20", "go2", "whole_body_rnea", 20, [("syn", k) for k in range(4)] + [("stand",)], 3, "trot", {},
+     2, {"include_acc": False}),
+    ("b2g_rnea_fd_n50", "b2g", "whole_body_rnea", 50, [("syn", 0), ("syn", 1)], 1, "trot", {}, 1,
+     {"include_acc": False}),
 ]
 
 # Interior-point (Fatrop branch) fixtures: name, robot, dynamics, N, problems, closed-loop
@@ -128,7 +134,7 @@ def make_problem(R, lay, dyn, N, spec):
         for i in range(N):
             o = lay.x_off[i] + lay.ndx
             if dyn == "whole_body_rnea":
-                u = np.concatenate([np.zeros(R.nv), f] + ([tau[6:]] if i < lay.tau_nodes else []))
+                u = np.concatenate([np.zeros(lay.na), f] + ([tau[6:]] if i < lay.tau_nodes else []))
             elif dyn == "whole_body_aba":  # u = [tau_j, f]
                 u = np.concatenate([tau[6:], f])
             else:  # acc / centroidal families: zero accelerations / velocities, the same forces
@@ -223,7 +229,7 @@ def sqp_fixture(name, rname, dyn, N, problems, loop_steps, gait, osqp, njac, kw=
         P[b], X[b], XS[b], T0[b] = make_problem(R, lay, dyn, N, spec)
     rec = {"P": P, "X": X, "XS": XS, "T0": T0, "gait": np.array(gait), "kinds": np.array([s[0] for s in problems]),
            "osqp_eps": np.array([settings["eps_abs"], settings["eps_rel"]]), "osqp_max_iter": settings["max_iter"],
-           "include_base": int(kw.get("include_base", True))}
+           "include_base": int(kw.get("include_base", True)), "include_acc": int(kw.get("include_acc", True))}
     keys = ("g", "lbg", "ubg", "grad", "f", "J_indptr", "J_indices", "J_data", "dx", "x_new", "xs_next", "status",
             "iters", "accepted", "alpha", "branch", "trials", "viol_max", "quat_trace_le0")
     per = {k: [] for k in keys}

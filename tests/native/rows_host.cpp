@@ -49,6 +49,7 @@ extern "C" int th_node_rows(const void* model, const void* oc, int i, const doub
     case PL_DYN_CA: return run<PL_DYN_CA>(M, O, i, p, dx, u, dxn, seed, g, lb, ub, tan);
     case PL_DYN_ACCNB: return run<PL_DYN_ACCNB>(M, O, i, p, dx, u, dxn, seed, g, lb, ub, tan);
     case PL_DYN_CVNB: return run<PL_DYN_CVNB>(M, O, i, p, dx, u, dxn, seed, g, lb, ub, tan);
+    case PL_DYN_RNEAFD: return run<PL_DYN_RNEAFD>(M, O, i, p, dx, u, dxn, seed, g, lb, ub, tan);
     default: return run<PL_DYN_ABA>(M, O, i, p, dx, u, dxn, seed, g, lb, ub, tan);
   }
 }

@@ -96,6 +96,35 @@ def test_host_handle_dims_and_pattern(rname, dyn, N, n, m, np_):
     bo.close()
 
 
+@pytest.mark.parametrize("rname,N", [("go2", 20), ("b2g", 50)])
+def test_host_handle_rnea_include_acc_false(rname, N):
+    """whole_body_rnea include_acc=False (ocp_whole_body_rnea.py:21-26, 69-76, 157-159):
+    na_opt = 0 (u = [f | tau_j]), no dv_{i+1} rows, n and m as the oracle counts them, the
+    pattern covers the oracle's non-zeros (the RNEA rows of node i read dv_{i+1})."""
+    from pinoloco.ocp import BatchedOCP
+    from pinoloco.synthetic import build_batch
+    R = make_robot(rname)
+    bo = BatchedOCP(R, "whole_body_rnea", N, batch=1, device=-1, include_acc=False)
+    o = OracleOCP(R, "whole_body_rnea", N, include_acc=False)
+    full = OracleOCP(R, "whole_body_rnea", N)
+    assert bo.n == o.n == full.n - N * R.nv
+    lay, P, X, _, _ = build_batch(R, "whole_body_rnea", N, 1, 3, include_acc=False)
+    g, _, _ = o.eval_g(X[0], P[0])
+    gf, _, _ = full.eval_g(np.zeros(full.n), build_batch(R, "whole_body_rnea", N, 1, 3)[1][0])
+    assert bo.m == g.size == gf.size - N * R.nv
+    rows, cols = bo.pattern()
+    x = X[0] + np.random.default_rng(0).normal(0, 0.05, bo.n)
+    J = o.eval_J(x, P[0]).tocoo()
+    mine = set(zip(rows.tolist(), cols.tolist()))
+    big = {(r, c) for r, c, v in zip(J.row, J.col, J.data) if abs(v) > 1e-12}
+    assert not (big - mine)
+    # node 1's RNEA base rows reach into dv_2 (finite-difference a)
+    nt = bo.node_table()
+    dv2 = set(range(nt[2, 2] + R.nv, nt[2, 2] + 2 * R.nv))
+    assert any(c in dv2 for r, c in big if nt[1, 3] <= r < nt[1, 3] + nt[1, 4])
+    bo.close()
+
+
 def test_host_handle_refuses_solves():
     from pinoloco import _lib
     from pinoloco.ocp import BatchedOCP

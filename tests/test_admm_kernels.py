@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 
 from conftest import golden, make_robot
-from test_gpu import ACCF, CONFIGS, EDGE, _batched, _rel, step_tol
+from test_gpu import ACCF, CONFIGS, EDGE, FD, _batched, _kw, _rel, step_tol
 
 pytestmark = pytest.mark.gpu
 
@@ -52,6 +52,37 @@ def test_chain_sqp_step_matches_golden(name, rname, dyn, N):
         assert _rel(xn[b], G["x_new"][b]) < step_tol(name), b
         g, l, u = o.eval_g(xn[b], G["P"][b])
         assert st["viol_max"][b] == pytest.approx(o.violation_max(g, l, u), rel=1e-10, abs=1e-14), b
+
+
+@pytest.mark.parametrize("name,rname,dyn,N", FD)
+@pytest.mark.parametrize("kernel", ["sweep", "sweep2"])
+def test_general_coupling_sweeps_match_golden(name, rname, dyn, N, kernel):
+    """whole_body_rnea include_acc=False: the RNEA rows of node i read dv_{i+1}, so the
+    factor takes the general coupling program (E_{i+1} = Wc^T Z Wc) and the sweeps the
+    coupling lists with several entries per dx_{i+1} column; the test_gpu.py bars."""
+    from oracle.ocp import OracleOCP
+    G, R, (st, dx, xn) = _solve(name, rname, dyn, N, kernel)
+    o = OracleOCP(R, dyn, N, **_kw(G))
+    for b in range(G["P"].shape[0]):
+        for key, gk in (("status", "status"), ("admm_iters", "iters"), ("ls_branch", "branch"),
+                        ("ls_trials", "trials"), ("ls_alpha", "alpha")):
+            assert st[key][b] == G[gk][b], (key, b)
+        assert _rel(dx[b], G["dx"][b]) < step_tol(name), b
+        assert _rel(xn[b], G["x_new"][b]) < step_tol(name), b
+        g, l, u = o.eval_g(xn[b], G["P"][b])
+        assert st["viol_max"][b] == pytest.approx(o.violation_max(g, l, u), rel=1e-10, abs=1e-14), b
+
+
+def test_general_coupling_refuses_chain_kernel():
+    """The chain kernel's blocks F_i = C_i S_i[:, dx] assume one coupling row per dx_{i+1}
+    column: selecting it for include_acc=False fails loudly; AUTO picks a sweep kernel."""
+    from pinoloco import _lib
+    G = golden("sqp_go2_rnea_fd_n20.npz")
+    R, bo = _batched("go2", "whole_body_rnea", 20, G)
+    assert bo.admm_kernel() in ("sweep", "sweep2")
+    with pytest.raises(_lib.PinolocoError):
+        bo.set_admm_kernel("chain")
+    bo.close()
 
 
 @pytest.mark.parametrize("name,rname,dyn,N", CONFIGS)

@@ -16,7 +16,8 @@ def _cpu(name, rname, dyn, N):
     eps = G["osqp_eps"]
     s = {"eps_abs": float(eps[0]), "eps_rel": float(eps[1]), "max_iter": int(G["osqp_max_iter"])}
     R = make_robot(rname, str(G["gait"]))
-    return G, CpuOCP(R, dyn, N, osqp_settings=s, gait_type=str(G["gait"]))
+    kw = {k: bool(int(G[k])) for k in ("include_base", "include_acc") if k in G}
+    return G, CpuOCP(R, dyn, N, osqp_settings=s, gait_type=str(G["gait"]), **kw)
 
 
 @pytest.mark.parametrize("name,rname,dyn,N,probs", [
@@ -29,6 +30,8 @@ def _cpu(name, rname, dyn, N):
     ("go2_rnea_n20_eps5", "go2", "whole_body_rnea", 20, [0]),
     ("go2_rnea_n20_eps6", "go2", "whole_body_rnea", 20, [0]),
     ("go2_rnea_n20_infeas", "go2", "whole_body_rnea", 20, [0, 1]),
+    # include_acc=False (the RNEA rows read dv_{i+1}): the CPU restatement's KKT is generic
+    ("go2_rnea_fd_n20", "go2", "whole_body_rnea", 20, [0, 1, 4]),
 ])
 def test_cpu_sqp_step_matches_golden(name, rname, dyn, N, probs):
     G, c = _cpu(name, rname, dyn, N)
@@ -46,7 +49,8 @@ def test_cpu_sqp_step_matches_golden(name, rname, dyn, N, probs):
 
 @pytest.mark.parametrize("name,rname,dyn,N", [("go2_rnea_n20", "go2", "whole_body_rnea", 20),
                                               ("go2_cv_n20", "go2", "centroidal_vel", 20),
-                                              ("go2_rnea_n20_walk", "go2", "whole_body_rnea", 20)])
+                                              ("go2_rnea_n20_walk", "go2", "whole_body_rnea", 20),
+                                              ("go2_rnea_fd_n20", "go2", "whole_body_rnea", 20)])
 def test_cpu_mpc_loop_matches_golden(name, rname, dyn, N):
     G, c = _cpu(name, rname, dyn, N)
     K = len(G["loop_states"])

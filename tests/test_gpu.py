@@ -41,11 +41,16 @@ ACCF = [("go2_acc_nb_n20", "go2", "whole_body_acc", 20), ("go2_ca_n20", "go2", "
         ("go2_cv_nb_n20", "go2", "centroidal_vel", 20),
         # B2G centroidal_vel: ndx = 6 + nv = 30, the factor sweeps with a 2-row identity pad
         ("b2g_cv_n50", "b2g", "centroidal_vel", 50)]
+# whole_body_rnea with include_acc=False: a = (v_{i+1} - v_i) / dt, the RNEA rows of node i
+# read dv_{i+1} (general coupling in the factor, ocp_whole_body_rnea.py:183-191)
+FD = [("go2_rnea_fd_n20", "go2", "whole_body_rnea", 20), ("b2g_rnea_fd_n50", "b2g", "whole_body_rnea", 50)]
 
 
 # step bars looser than 1e-9, with the error measured on them (all ADMM kernels)
 STEP_TOL = {"go2_rnea_n20_walk": 2e-8,    # measured 5.4e-9
-            "go2_rnea_n20_stand": 3e-7}   # measured 1.0e-7 (all four feet in stance)
+            "go2_rnea_n20_stand": 3e-7,   # measured 1.0e-7 (all four feet in stance)
+            "go2_rnea_fd_n20": 1e-8}      # measured 2.7e-9 (problem 2; include_acc=False: the
+                                          # dense M / dt coupling blocks enter E_{i+1})
 
 
 def step_tol(name):
@@ -64,20 +69,24 @@ def _settings(G):
     return {"eps_abs": float(eps[0]), "eps_rel": float(eps[1]), "max_iter": mi}, gait
 
 
+def _kw(G):
+    """include_base / include_acc the fixture was generated with."""
+    return {k: bool(int(G[k])) if k in G else True for k in ("include_base", "include_acc")}
+
+
 def _batched(rname, dyn, N, G, B=None):
     from pinoloco.ocp import BatchedOCP
     settings, gait = _settings(G)
     R = make_robot(rname, gait)
     B = B or G["P"].shape[0]
-    ib = bool(int(G["include_base"])) if "include_base" in G else True
-    bo = BatchedOCP(R, dyn, N, batch=B, device=0, osqp_settings=settings, gait_type=gait, include_base=ib)
+    bo = BatchedOCP(R, dyn, N, batch=B, device=0, osqp_settings=settings, gait_type=gait, **_kw(G))
     bo.set_params(G["P"][:B])
     bo.set_x(G["X"][:B])
     bo.init_solver()
     return R, bo
 
 
-@pytest.mark.parametrize("name,rname,dyn,N", CONFIGS + ACCF)
+@pytest.mark.parametrize("name,rname,dyn,N", CONFIGS + ACCF + FD)
 def test_eval_sqp_data_matches_golden(name, rname, dyn, N):
     G = golden(f"sqp_{name}.npz")
     R, bo = _batched(rname, dyn, N, G)
@@ -99,7 +108,7 @@ def test_eval_sqp_data_matches_golden(name, rname, dyn, N):
     bo.close()
 
 
-@pytest.mark.parametrize("name,rname,dyn,N", CONFIGS + EDGE + ACCF)
+@pytest.mark.parametrize("name,rname,dyn,N", CONFIGS + EDGE + ACCF + FD)
 def test_sqp_step_matches_golden(name, rname, dyn, N):
     """One SQP iteration per problem: solver outcome exact, step <= step_tol; the max
     violation at the returned point <= 1e-10 against the oracle's metric at the same
@@ -110,7 +119,7 @@ def test_sqp_step_matches_golden(name, rname, dyn, N):
     st = bo.solve()
     dx = bo.get_step()
     xn = bo.get_x()
-    o = OracleOCP(R, dyn, N, include_base=bool(int(G["include_base"])) if "include_base" in G else True)
+    o = OracleOCP(R, dyn, N, **_kw(G))
     for b in range(G["P"].shape[0]):
         assert st["status"][b] == G["status"][b], b
         assert st["admm_iters"][b] == G["iters"][b], b
@@ -151,7 +160,7 @@ def test_fixture_coverage():
 
 
 @pytest.mark.parametrize("name,rname,dyn,N", [CONFIGS[0], CONFIGS[1], EDGE[0], EDGE[1], EDGE[4], ACCF[0], ACCF[1],
-                                               ACCF[5], ACCF[6]])
+                                               ACCF[5], ACCF[6], FD[0]])
 def test_device_mpc_loop_matches_oracle_loop(name, rname, dyn, N):
     """run_mpc.py:127-143 executed on the device (gait, x_init, warm start, solve,
     x <- integrate(x, DX[1])) vs the oracle's closed loop in the golden file: states
@@ -197,6 +206,42 @@ def test_make_ocp_surface_matches_oracle():
         assert _rel(x_init, want) < 1e-7, k
         assert _rel(ocp.U_prev[0], G["loop_u0"][k]) < 1e-6, k
         assert len(ocp.q_sol) == k + 1 and ocp.get_tau_sol(1).shape == (R.nj,)
+
+
+def test_make_ocp_rnea_include_acc_false_matches_oracle():
+    """make_ocp("whole_body_rnea", include_acc=False) (ocp_whole_body_rnea.py:9-26,
+    183-191) in the run_mpc.py:115-143 loop on the GPU against the oracle's closed loop;
+    u = [f | tau_j], retract leaves a_sol empty (u_sol[:na_opt], na_opt = 0); the Fatrop
+    branch refuses it (the reference keeps a in u for Fatrop, ocp_whole_body_rnea.py:21)."""
+    from pinoloco import _lib
+    from pinoloco.ocp import OCP_ARGS, make_ocp
+    from pinoloco.synthetic import DT_MAX, DT_MIN, SWING_HEIGHT, SWING_VEL_LIMITS, random_state
+    G = golden("sqp_go2_rnea_fd_n20.npz")
+    R = make_robot("go2")
+    xs, t0, vx = random_state(R, 0)
+    ocp = make_ocp("whole_body_rnea", OCP_ARGS["whole_body_rnea"], robot=R, nodes=20, solver="osqp",
+                   include_acc=False)
+    assert ocp.na_opt == 0 and ocp.nu_opt[0] == R.nf + R.nj
+    ocp.set_time_params(DT_MIN, DT_MAX)
+    ocp.set_swing_params(SWING_HEIGHT, list(SWING_VEL_LIMITS))
+    ocp.set_tracking_targets([vx, 0, 0, 0, 0, 0], [0, 0, 0], [0, 0, 0])
+    x_init = xs.copy()
+    ocp.update_initial_state(x_init)
+    ocp.update_gait_sequence(t0)
+    ocp.update_previous_torques(np.zeros(R.nj))
+    ocp.init_solver()
+    for k, want in enumerate(G["loop_states"]):
+        ocp.update_initial_state(x_init)
+        ocp.update_gait_sequence(t0 + k * DT_MIN)
+        ocp.warm_start()
+        ocp.solve(retract_all=False)
+        x_init = ocp.dyn.state_integrate()(x_init, ocp.DX_prev[1])
+        assert _rel(x_init, want) < 1e-7, k
+        assert _rel(ocp.U_prev[0], G["loop_u0"][k]) < 1e-6, k
+        assert ocp.a_sol[-1].shape == (0,) and ocp.tau_sol[-1].shape == (R.nj,)
+    with pytest.raises(_lib.PinolocoError):
+        make_ocp("whole_body_rnea", OCP_ARGS["whole_body_rnea"], robot=R, nodes=20, solver="fatrop",
+                 include_acc=False)
 
 
 def test_make_ocp_centroidal_vel_surface_matches_oracle():

@@ -62,6 +62,9 @@ def _consts(bo):
     # B2G (Z1 arm) centroidal_vel: ndx = 6 + nv = 30 (arm joints in the centroidal map)
     ("b2g", "centroidal_vel", 50, [0, 1, 25, 49], {}),
     ("b2g", "centroidal_vel", 50, [0, 30], {"include_base": False}),
+    # whole_body_rnea with finite-difference accelerations: the RNEA rows read dv_{i+1}
+    ("go2", "whole_body_rnea", 20, None, {"include_acc": False}),
+    ("b2g", "whole_body_rnea", 50, [0, 2, 3, 49], {"include_acc": False}),
 ])
 def test_node_rows_and_dual_jacobian(harness, rname, dyn, N, nodes_checked, kw):
     from pinoloco.ocp import BatchedOCP

@@ -17,7 +17,7 @@ ROOT = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)),
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "pino-locoman_amd")]
 
 from conftest import golden  # noqa: E402
-from test_gpu import ACCF, CONFIGS, EDGE, _batched  # noqa: E402
+from test_gpu import ACCF, CONFIGS, EDGE, FD, _batched  # noqa: E402
 
 
 def rel(a, b):
@@ -29,7 +29,7 @@ def rel(a, b):
 
 def main():
     out = {}
-    for name, rname, dyn, N in CONFIGS + EDGE + ACCF:
+    for name, rname, dyn, N in CONFIGS + EDGE + ACCF + FD:
         G = golden(f"sqp_{name}.npz")
         out[name] = {"kernels": {}}
         for kernel in ("sweep", "sweep2", "chain"):
