@@ -1464,6 +1464,79 @@ extern "C" int pl_ocp_set_sqp_iters(pl_ocp* o, int sqp_iters) {
 // Solver selection (ocp.py:248 / :265 dispatch on the solver string).  The interior
 // point's per-problem state (slacks and multipliers, 7 x m doubles per problem) is
 // allocated on first selection.
+// ---- structurally non-zero pairs of the Lagrangian Hessian blocks (k_lag_hess work list)
+// Probed once on the host with the same hyper-dual row code (rows.h) at a generic point:
+// random x, parameters and multipliers, contact c = 0.5 so that stance and swing rows are
+// both active.  A column pair whose contracted second derivative is exactly 0 there is
+// identically 0 (RNEA is linear in a and f, the velocity rows in v, the integration rows in
+// everything, the base position never enters): about half of the pairs of a whole-body node.
+namespace {
+struct HostHessEmit {
+  const double* lam;
+  double acc;
+  int r;
+  void operator()(const HDual& v, double, double) {
+    acc += lam[r] * v.c;
+    ++r;
+  }
+};
+
+template <int DYN>
+void probe_hess(const PlModel& M, const PlOcpConst& O, int i, const double* p, const double* xw, int nw,
+                const double* lam, std::vector<uint8_t>& nz) {
+  std::vector<HDual> kst(PL_KIN_STORE);
+  const int ndx = O.ndx;
+  nz.assign((size_t)nw * (nw + 1) / 2, 0);
+  for (int k = 0; k < nw; ++k)
+    for (int j = 0; j <= k; ++j) {
+      pl::VecIn<HDual> dx{xw, nullptr, 0.0, j, k};
+      pl::VecIn<HDual> u{xw + ndx, nullptr, 0.0, j - ndx, k - ndx};
+      pl::VecIn<HDual> dxn{xw + nw, nullptr, 0.0, j - nw, k - nw};
+      HostHessEmit e{lam, 0.0, 0};
+      pl::node_rows<HDual, DYN>(M, O, i, p, dx, u, dxn, e, kst.data(), 1);
+      nz[(size_t)k * (k + 1) / 2 + j] = e.acc != 0.0;
+    }
+}
+
+void hess_pattern(const PlOcpHandle& h, const std::vector<PlNode>& nodes, int i, std::vector<uint8_t>& nz) {
+  const PlOcpConst& O = h.oc;
+  uint64_t st = 0x9e3779b97f4a7c15ull ^ (uint64_t)(i + 1);
+  auto rnd = [&]() {  // uniform in (0.5, 1.5)
+    st = st * 6364136223846793005ull + 1442695040888963407ull;
+    return 0.5 + (double)(st >> 11) / 9007199254740992.0;
+  };
+  std::vector<double> p(O.P.np);
+  for (double& v : p) v = rnd();
+  p[O.P.dt_min] = 0.02;
+  p[O.P.dt_max] = 0.05;
+  for (int k = 0; k < 4 * O.N; ++k) {
+    p[O.P.contact + k] = 0.5;
+    p[O.P.swing + k] = 0.3;
+  }
+  p[O.P.n_contacts] = 2.0;
+  p[O.P.swing_period] = 0.4;
+  p[O.P.swing_vel_limits + 1] = -0.2;
+  const int qo = PL_IS_CV(O.dyn) ? 9 : 3;  // quaternion of x_init
+  double qn = 0.0;
+  for (int k = 0; k < 4; ++k) qn += p[O.P.x_init + qo + k] * p[O.P.x_init + qo + k];
+  for (int k = 0; k < 4; ++k) p[O.P.x_init + qo + k] /= sqrt(qn);
+  const int nw = nodes[i].nw;
+  std::vector<double> xw(nw + O.ndx), lam(nodes[i].nrow);
+  for (double& v : xw) v = 0.2 * (rnd() - 1.0);
+  for (size_t r = 0; r < lam.size(); ++r) lam[r] = (r & 1) ? rnd() : -rnd();
+  const PlModel& M = h.model;
+  switch (O.dyn) {
+    case PL_DYN_RNEA: probe_hess<PL_DYN_RNEA>(M, O, i, p.data(), xw.data(), nw, lam.data(), nz); break;
+    case PL_DYN_ACC: probe_hess<PL_DYN_ACC>(M, O, i, p.data(), xw.data(), nw, lam.data(), nz); break;
+    case PL_DYN_CV: probe_hess<PL_DYN_CV>(M, O, i, p.data(), xw.data(), nw, lam.data(), nz); break;
+    case PL_DYN_CA: probe_hess<PL_DYN_CA>(M, O, i, p.data(), xw.data(), nw, lam.data(), nz); break;
+    case PL_DYN_ACCNB: probe_hess<PL_DYN_ACCNB>(M, O, i, p.data(), xw.data(), nw, lam.data(), nz); break;
+    case PL_DYN_CVNB: probe_hess<PL_DYN_CVNB>(M, O, i, p.data(), xw.data(), nw, lam.data(), nz); break;
+    default: probe_hess<PL_DYN_ABA>(M, O, i, p.data(), xw.data(), nw, lam.data(), nz); break;
+  }
+}
+}  // namespace
+
 extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
   REQUIRE_DEVICE(o);
   if (solver != PL_SOLVER_OSQP && solver != PL_SOLVER_IP) {
@@ -1486,24 +1559,24 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
         dalloc(o, &h->d.ipinfo, (size_t)h->B) || dalloc(o, &h->d.ip_dwi, (size_t)2 * h->B) ||
         dalloc(o, &h->d.ip_iflag, (size_t)4 * h->B))
       return -2;
-    // Lagrangian Hessian work list (k_hess.hip): column pairs j <= k of every w_i block,
-    // without the rnea tau_j columns (the rows are linear in them); node blocks packed lower
+    // Lagrangian Hessian work list (k_hess.hip): the structurally non-zero column pairs
+    // j <= k of every w_i block (hess_pattern, one probe per node type); node blocks packed
+    // lower, the pairs not listed stay 0
     std::vector<int2> hl;
     std::vector<int> hoff;
     long long off = 0;
     const PlOcpConst& O = h->oc;
+    std::vector<uint8_t> pat[3];
     for (int i = 0; i <= h->N; ++i) {
       const int nw = o->nodes[i].nw;
       hoff.push_back((int)off);
       off += (long long)nw * (nw + 1) / 2;
       if (i == h->N) break;  // no rows on the last node
-      for (int k = 0; k < nw; ++k) {
-        const bool tk = O.dyn == PL_DYN_RNEA && k >= O.ndx + O.na + O.nf;
-        for (int j = 0; j <= k && !tk; ++j) {
-          if (O.dyn == PL_DYN_RNEA && j >= O.ndx + O.na + O.nf) continue;
-          hl.push_back(make_int2(i, j | (k << 16)));
-        }
-      }
+      const int type = pl::node_type(O, i);
+      if (pat[type].empty()) hess_pattern(*h, o->nodes, i, pat[type]);
+      for (int k = 0; k < nw; ++k)
+        for (int j = 0; j <= k; ++j)
+          if (pat[type][(size_t)k * (k + 1) / 2 + j]) hl.push_back(make_int2(i, j | (k << 16)));
     }
     h->hl_len = (int)hl.size();
     h->hl_stride = (off + 1) & ~1LL;
