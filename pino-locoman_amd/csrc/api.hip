@@ -1781,12 +1781,11 @@ extern "C" int pl_mpc_export(pl_ocp* o, void* device_dst) {
   const int nu0 = o->nodes[0].nu;
   const size_t row = (size_t)nu0 + h->nx;
   char* dst = (char*)device_dst;
-  for (int b = 0; b < h->B; ++b) {
-    PL_CHECK_HIP(hipMemcpyAsync(dst + b * row * 8, h->d.x + (size_t)b * h->n + h->ndx, nu0 * 8,
+  // two strided copies on the handle's stream: u_0 of every problem, then x_state
+  PL_CHECK_HIP(hipMemcpy2DAsync(dst, row * 8, h->d.x + h->ndx, (size_t)h->n * 8, (size_t)nu0 * 8, h->B,
                                 hipMemcpyDeviceToDevice, h->stream));
-    PL_CHECK_HIP(hipMemcpyAsync(dst + (b * row + nu0) * 8, h->d.xstate + (size_t)b * h->nx, h->nx * 8,
-                                hipMemcpyDeviceToDevice, h->stream));
-  }
+  PL_CHECK_HIP(hipMemcpy2DAsync(dst + (size_t)nu0 * 8, row * 8, h->d.xstate, (size_t)h->nx * 8, (size_t)h->nx * 8,
+                                h->B, hipMemcpyDeviceToDevice, h->stream));
   PL_CHECK_HIP(hipStreamSynchronize(h->stream));
   return 0;
 }
