@@ -65,24 +65,26 @@ def test_shapes_and_sparsity(rname, dyn, N):
     bo.close()
 
 
-def test_retract_solution_matches_oracle():
+@pytest.mark.parametrize("include_acc", [True, False])
+def test_retract_solution_matches_oracle(include_acc):
     """retract_solution (ocp_whole_body_rnea.py:326-366): node-major rows of q, v, a,
-    forces, tau over the first 3 nodes, q/v by the Lie-group integrate."""
+    forces, tau over the first 3 nodes, q/v by the Lie-group integrate; with
+    include_acc=False a is u_sol[:0] (no columns)."""
     from oracle.ocp import OracleOCP
     from pinoloco import casadi_ext
     from pinoloco.ocp import BatchedOCP
     R = make_robot("b2g")
     N = 8
-    bo = BatchedOCP(R, "whole_body_rnea", N, batch=1, device=-1)
+    bo = BatchedOCP(R, "whole_body_rnea", N, batch=1, device=-1, include_acc=include_acc)
     casadi_ext.bind(bo, 3)
     fr = casadi_ext.ExternalFunction("retract_solution")
     rng = np.random.default_rng(3)
     sol = rng.normal(size=bo.n) * 0.1
     x_init = np.concatenate([R.q0, rng.normal(size=R.nv) * 0.1])
     q, v, a, f, tau = fr(sol, x_init)
-    o = OracleOCP(R, "whole_body_rnea", N)
+    o = OracleOCP(R, "whole_body_rnea", N, include_acc=include_acc)
     DX, U = o.split(sol)
-    assert q.shape == (3, R.nq) and v.shape == (3, R.nv)
+    assert q.shape == (3, R.nq) and v.shape == (3, R.nv) and a.shape == (3, o.na)
     for i in range(3):
         xs = o.integrate_state(x_init, DX[i])
         assert np.abs(q[i] - xs[:R.nq]).max() < 1e-12
