@@ -937,12 +937,12 @@ int build_factor_prog(pl_ocp* o) {
   for (int g = 0; g < h.nfgroup; ++g)
     if (h.fg_lds[g] > 160 * 1024) { pl_set_error("factor kernel: node needs %d bytes of LDS", h.fg_lds[g]); return -1; }
   // k_fchain LDS: packed lower S (even) | Y / transpose buffer, the pivot buffer during the
-  // sweep | E (packed lower) | staged coupling values (ncw + 2 X) | timing stamps (84 KB for
-  // B2G rnea, one chain per CU: the chain is latency-bound, 81 k cycles per node)
+  // sweep | E (packed lower) | staged coupling values (ncw + 2 X) | timing stamps (74 KB for
+  // B2G rnea: two chains per CU, which the latency-bound chain needs)
   // (general coupling: Y [npc][nc], then T = Z Wc [nc][X] in the Y buffer, and behind the
   // stamps Z [nc][nc], the staged dx_{i+1} values [nxc] and rho of the coupling rows [nc])
   const int nS = (h.nw_max * (h.nw_max + 1) / 2 + 1) & ~1;
-  int ny = std::max(std::max(npc_max * X, X * (X + 1)), 1024);
+  int ny = std::max(std::max((npc_max + 1) / 2 * X, X * (X + 1)), 1024);  // Y in two halves (k_fchain)
   if (h.fac_gc) ny = std::max(ny, std::max(npc_max, X) * nc_max);
   ny = (ny + 1) & ~1;
   const int nE = (X * (X + 1) / 2 + 1) & ~1;

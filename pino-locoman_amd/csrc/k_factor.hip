@@ -46,6 +46,14 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Workgroup barrier that orders LDS only (lgkmcnt + s_barrier): __syncthreads() would also
+// wait for every outstanding global store.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // compile-time loop: f(std::integral_constant<int, k>) for k in [K0, K1), so register
 // arrays indexed by k stay in registers
 template <int K0, int K1, class F>
@@ -73,98 +81,108 @@ __device__ __forceinline__ f64x4 mfma4(double a, double b, f64x4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// Blocked sweep of the first 4 nblocks pivots of a symmetric matrix whose columns are
-// held one per lane (R rows in registers), four pivots P = [k, k + 4) per block:
+// Blocked symmetric sweep, four pivots P = [k, k + 4) per block:
 //   Q = M_PP^-1;  non-pivot column j: t = Q M_Pj, M_rj -= M_rP t, M_Pj = t;
 //   pivot column j = k + q: M_rj = (M_rP Q)_q, M_Pj = -Q_:q.
 // After all pivots the swept block holds -M^-1 (Schur complements / G elsewhere).
-// The loop is rolled (small code: the instruction cache holds it) and the register
-// column rotates by four rows per block, so the current pivot rows are always
-// col[0..3]: at block B, col[r] holds row (r + 4 B) mod R.  The publishing wave
-// writes its pivot-row entries (M_{k+p, l} = M_{l, k+p} by symmetry) twice, at lane l
-// and lane l + R, so row (r + k) needs no modulo.  pb: 2 x [2 R_pub][4] doubles.
-// kSync: 0 = one wave (wave-scope fence), 1 = workgroup barrier (publisher and
-// readers are different waves; every wave of the group must call).
-// kTrack: pmin <- min(pmin, every pivot) (the positive-definiteness test of the
-// interior-point inertia correction; pivots are wave-uniform)
-template <int R, int kSync, int kBatch, bool kTrack = false>
-__device__ __forceinline__ void sweep_rot(double (&col)[R], double* pb, int pbstride, int l, int nblocks,
-                                          bool publish, bool active, bool pivcols, double* pmin = nullptr) {
+// Columns are held one per lane.  The loop over the pivot blocks is rolled (small code:
+// the instruction cache holds it; the fully unrolled 48-step sweep was ~60 KB of code and
+// ran 4x slower).  Until r03 one wave held all rows of its columns with the register column
+// rotating four rows per block (sweep_rot); the rows are now dealt to several waves.
+// The rows of every column are dealt to NW waves in blocks of four
+// (block B -> wave B % NW of the column set, local block B / NW): a wave holds NB local
+// blocks = 4 NB rows of column l (lane), col[4 j + q] = row 4 (ws + NW j) + q, ws = the
+// wave's index within its column set.  Per pivot block the owner wave of each column set
+// publishes its four pivot rows at its columns (pkC: the set holding the pivot columns,
+// whose entries at column r are also M_{r,P} by symmetry; pkO: this wave's set), one
+// barrier, then every wave updates its own rows from the broadcast pivot rows.  Each
+// element sees the same operations in the same order as in the one-wave rotated sweep, with
+// 1 / NW of the rows per wave.  No rotation: col[] ends in natural order.  Rows past R (waves with fewer
+// blocks) are padding and never used.  Every wave of the workgroup must call.
+//   isC: this wave belongs to the set holding the pivot columns (identity on its pivot lanes)
+//   ncol: lanes carrying a column of this wave's set (the others duplicate column ncol - 1)
+//   side(B): independent work interleaved with pivot block B (k_fchain: slices of the
+//   previous node's tile store); the barriers order LDS only, so its global stores drain
+//   in the background
+template <int NB, int R, int NW, bool kTrack = false, class Side>
+__device__ __forceinline__ void sweep_split(double (&col)[4 * NB], double* pbC, double* pbO, int pbstride, int l,
+                                            int ws, bool isC, int ncol, double* pmin, Side&& side) {
+  constexpr int nblocks = R / 4;
+  // outer loop unrolled over the local block index (so the owner's pivot rows are
+  // compile-time register indices), inner loop rolled over the owner wave
+#pragma unroll
+  for (int lb = 0; lb < NB; ++lb)
 #pragma unroll 1
-  for (int B = 0; B < nblocks; ++B) {
+  for (int ow = 0; ow < NW; ++ow) {
+    const int B = NW * lb + ow;
+    if (B >= nblocks) break;
     const int k = 4 * B;
-    double* pk = pb + (B & 1) * pbstride;
-    if (publish && l < R) {  // lanes past R hold no row of the swept block
-      const double2 v0 = make_double2(col[0], col[1]), v1 = make_double2(col[2], col[3]);
-      double2* pw = reinterpret_cast<double2*>(pk + 4 * l);
-      pw[0] = v0;
-      pw[1] = v1;
-      double2* pw2 = reinterpret_cast<double2*>(pk + 4 * (l + R));
-      pw2[0] = v0;
-      pw2[1] = v1;
+    double* pkC = pbC + (B & 1) * pbstride;
+    double* pkO = pbO + (B & 1) * pbstride;
+    if (ws == ow && l < ncol) {
+      double2* pw = reinterpret_cast<double2*>(pkO + 4 * l);
+      pw[0] = make_double2(col[4 * lb], col[4 * lb + 1]);
+      pw[1] = make_double2(col[4 * lb + 2], col[4 * lb + 3]);
     }
-    if constexpr (kSync == 0) wsync();
-    else __syncthreads();
-    if (active) {
-      const double2* pr = reinterpret_cast<const double2*>(pk + 4 * k);  // row k + r at pr[2 r]
-      double m[4][4];
+    lds_barrier();
+    side(B);
+    const double2* pr = reinterpret_cast<const double2*>(pkC + 4 * k);
+    double m[4][4];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const double2 a = pr[2 * p], b = pr[2 * p + 1];
-        m[p][0] = a.x; m[p][1] = a.y; m[p][2] = b.x; m[p][3] = b.y;
+    for (int p = 0; p < 4; ++p) {
+      const double2 a = pr[2 * p], b = pr[2 * p + 1];
+      m[p][0] = a.x; m[p][1] = a.y; m[p][2] = b.x; m[p][3] = b.y;
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if constexpr (kTrack) *pmin = fmin(*pmin, m[p][p]) + (m[p][p] == m[p][p] ? 0.0 : -1.0);  // NaN: fails
+      const double pinv = rcp_nr(m[p][p]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (r != p && c != p) m[r][c] = fma(-m[r][p] * pinv, m[p][c], m[r][c]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r != p) { m[r][p] *= pinv; m[p][r] *= pinv; }
+      m[p][p] = -pinv;
+    }
+    // this lane's column of the pivot rows
+    const int lc = min(l, ncol - 1);
+    const double2 o0 = reinterpret_cast<const double2*>(pkO + 4 * lc)[0];
+    const double2 o1 = reinterpret_cast<const double2*>(pkO + 4 * lc)[1];
+    const double own[4] = {o0.x, o0.y, o1.x, o1.y};
+    const int q = l - k;
+    const bool piv = isC && (unsigned)q < 4u;
+    const double pv = piv ? 1.0 : 0.0;
+    double e[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) e[p] = (piv && q == p) ? 1.0 : 0.0;
+    double t[4], nb[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const double qf = -(m[p][0] * own[0] + m[p][1] * own[1] + m[p][2] * own[2] + m[p][3] * own[3]);
+      const double qcol = m[p][0] * e[0] + m[p][1] * e[1] + m[p][2] * e[2] + m[p][3] * e[3];
+      nb[p] = fma(1.0 - pv, qf, qcol);
+      t[p] = nb[p] + e[p];
+    }
+    const bool own_blk = ws == ow;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int g0 = 4 * (ws + NW * j);  // first row of local block j
+      if (own_blk && lb == j) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) col[4 * j + p] = nb[p];
+      } else if (g0 < R) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const double2 ra = reinterpret_cast<const double2*>(pkC + 4 * (g0 + p))[0];
+          const double2 rb = reinterpret_cast<const double2*>(pkC + 4 * (g0 + p))[1];
+          const double h0 = fma(ra.y, t[1], ra.x * t[0]);
+          const double h1 = fma(rb.y, t[3], rb.x * t[2]);
+          col[4 * j + p] = col[4 * j + p] - (h0 + h1);
+        }
       }
-      // m <- -M_PP^-1 (4-pivot sweep, wave-uniform values)
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        if constexpr (kTrack) *pmin = fmin(*pmin, m[p][p]) + (m[p][p] == m[p][p] ? 0.0 : -1.0);  // NaN: fails
-        const double pinv = rcp_nr(m[p][p]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (r != p && c != p) m[r][c] = fma(-m[r][p] * pinv, m[p][c], m[r][c]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (r != p) { m[r][p] *= pinv; m[p][r] *= pinv; }
-        m[p][p] = -pinv;
-      }
-      // branch-free: e_s = [q == s] on pivot lanes (0 elsewhere), pv = [pivot lane]
-      const int q = l - k;
-      const bool piv = pivcols && (unsigned)q < 4u;
-      const double pv = piv ? 1.0 : 0.0;
-      double e[4];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) e[p] = (piv && q == p) ? 1.0 : 0.0;
-      double t[4], nb[4];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const double qf = -(m[p][0] * col[0] + m[p][1] * col[1] + m[p][2] * col[2] + m[p][3] * col[3]);
-        const double qcol = m[p][0] * e[0] + m[p][1] * e[1] + m[p][2] * e[2] + m[p][3] * e[3];  // -Q_pq
-        nb[p] = fma(1.0 - pv, qf, qcol);
-        t[p] = nb[p] + e[p];
-      }
-      // rank-4 update of the other rows, rotated into place: col[r - 4] <- row r, the
-      // broadcast reads issued kBatch rows at a time (registers vs. latency), two-deep chains
-#pragma unroll
-      for (int r0 = 4; r0 < R; r0 += kBatch) {
-        double2 ra[kBatch], rb[kBatch];
-#pragma unroll
-        for (int j = 0; j < kBatch; ++j)
-          if (r0 + j < R) {
-            ra[j] = pr[2 * (r0 + j)];
-            rb[j] = pr[2 * (r0 + j) + 1];
-          }
-#pragma unroll
-        for (int j = 0; j < kBatch; ++j)
-          if (r0 + j < R) {
-            const double h0 = fma(ra[j].y, t[1], ra[j].x * t[0]);
-            const double h1 = fma(rb[j].y, t[3], rb[j].x * t[2]);
-            col[r0 + j - 4] = col[r0 + j] - (h0 + h1);
-          }
-        if (kBatch < R) __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int p = 0; p < 4; ++p) col[R - 4 + p] = nb[p];
     }
   }
 }
@@ -243,42 +261,46 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
   double* Gg = Ag + X * X;
   double* Cg = Gg + U * X;
   if (U > 0) {
-    // ---- sweep the u pivots of [C | B^T]: wave 0 holds column l of C, wave 1 column l of B^T
-    double col[UM];
-    if (w == 0) {
+    // ---- sweep the u pivots of [C | B^T]: waves 0, 2 hold column l of C, waves 1, 3 column
+    // l of B^T, the rows of each column split between the two waves of its set (sweep_split)
+    constexpr int NBU = (UM / 4 + 1) / 2;
+    const int set = w & 1, ws = w >> 1;
+    double col[4 * NBU];
 #pragma unroll
-      for (int r = 0; r < UM; ++r) {  // clamped unconditional loads, then select (no per-element branches)
-        const double v = K[sidx(X + min(r, U - 1), X + min(l, U - 1))];
-        // arithmetic masks, not selects: a select lets the compiler sink each load
-        // into its own branch (one serialised round trip per element)
-        col[r] = fma(v, (r < U && l < U) ? 1.0 : 0.0, (r == l && l >= U) ? 1.0 : 0.0);
-      }
-    } else if (w == 1) {
+    for (int j = 0; j < NBU; ++j)
 #pragma unroll
-      for (int r = 0; r < UM; ++r) {
-        const double v = K[lidx(X + min(r, U - 1), min(l, X - 1))];
-        col[r] = v * ((r < U && l < X) ? 1.0 : 0.0);
+      for (int p = 0; p < 4; ++p) {
+        const int r = 4 * (ws + 2 * j) + p;
+        // clamped unconditional loads, arithmetic masks (no per-element branches)
+        if (set == 0) {
+          const double v = K[sidx(X + min(r, U - 1), X + min(l, U - 1))];
+          col[4 * j + p] = fma(v, (r < U && l < U) ? 1.0 : 0.0, (r == l && l >= U) ? 1.0 : 0.0);
+        } else {
+          const double v = K[lidx(X + min(r, U - 1), min(l, X - 1))];
+          col[4 * j + p] = v * ((r < U && l < X) ? 1.0 : 0.0);
+        }
       }
-    }
-    // pivots k >= U meet an identity pad (wave 0) and zero rows (wave 1): no-ops;
-    // the rotation is back to the identity once all UM / 4 blocks are swept
+    // pivots k >= U meet an identity pad (C) and zero rows (B^T): no-ops
     double pmin = 1.0;
-    sweep_rot<UM, 1, 8, HL>(col, pb, 8 * 64, l, UM / 4, w == 0, w < 2, w == 0, &pmin);
+    sweep_split<NBU, UM, 2, HL>(col, pb, pb + 2 * 256 * set, 256, l, ws, set == 0, set == 0 ? UM : 64, &pmin,
+                                [](int) {});
     if constexpr (HL) {
       if (w == 0 && l == 0 && !(pmin > 0.0)) d.ip_iflag[4 * b] = 1;
     }
-    if (w == 0 && l < U) {
+    __syncthreads();  // every wave is done with the pivot buffers (they share Gs' region)
 #pragma unroll
-      for (int r = 0; r < UM; ++r)
-        if (r < U) Cg[r * U + l] = -col[r];
-    } else if (w == 1 && l < X) {
+    for (int j = 0; j < NBU; ++j)
 #pragma unroll
-      for (int r = 0; r < UM; ++r)
+      for (int p = 0; p < 4; ++p) {
+        const int r = 4 * (ws + 2 * j) + p;
         if (r < U) {
-          Gg[r * X + l] = col[r];
-          Gs[r * X + l] = col[r];
+          if (set == 0 && l < U) Cg[r * U + l] = -col[4 * j + p];
+          if (set == 1 && l < X) {
+            Gg[r * X + l] = col[4 * j + p];
+            Gs[r * X + l] = col[4 * j + p];
+          }
         }
-    }
+      }
     __syncthreads();
   }
   // ---- A' = A - B G (X x X) on the f64 MFMA: lower 16 x 16 tiles (mt >= nt), K = U in
@@ -320,12 +342,10 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
 //
 // Store S_i in the ADMM lane-tile layout (state.h): 4x4 tile t = K l + k of lane l,
 // pair j at s_off + ((k * 8 + j) * 64 + l) * 2 (coalesced over o).  Threads [t0, t0 + nt).
-__device__ __forceinline__ void store_tiles(const PlDev& d, CFac fn, const double* Sl, double* Sg, int t0, int nt,
-                                            int tid) {
+__device__ __forceinline__ void store_tiles_range(CFac fn, const double* Sl, double* Sg, int o0, int o1, int nt) {
   double* Sn = Sg + fn->s_off;
   const int nunit = fn->nunit, ntl = fn->ntl, nw = fn->nw;
-  const int total = nunit * 64 * 16;
-  for (int o = tid - t0; o < total; o += nt) {
+  for (int o = o0; o < o1; o += nt) {
     const int slot = o & 1, ln = (o >> 1) & 63, j = (o >> 7) & 7, k = o >> 10;
     const int t = nunit * ln + k;
     double val = 0.0;
@@ -339,6 +359,12 @@ __device__ __forceinline__ void store_tiles(const PlDev& d, CFac fn, const doubl
     }
     Sn[o] = val;
   }
+}
+
+__device__ __forceinline__ void store_tiles(const PlDev& d, CFac fn, const double* Sl, double* Sg, int t0, int nt,
+                                            int tid) {
+  (void)d;
+  store_tiles_range(fn, Sl, Sg, tid - t0, fn->nunit * 64 * 16, nt);
 }
 
 template <int X, bool HL>
@@ -405,65 +431,80 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
     const double* __restrict__ rhob = d.rho + (size_t)b * m + fn->row_off;
     __syncthreads();
     T(-1);
-    if (w == 0) {
-      // ---- S_xx = (A' + E_i)^-1, one column per lane.  The sweep runs on XS = X rounded up
-      // to 4 pivots: rows / columns X..XS-1 are an identity pad (their pivots are no-ops),
-      // e.g. X = 30 for B2G centroidal_vel (6 + nv).
-      constexpr int XS = (X + 3) & ~3;
-      double col[XS];
-#pragma unroll
-      for (int r = 0; r < XS; ++r)
-      {
-        // lanes >= XS duplicate column XS - 1: never pivots, never published, never stored
-        const int lc = min(l, XS - 1);
-        const int rc = min(r, X - 1), cc = min(lc, X - 1);
-        const double v = Ag[rc * X + cc] + Eb[sidx(rc, cc)];
-        col[r] = (r < X && lc < X) ? v : (r == lc ? 1.0 : 0.0);
+    // ---- all waves: stage node i's coupling values (S_{i-1}, still in Sl, is stored in
+    // slices interleaved with the sweep below)
+    if (i < N && gc) {
+      const int ncwi = (int)gcwptr[nc], nxci = (int)gxcptr[X];
+      for (int q = tid; q < ncwi; q += NT) Acw[q] = Asb[gcwl[q] & 0xffff];
+      for (int q = tid; q < nxci; q += NT) Axc[q] = Asb[gxcl[q] & 0xffff];
+      for (int q = tid; q < nc; q += NT) rcl[q] = rhob[crow[q]];
+    } else if (i < N) {
+      const int ncwi = (int)cwptr[X];
+      for (int q = tid; q < ncwi; q += NT) Acw[q] = Asb[cwl[q] & 0xffff];
+      for (int a = tid; a < X; a += NT) {
+        const double ea = Asb[cent[a]];
+        ev[a] = ea;
+        cv[a] = rhob[crow[a]] * ea;
       }
+    }
+    T(7);
+    {
+      // ---- S_xx = (A' + E_i)^-1, one column per lane, rows over the four waves
+      // (sweep_split).  The sweep runs on XS = X rounded up to 4 pivots: rows / columns
+      // X..XS-1 are an identity pad (their pivots are no-ops), e.g. X = 30 for B2G
+      // centroidal_vel (6 + nv).  Lanes >= XS duplicate column XS - 1: never pivot, never
+      // published, never stored.
+      constexpr int XS = (X + 3) & ~3;
+      constexpr int NB = (XS / 4 + 3) / 4;
+      double col[4 * NB];
+      const int lc = min(l, XS - 1);
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int r = 4 * (w + 4 * j) + p;
+          const int rc = min(r, X - 1), cc = min(lc, X - 1);
+          // clamped unconditional loads, arithmetic masks (a select would sink each load
+          // into its own branch)
+          const double v = Ag[rc * X + cc] + Eb[sidx(rc, cc)];
+          col[4 * j + p] = fma(v, (r < X && lc < X) ? 1.0 : 0.0, (r == lc && !(r < X && lc < X)) ? 1.0 : 0.0);
+        }
       unsigned long long ts0 = 0;
       if (TIMING) ts0 = __builtin_amdgcn_s_memtime();
       double pmin = 1.0;
-      sweep_rot<XS, 0, XS, HL>(col, pb, 8 * 64, l, XS / 4, true, true, true, &pmin);
+      CFac fp = (CFac)d.fnodes + (i > 0 ? i - 1 : 0);
+      const int stot = i > 0 ? fp->nunit * 64 * 16 : 0;
+      constexpr int nblk = XS / 4;
+      const int slice = ((stot + nblk - 1) / nblk + NT - 1) / NT * NT;
+      sweep_split<NB, XS, 4, HL>(col, pb, pb, 8 * 64, l, w, true, XS, &pmin, [&](int B) {
+        const int o0 = B * slice, o1 = min(o0 + slice, stot);
+        if (o0 < o1) store_tiles_range(fp, Sl, Sg, o0 + tid, o1, NT);
+      });
       if constexpr (HL) {
         if (l == 0 && !(pmin > 0.0)) d.ip_iflag[4 * b] = 1;
       }
       if (TIMING) {
         const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
-        if (l == 0) tacc[5] += ts1 - ts0;
+        if (tid == 0) tacc[5] += ts1 - ts0;
       }
-      // symmetrise -col (sweep round-off) through the transpose buffer
+      // symmetrise -col (sweep round-off) through the transpose buffer; the pivot rows of
+      // the last block (pb, inside Yb) are read by every wave before the barrier
       constexpr int XP = X + 1;
+      lds_barrier();  // LDS only: the tile stores issued during the sweep keep draining
       if (l < X) {
 #pragma unroll
-        for (int r = 0; r < X; ++r) Yb[r * XP + l] = -col[r];
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const int r = 4 * (w + 4 * j) + p;
+            if (r < X) Yb[r * XP + l] = -col[4 * j + p];
+          }
       }
-      __syncthreads();  // (a) the other waves are done with Sl (tile store of S_{i-1})
-      if (l < X)
-        for (int r = l; r < X; ++r) Sl[lidx(r, l)] = 0.5 * (Yb[r * XP + l] + Yb[l * XP + r]);
-    } else {
-      // ---- waves 1-3, while wave 0 sweeps: store S_{i-1}, stage node i's coupling values
-      unsigned long long ts0 = 0;
-      if (TIMING) ts0 = __builtin_amdgcn_s_memtime();
-      if (i > 0) store_tiles(d, (CFac)d.fnodes + (i - 1), Sl, Sg, 64, NT - 64, tid);
-      if (i < N && gc) {
-        const int ncwi = (int)gcwptr[nc], nxci = (int)gxcptr[X];
-        for (int q = tid - 64; q < ncwi; q += NT - 64) Acw[q] = Asb[gcwl[q] & 0xffff];
-        for (int q = tid - 64; q < nxci; q += NT - 64) Axc[q] = Asb[gxcl[q] & 0xffff];
-        for (int q = tid - 64; q < nc; q += NT - 64) rcl[q] = rhob[crow[q]];
-      } else if (i < N) {
-        const int ncwi = (int)cwptr[X];
-        for (int q = tid - 64; q < ncwi; q += NT - 64) Acw[q] = Asb[cwl[q] & 0xffff];
-        for (int a = tid - 64; a < X; a += NT - 64) {
-          const double ea = Asb[cent[a]];
-          ev[a] = ea;
-          cv[a] = rhob[crow[a]] * ea;
-        }
+      lds_barrier();
+      for (int o = tid; o < X * X; o += NT) {
+        const int r = o / X, c = o - r * X;
+        if (c <= r) Sl[lidx(r, c)] = 0.5 * (Yb[r * XP + c] + Yb[c * XP + r]);
       }
-      if (TIMING) {
-        const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
-        if (tid == 64) tacc[7] += ts1 - ts0;
-      }
-      __syncthreads();  // (a)
     }
     __syncthreads();
     T(0);
@@ -586,39 +627,54 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
       continue;
     }
     // ---- E_{i+1} = D - Kc S Kc^T, Kc row a = rho_a A_{e_a} w_{s_a}^T (one coupling row per column)
-    // Y[pc][bb] = (S w_{s_bb})[pcl[pc]]: thread (w, l) -> bb = l, pc = w (mod 4)
-    if (l < X) {
-      const int q0 = (int)cwptr[l], q1 = (int)cwptr[l + 1];
-      constexpr int CR = 4;  // list entries held in registers (longer lists: LDS loop)
-      double av[CR];
-      int qc[CR];
+    // Y[pc][bb] = (S w_{s_bb})[pcl[pc]]: thread (w, l) -> bb = l, pc = w (mod 4).  The support
+    // columns are taken in two halves (Y holds ceil(npc / 2) rows: the chain's LDS fits two
+    // workgroups per CU); the E sums run over a coupling row's list in order, the first
+    // half's entries (a prefix: pcl is sorted) in pass 0, the rest in pass 1, so every E
+    // entry sees the same FMA sequence as with the whole Y.
+    const int H = (npc + 1) >> 1;
+    for (int h = 0; h < 2; ++h) {
+      const int pc0 = h * H, pc1 = min(npc, pc0 + H);
+      if (l < X) {
+        const int q0 = (int)cwptr[l], q1 = (int)cwptr[l + 1];
+        constexpr int CR = 4;  // list entries held in registers (longer lists: LDS loop)
+        double av[CR];
+        int qc[CR];
 #pragma unroll
-      for (int j = 0; j < CR; ++j) {
-        const bool ok = q0 + j < q1;
-        av[j] = ok ? Acw[q0 + j] : 0.0;
-        qc[j] = ok ? (int)((cwl[q0 + j] >> 16) & 0xff) : 0;
-      }
-      for (int pc = w; pc < npc; pc += 4) {
-        const int p = (int)pcl[pc];
-        double acc = 0.0;
+        for (int j = 0; j < CR; ++j) {
+          const bool ok = q0 + j < q1;
+          av[j] = ok ? Acw[q0 + j] : 0.0;
+          qc[j] = ok ? (int)((cwl[q0 + j] >> 16) & 0xff) : 0;
+        }
+        for (int pc = pc0 + w; pc < pc1; pc += 4) {
+          const int p = (int)pcl[pc];
+          double acc = 0.0;
 #pragma unroll
-        for (int j = 0; j < CR; ++j) acc = fma(av[j], Sl[sidx(p, qc[j])], acc);
-        for (int q = q0 + CR; q < q1; ++q) acc = fma(Acw[q], Sl[sidx(p, (cwl[q] >> 16) & 0xff)], acc);
-        Yb[pc * X + l] = acc;
+          for (int j = 0; j < CR; ++j) acc = fma(av[j], Sl[sidx(p, qc[j])], acc);
+          for (int q = q0 + CR; q < q1; ++q) acc = fma(Acw[q], Sl[sidx(p, (cwl[q] >> 16) & 0xff)], acc);
+          Yb[(pc - pc0) * X + l] = acc;
+        }
       }
-    }
-    __syncthreads();
-    T(3);
-    if (l < X) {
-      const double cb = cv[l];
-      for (int a = w; a < X; a += 4) {  // lower triangle (l <= a) only: E is symmetric
-        if (l > a) continue;
-        const double ca = cv[a];
-        double acc = 0.0;
-        for (int q = (int)cwptr[a]; q < (int)cwptr[a + 1]; ++q)
-          acc = fma(Acw[q], Yb[(cwl[q] >> 24) * X + l], acc);
-        Eb[lidx(a, l)] = (a == l ? ca * ev[a] : 0.0) - ca * cb * acc;
+      __syncthreads();
+      T(3);
+      if (l < X) {
+        const double cb = cv[l];
+        for (int a = w; a < X; a += 4) {  // lower triangle (l <= a) only: E is symmetric
+          if (l > a) continue;
+          double acc = h ? Eb[lidx(a, l)] : 0.0;
+          for (int q = (int)cwptr[a]; q < (int)cwptr[a + 1]; ++q) {
+            const int pq = (int)(cwl[q] >> 24);
+            if (pq >= pc0 && pq < pc1) acc = fma(Acw[q], Yb[(pq - pc0) * X + l], acc);
+          }
+          if (h == 0) {
+            Eb[lidx(a, l)] = acc;
+          } else {
+            const double ca = cv[a];
+            Eb[lidx(a, l)] = (a == l ? ca * ev[a] : 0.0) - ca * cb * acc;
+          }
+        }
       }
+      if (h == 0) __syncthreads();
     }
     T(4);
   }
