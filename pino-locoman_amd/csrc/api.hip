@@ -727,7 +727,7 @@ int build_factor_prog(pl_ocp* o) {
   };
   long long fs = 0;
   std::vector<int> lds_of(N + 1), um_of(N + 1);
-  int npc_max = 1, ncw_max = 2, nc_max = 1, nxc_max = 2;
+  int npc_max = 1, ncw_max = 2, nc_max = 1, nxc_max = 2, cwlen_max = 0;
   // General coupling (h.fac_gc) when some node's rows touch a dx_{i+1} column more than once
   // or one row touches several (whole_body_rnea include_acc = False: the RNEA rows read
   // a = (v_{i+1} - v_i) / dt); otherwise every dx_{i+1} column has exactly one coupling row.
@@ -908,6 +908,7 @@ int build_factor_prog(pl_ocp* o) {
       f.npc = (int)pcl.size();
       npc_max = std::max(npc_max, f.npc);
       ncw_max = std::max(ncw_max, (int)q);
+      for (int a = 0; a < X; ++a) cwlen_max = std::max(cwlen_max, (int)cw[a].size());
       f.cp_off = intern32(cpls, cpl_offs, o->kcpl, C);
     }
     f.fs_off = fs;
@@ -947,6 +948,9 @@ int build_factor_prog(pl_ocp* o) {
   ny = (ny + 1) & ~1;
   const int nE = (X * (X + 1) / 2 + 1) & ~1;
   h.fchain_ny = ny;
+  // short coupling-row lists (the integration rows of rnea / acc: 2 entries): E_{i+1} straight
+  // from S (4 products per entry) instead of through Y
+  h.fchain_short = !h.fac_gc && cwlen_max <= 4;
   h.fchain_ncw = (ncw_max + 1) & ~1;
   h.fchain_nc = h.fac_gc ? nc_max : 0;
   h.fchain_nxc = h.fac_gc ? (nxc_max + 1) & ~1 : 0;

@@ -369,7 +369,8 @@ __device__ __forceinline__ void store_tiles(const PlDev& d, CFac fn, const doubl
 
 template <int X, bool HL>
 __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, int S_stride, long long fs_stride,
-                                               int nwm, int ny, int ncw, int fac_only, int gc, int ncm, int nxcm) {
+                                               int nwm, int ny, int ncw, int fac_only, int gc, int ncm, int nxcm,
+                                               int short_cw) {
   const int b = blockIdx.x;
   if constexpr (HL) {
     if (fac_only && !d.ip_iflag[4 * b + 1]) return;
@@ -627,6 +628,26 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
       continue;
     }
     // ---- E_{i+1} = D - Kc S Kc^T, Kc row a = rho_a A_{e_a} w_{s_a}^T (one coupling row per column)
+    if (short_cw) {
+      // short lists: E[a][b] = d_ab - c_a c_b sum_{q in a} A_q sum_{q' in b} A_q' S[c_q][c_q'] straight
+      // from S, in the FMA order of the Y route below (bit-identical)
+      for (int o = tid; o < X * X; o += NT) {
+        const int a = o / X, bb = o - a * X;
+        if (bb > a) continue;
+        const int qb0 = (int)cwptr[bb], qb1 = (int)cwptr[bb + 1];
+        double acc = 0.0;
+        for (int q = (int)cwptr[a]; q < (int)cwptr[a + 1]; ++q) {
+          const int p = (int)((cwl[q] >> 16) & 0xff);
+          double y = 0.0;
+          for (int q2 = qb0; q2 < qb1; ++q2) y = fma(Acw[q2], Sl[sidx(p, (cwl[q2] >> 16) & 0xff)], y);
+          acc = fma(Acw[q], y, acc);
+        }
+        const double ca = cv[a];
+        Eb[lidx(a, bb)] = (a == bb ? ca * ev[a] : 0.0) - ca * cv[bb] * acc;
+      }
+      T(4);
+      continue;
+    }
     // Y[pc][bb] = (S w_{s_bb})[pcl[pc]]: thread (w, l) -> bb = l, pc = w (mod 4).  The support
     // columns are taken in two halves (Y holds ceil(npc / 2) rows: the chain's LDS fits two
     // workgroups per CU); the E sums run over a coupling row's list in order, the first
@@ -708,7 +729,7 @@ void launch_fchain(PlOcpHandle* h) {
   }
   hipLaunchKernelGGL((k_fchain<X, HL>), dim3(h->B), dim3(NT), h->fchain_lds, h->stream, h->d, h->N, h->m, h->nnz,
                      h->S_stride, h->fs_stride, h->nw_max, h->fchain_ny, h->fchain_ncw, h->fac_only, h->fac_gc,
-                     h->fchain_nc, h->fchain_nxc);
+                     h->fchain_nc, h->fchain_nxc, h->fchain_short);
 }
 
 template <int X, bool HL>

@@ -275,6 +275,7 @@ struct PlOcpHandle {
   int fac_gc;                       // 1: general coupling (rows of node i touch several dx_{i+1} columns:
                                     //    whole_body_rnea include_acc = False), E_{i+1} = Wc^T Z Wc in k_fchain
   int fchain_nc, fchain_nxc;        // general coupling: max coupling rows, max dx_{i+1} entries per node
+  int fchain_short;                 // 1: coupling rows' w lists <= 4 entries: k_fchain forms E without Y
   PlSettings set;
   PlModel model;
   PlOcpConst oc;
