@@ -48,6 +48,12 @@ struct pl_ocp {
   std::vector<double> h_params;  // host copy of the parameters (B x np)
   std::vector<void*> allocs;
   hipEvent_t ev[5];
+  // pl_mpc_step replay: the launches of one OSQP-SQP MPC step after k_mpc_prepare, captured
+  // once into a HIP graph and replayed while the handle's host state is unchanged
+  hipGraphExec_t mpc_graph = nullptr;
+  std::vector<unsigned char> mpc_key;  // bytes of `h` the graph was captured with (or last seen)
+  int mpc_graph_off = 0;               // 1: capture failed or PL_MPC_GRAPH=0: launch eagerly
+  long long mpc_captures = 0;
 };
 
 extern "C" const char* pl_last_error(void) { return g_err; }
@@ -1274,6 +1280,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
     }
     if (admm_select(o, kind)) { pl_ocp_destroy(o); return -2; }
   }
+  o->mpc_graph_off = getenv("PL_MPC_GRAPH") && atoi(getenv("PL_MPC_GRAPH")) == 0;
   if (hipMemcpy(D.model, &h.model, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(D.oc, &h.oc, sizeof(PlOcpConst), hipMemcpyHostToDevice) != hipSuccess) {
     pl_set_error("upload of model tables failed");
@@ -1294,6 +1301,7 @@ extern "C" void pl_ocp_destroy(pl_ocp* o) {
     hipStreamSynchronize(o->h.stream);
     for (void* p : o->allocs) hipFree(p);
     for (int k = 0; k < 5; ++k) hipEventDestroy(o->ev[k]);
+    if (o->mpc_graph) hipGraphExecDestroy(o->mpc_graph);
     hipStreamDestroy(o->h.stream);
   }
   delete o;
@@ -1749,19 +1757,74 @@ extern "C" int pl_mpc_setup(pl_ocp* o, const double* x_state, const double* t0) 
   return 0;
 }
 
+// The OSQP-SQP part of an MPC step (every launch after k_mpc_prepare) as one HIP graph.
+// The sequence is fixed by the handle's host state (sizes, settings, kernel choice,
+// device pointers): it is captured on the second step that sees the same bytes of `h`
+// (the first runs eagerly, so every one-time kernel attribute is set outside a capture)
+// and replayed while they stay the same; any change (a setter, another kernel choice)
+// runs eagerly once and re-captures.  Per-call data lives in device memory, so a replay
+// is the eager sequence.  Profiling runs (per-launch events) and PL_MPC_GRAPH=0 stay eager.
+static void enqueue_mpc_sqp(pl_ocp* o) {
+  for (int it = 0; it < o->h.sqp_iters; ++it) enqueue_solve(o, false);
+  launch_mpc_finish(&o->h);
+}
+
+static int mpc_sqp_graph(pl_ocp* o) {
+  PlOcpHandle* h = &o->h;
+  const unsigned char* hb = reinterpret_cast<const unsigned char*>(h);
+  const bool same = o->mpc_key.size() == sizeof(PlOcpHandle) && !memcmp(o->mpc_key.data(), hb, sizeof(PlOcpHandle));
+  if (same && o->mpc_graph) return hipGraphLaunch(o->mpc_graph, h->stream) == hipSuccess ? 0 : -1;
+  if (o->mpc_graph) {
+    hipGraphExecDestroy(o->mpc_graph);
+    o->mpc_graph = nullptr;
+  }
+  if (!same) {  // first sighting of this state: eager, remember it
+    o->mpc_key.assign(hb, hb + sizeof(PlOcpHandle));
+    enqueue_mpc_sqp(o);
+    return 0;
+  }
+  hipGraph_t g = nullptr;
+  if (hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) return -1;
+  enqueue_mpc_sqp(o);
+  const hipError_t ec = hipStreamEndCapture(h->stream, &g);
+  if (ec != hipSuccess || !g) {
+    (void)hipGetLastError();
+    if (g) hipGraphDestroy(g);
+    return -1;
+  }
+  const hipError_t ei = hipGraphInstantiate(&o->mpc_graph, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (ei != hipSuccess) {
+    o->mpc_graph = nullptr;
+    return -1;
+  }
+  ++o->mpc_captures;
+  return hipGraphLaunch(o->mpc_graph, h->stream) == hipSuccess ? 0 : -1;
+}
+
 extern "C" int pl_mpc_step(pl_ocp* o, int k) {
   REQUIRE_DEVICE(o);
   if (o->h.profile && o->h.prof_n > 48) prof_collect(&o->h);
   launch_mpc_prepare(&o->h, k);
+  if (o->h.solver != PL_SOLVER_IP && !o->h.profile && !o->mpc_graph_off) {
+    if (mpc_sqp_graph(o)) {
+      // capture or replay refused: nothing of the step ran; from now on launch eagerly
+      (void)hipGetLastError();
+      o->mpc_graph_off = 1;
+      enqueue_mpc_sqp(o);
+    }
+    PL_CHECK_HIP(hipGetLastError());
+    return 0;
+  }
   if (o->h.solver == PL_SOLVER_IP) {
     enqueue_ip(&o->h);
     // warm_start() of the next step passes this solve's lam_g back (ocp.py:373, ocp_*.py warm_start)
     PlOcpHandle* h = &o->h;
     PL_CHECK_HIP(hipMemcpyAsync(h->d.ip_lam0, h->d.ip_lam, (size_t)h->B * h->m * 8, hipMemcpyDeviceToDevice, h->stream));
     h->ip_lam_warm = 1;
+    launch_mpc_finish(&o->h);
   } else
-    for (int it = 0; it < o->h.sqp_iters; ++it) enqueue_solve(o, false);
-  launch_mpc_finish(&o->h);
+    enqueue_mpc_sqp(o);
   PL_CHECK_HIP(hipGetLastError());
   return 0;
 }

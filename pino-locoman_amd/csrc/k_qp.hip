@@ -489,9 +489,9 @@ void launch_admm_init(PlOcpHandle* h) {
 // ---------------------------------------------------------------------------
 // Termination (OSQP 0.6 update_info + check_termination, incl. infeasibility
 // certificates and the x10 "approximate" check at max_iter).
-// Residual norms per (problem, node): the node's A values, x (w_i and dx_{i+1} are
-// contiguous in x) and y are staged in LDS so the row gathers of A x never leave the
-// workgroup; one 64-thread block per (problem, node), partial maxima to d.chk.
+// Residual norms per (problem, node): x (w_i and dx_{i+1} are contiguous in x) is staged
+// in LDS for the row gathers of A x; one 64-thread block per (problem, node), partial
+// maxima to d.chk.
 //   chk[b][i][0..2] = max |E^-1 (A x - z)|, |E^-1 z|, |E^-1 A x|   over node i's rows
 //   chk[b][i][3..6] = max |D^-1 (P x + q + A^T y)|, |D^-1 q|, |D^-1 A^T y|, |D^-1 P x|
 //                     over node i's columns w_i
@@ -503,18 +503,18 @@ __global__ __launch_bounds__(64) void k_check_part(PlDev d, int N, int n, int m,
   if (d.info[b].done) return;
   const PlNode nd = d.nodes[i];
   const int tid = threadIdx.x;
-  const int nent = nd.nent, nrow = nd.nrow, nw = nd.nw, ncol = nd.ncol;
-  // the node's A values are read in place: one block touches ~8 KB of A, L1-resident
-  const double* __restrict__ Al = d.As + (size_t)b * nnz + nd.ent_off;
-  double* xl = lds;                    // ncol (w_i, dx_{i+1})
-  double* yl = xl + ((ncol + nw + 1) & ~1);  // nrow
-  const double* As = d.As + (size_t)b * nnz;
+  const int nrow = nd.nrow, nw = nd.nw, ncol = nd.ncol;
+  const double* __restrict__ As = d.As + (size_t)b * nnz;
+  double* xl = lds;  // ncol (w_i, dx_{i+1})
   const double* xa = d.xa + (size_t)b * n;
-  const double* ya = d.ya + (size_t)b * m;
+  const double* __restrict__ ya = d.ya + (size_t)b * m;
   for (int c = tid; c < max(ncol, nw); c += 64) xl[c] = xa[nd.x_off + c];
-  for (int r = tid; r < nrow; r += 64) yl[r] = ya[nd.row_off + r];
   __syncthreads();
   double v[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  // The gathers run in chunks of CK entries: the CK index words, then the CK values, then
+  // the CK FMAs in entry order, so a row of length L costs ~2 L / CK dependent memory round
+  // trips instead of ~2 L / 4 (same FMA sequence, hence the same bits as one entry at a time).
+  constexpr int CK = 8;
   {
     const double* za = d.za + (size_t)b * m + nd.row_off;
     const double* E = d.E + (size_t)b * m + nd.row_off;
@@ -522,15 +522,21 @@ __global__ __launch_bounds__(64) void k_check_part(PlDev d, int N, int n, int m,
     const int2* __restrict__ ec = d.gr_ec;
     for (int r = tid; r < nrow; r += 64) {
       double ax = 0.0;
-      const int q1 = rp[r + 1];
-#pragma unroll 4
-      for (int q = rp[r]; q < q1; ++q) {
-        const int2 ej = ec[q];  // the row's entries and columns belong to node i
-        ax += Al[ej.x - nd.ent_off] * xl[ej.y - nd.x_off];
+      const int q0 = rp[r], q1 = rp[r + 1];
+      const double ei = 1.0 / E[r], zr = za[r];
+      for (int q = q0; q < q1; q += CK) {
+        int2 ej[CK];
+        double av[CK];
+#pragma unroll
+        for (int k = 0; k < CK; ++k) ej[k] = ec[min(q + k, q1 - 1)];  // the row's entries and columns belong to node i
+#pragma unroll
+        for (int k = 0; k < CK; ++k) av[k] = As[ej[k].x];
+#pragma unroll
+        for (int k = 0; k < CK; ++k)
+          if (q + k < q1) ax += av[k] * xl[ej[k].y - nd.x_off];
       }
-      const double ei = 1.0 / E[r];
-      v[0] = fmax(v[0], fabs(ei * (ax - za[r])));
-      v[1] = fmax(v[1], fabs(ei * za[r]));
+      v[0] = fmax(v[0], fabs(ei * (ax - zr)));
+      v[1] = fmax(v[1], fabs(ei * zr));
       v[2] = fmax(v[2], fabs(ei * ax));
     }
   }
@@ -542,17 +548,25 @@ __global__ __launch_bounds__(64) void k_check_part(PlDev d, int N, int n, int m,
     const int2* __restrict__ er = d.gc_er;
     for (int lc = tid; lc < nw; lc += 64) {
       double aty = 0.0;
-      const int q1 = cp[lc + 1];
-#pragma unroll 4
-      for (int q = cp[lc]; q < q1; ++q) {
-        const int2 e = er[q];  // own-node entries first, then node i-1's (dx_i columns)
-        const int le = e.x - nd.ent_off;
-        aty += le >= 0 ? Al[le] * yl[e.y - nd.row_off] : As[e.x] * ya[e.y];
-      }
-      const double di = 1.0 / D[lc];
+      const int q0 = cp[lc], q1 = cp[lc + 1];
+      const double di = 1.0 / D[lc], qc = qs[lc];
       const double px = Ps[lc] * xl[lc];
-      v[3] = fmax(v[3], fabs(di * (px + qs[lc] + aty)));
-      v[4] = fmax(v[4], fabs(di * qs[lc]));
+      for (int q = q0; q < q1; q += CK) {
+        int2 e[CK];
+        double av[CK], yv[CK];
+#pragma unroll
+        for (int k = 0; k < CK; ++k) e[k] = er[min(q + k, q1 - 1)];  // own-node entries first, then node i-1's
+#pragma unroll
+        for (int k = 0; k < CK; ++k) {
+          av[k] = As[e[k].x];
+          yv[k] = ya[e[k].y];
+        }
+#pragma unroll
+        for (int k = 0; k < CK; ++k)
+          if (q + k < q1) aty += av[k] * yv[k];
+      }
+      v[3] = fmax(v[3], fabs(di * (px + qc + aty)));
+      v[4] = fmax(v[4], fabs(di * qc));
       v[5] = fmax(v[5], fabs(di * aty));
       v[6] = fmax(v[6], fabs(di * px));
     }
@@ -696,7 +710,7 @@ __global__ __launch_bounds__(CHECK_NT) void k_check(PlDev d, int N, int n, int m
 void launch_check(PlOcpHandle* h, int it, int final_check) {
   (void)it;
   {
-    const int lds = ((2 * h->ncol_max + 1) & ~1) + ((h->nrow_max + 1) & ~1);
+    const int lds = (2 * h->ncol_max + 1) & ~1;
     hipLaunchKernelGGL(k_check_part, dim3(h->B * (h->N + 1)), dim3(64), lds * 8, h->stream, h->d, h->N, h->n, h->m,
                        h->nnz, h->ndx);
   }
