@@ -14,7 +14,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.normpath(os.path.join(HERE, "..", "csrc"))
 LIB = os.path.join(HERE, "libpinoloco.so")
-SOURCES = ["api.hip", "k_eval.hip", "k_qp.hip", "k_admm.hip", "k_factor.hip", "k_dyn.hip", "k_admm2.hip", "k_ip.hip", "k_admm_rc.hip", "k_hess.hip"]
+SOURCES = ["api.hip", "api_build.hip", "api_casadi.hip", "k_eval.hip", "k_qp.hip", "k_admm.hip", "k_factor.hip", "k_dyn.hip", "k_admm2.hip", "k_ip.hip", "k_admm_rc.hip", "k_hess.hip"]
 ARCH = os.environ.get("PL_OFFLOAD_ARCH", "gfx950")
 
 
