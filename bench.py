@@ -304,7 +304,7 @@ def main():
                        "solver": ("osqp-sqp (1 SQP iteration, max_iter 100)" if args.solver == "osqp" else
                                   "fatrop-equivalent interior point (max_iter 10, tol 1e-3, mu_init 1e-4)"),
                        "parallelism": f"batch-sharded dp{world}"},
-            "roofline": {"bound": "hbm", "kernel": "k_admm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": {"sweep": "k_admm", "sweep2": "k_admm2", "chain": "k_admm_rc"}[bo.admm_kernel()], "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": per_launch_bytes,
                          "bytes_per_problem_iter": bytes_it, "bytes_per_problem_iter_padded": bytes_it_padded,

@@ -207,7 +207,10 @@ int pl_ocp_get_step(pl_ocp* o, double* dx);
  * x_state [batch][nx] = x_init, t0 [batch] = gait time offset. */
 int pl_mpc_setup(pl_ocp* o, const double* x_state, const double* t0);
 /* One MPC step k: gait schedule at t0 + k*dt_min, x_init, warm start, solve,
- * x_state <- integrate(x_state, DX[1]).  No host transfers. */
+ * x_state <- integrate(x_state, DX[1]).  No host transfers.  With the OSQP solver and
+ * profiling off, the launches after the gait / warm-start kernel are replayed from a HIP
+ * graph captured on the second step with unchanged handle settings (bit-identical to
+ * launching them; PL_MPC_GRAPH=0 at creation launches them one by one). */
 int pl_mpc_step(pl_ocp* o, int k);
 int pl_mpc_get_state(pl_ocp* o, double* x_state);
 /* Solver stats of the last MPC step's (last) SQP iteration, as pl_ocp_solve reports. */
