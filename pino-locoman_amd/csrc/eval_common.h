@@ -8,19 +8,21 @@
 // One workgroup per problem.  f is written to work[b * 8 + 0].
 template <bool kGrad>
 __device__ inline double objective_wg(const PlDev& d, int b, int N, int n, int np, const double* x, const double* step,
-                               double alpha, double* grad) {
+                               double alpha, double* grad, double* red) {  // red: >= 256 doubles of LDS
   const PlOcpConst& O = *d.oc;
   const PlModel& M = *d.model;
   const double* p = d.p + (size_t)b * np;
   __shared__ double dxd[2 * PL_MAXV];
-  __shared__ double red[256];
   if (threadIdx.x == 0) pl::compute_dx_des(M, O, p, dxd);
   __syncthreads();
   const int ndx = O.ndx;
   const double* Q = p + O.P.Q_diag;
   const double* R = p + O.P.R_diag;
+  // 256 virtual threads (partial vt sums j = vt, vt + 256, ...) and a 256-wide tree, for
+  // any blockDim <= 256: the same summation order, hence the same bits, in every kernel
+  for (int vt = threadIdx.x; vt < 256; vt += blockDim.x) {
   double acc = 0.0;
-  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+  for (int j = vt; j < n; j += 256) {
     const int i = d.colnode[j];
     const int lc = j - d.nodes[i].x_off;
     const double xj = step ? x[j] + alpha * step[j] : x[j];
@@ -44,10 +46,11 @@ __device__ inline double objective_wg(const PlDev& d, int b, int N, int n, int n
     }
     if (kGrad) grad[j] = gj;
   }
-  red[threadIdx.x] = acc;
+  red[vt] = acc;
+  }
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+  for (int s = 128; s > 0; s >>= 1) {
+    for (int u = threadIdx.x; u < s; u += blockDim.x) red[u] += red[u + s];
     __syncthreads();
   }
   double f = red[0];
@@ -56,17 +59,29 @@ __device__ inline double objective_wg(const PlDev& d, int b, int N, int n, int n
 }
 
 
-__device__ inline void block_sum_max(double& s, double& mx, double* red) {
-  red[threadIdx.x] = s;
-  red[256 + threadIdx.x] = mx;
+// Sum of red[0..256) into red[0] and max of red[256..512) into red[256] over a fixed
+// 256-wide tree, whatever blockDim (<= 256) does the work.
+__device__ inline void block_tree_256(double* red) {
   __syncthreads();
-  for (int k = blockDim.x / 2; k > 0; k >>= 1) {
-    if (threadIdx.x < k) {
-      red[threadIdx.x] += red[threadIdx.x + k];
-      red[256 + threadIdx.x] = fmax(red[256 + threadIdx.x], red[256 + threadIdx.x + k]);
+  for (int k = 128; k > 0; k >>= 1) {
+    for (int u = threadIdx.x; u < k; u += blockDim.x) {
+      red[u] += red[u + k];
+      red[256 + u] = fmax(red[256 + u], red[256 + u + k]);
     }
     __syncthreads();
   }
+}
+
+__device__ inline void block_sum_max(double& s, double& mx, double* red) {
+  // 256 partials (threads past blockDim contribute 0: the sums and the non-negative
+  // maxima reduced here keep their 256-thread bits for any blockDim <= 256)
+  red[threadIdx.x] = s;
+  red[256 + threadIdx.x] = mx;
+  for (int u = blockDim.x + threadIdx.x; u < 256; u += blockDim.x) {
+    red[u] = 0.0;
+    red[256 + u] = 0.0;
+  }
+  block_tree_256(red);
   s = red[0];
   mx = red[256];
   __syncthreads();

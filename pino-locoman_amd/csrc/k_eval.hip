@@ -136,7 +136,8 @@ void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz, int jl_len) {
 
 __global__ __launch_bounds__(256) void k_objective(PlDev d, int N, int n, int np) {
   const int b = blockIdx.x;
-  double f = objective_wg<true>(d, b, N, n, np, d.x + (size_t)b * n, nullptr, 0.0, d.grad + (size_t)b * n);
+  __shared__ double red[256];
+  double f = objective_wg<true>(d, b, N, n, np, d.x + (size_t)b * n, nullptr, 0.0, d.grad + (size_t)b * n, red);
   if (threadIdx.x == 0) d.work[(size_t)b * 8 + 0] = f;
 }
 
@@ -213,11 +214,10 @@ struct ViolEmit {
 
 template <int DYN>
 __device__ void violation_at(const PlDev& d, int b, int N, int n, int np, const double* x, const double* step,
-                             double alpha, double* red, double* metric, double* vmax) {
+                             double alpha, double* kst, double* red, double* metric, double* vmax) {
   const PlOcpConst& O = *d.oc;
   const PlModel& M = *d.model;
   ViolEmit e{0.0, 0.0};
-  __shared__ double kst[PL_KIN_STORE * 64];
   for (int i = threadIdx.x; threadIdx.x < 64 && i < N; i += 64) {  // nodes on the first wave
     const PlNode nd = d.nodes[i];
     const PlNode nn = d.nodes[i + 1];
@@ -233,10 +233,17 @@ __device__ void violation_at(const PlDev& d, int b, int N, int n, int np, const 
 }
 }  // namespace
 
+// One wave per problem: the node rows of the trials run on 64 lanes and the ~350 registers
+// of the row code fit one wave per SIMD, so a 256-thread workgroup (three idle waves)
+// would hold a whole CU per problem.  Every sum keeps its 256-wide order (eval_common.h).
 template <int DYN>
-__global__ __launch_bounds__(256) void k_line_search(PlDev d, int N, int n, int m, int np) {
+__global__ __launch_bounds__(64) void k_line_search(PlDev d, int N, int n, int m, int np) {
   const int b = blockIdx.x;
-  __shared__ double red[512];
+  // the node rows' store; also the reduction buffer once a pass over the rows is done
+  // (one wave, in order), so the workgroup takes 39 KB of LDS and four fit a CU
+  __shared__ double kst[PL_KIN_STORE * 64];
+  static_assert(PL_KIN_STORE * 64 >= 512, "reduction buffer");
+  double* red = kst;
   __shared__ int s_flag;
   double* x = d.x + (size_t)b * n;
   const double* dxs = d.step + (size_t)b * n;
@@ -249,16 +256,21 @@ __global__ __launch_bounds__(256) void k_line_search(PlDev d, int N, int n, int 
   __syncthreads();
   const bool nan_step = s_flag != 0;
   // f, grad_f, g metric at the current x (ocp.py:441-445)
-  double f = objective_wg<false>(d, b, N, n, np, x, nullptr, 0.0, nullptr);
+  double f = objective_wg<false>(d, b, N, n, np, x, nullptr, 0.0, nullptr, red);
   double gm, vmax0;
-  violation_at<DYN>(d, b, N, n, np, x, nullptr, 0.0, red, &gm, &vmax0);
+  violation_at<DYN>(d, b, N, n, np, x, nullptr, 0.0, kst, red, &gm, &vmax0);
   double arm = 0.0;
   {
     const double* gr = d.grad + (size_t)b * n;
-    double s = 0.0, dummy = 0.0;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) s += gr[j] * dxs[j];
-    block_sum_max(s, dummy, red);
-    arm = s;
+    for (int vt = threadIdx.x; vt < 256; vt += blockDim.x) {  // 256 virtual threads (eval_common.h)
+      double s = 0.0;
+      for (int j = vt; j < n; j += 256) s += gr[j] * dxs[j];
+      red[vt] = s;
+      red[256 + vt] = 0.0;
+    }
+    block_tree_256(red);
+    arm = red[0];
+    __syncthreads();
   }
   const double armijo_factor = 1e-4, a_min = 1e-4, a_decay = 0.5, g_max = 1e-3, g_min = 1e-5, gamma = 1e-5;
   double a = 1.0;
@@ -269,8 +281,8 @@ __global__ __launch_bounds__(256) void k_line_search(PlDev d, int N, int n, int 
     trials = 14;
   } else {
     while (!accepted && a > a_min) {
-      new_f = objective_wg<false>(d, b, N, n, np, x, dxs, a, nullptr);
-      violation_at<DYN>(d, b, N, n, np, x, dxs, a, red, &new_gm, &vmax);
+      new_f = objective_wg<false>(d, b, N, n, np, x, dxs, a, nullptr, red);
+      violation_at<DYN>(d, b, N, n, np, x, dxs, a, kst, red, &new_gm, &vmax);
       ++trials;
       if (new_gm > g_max) {
         if (new_gm < (1.0 - gamma) * gm) { accepted = true; branch = 1; }
@@ -300,7 +312,7 @@ __global__ __launch_bounds__(256) void k_line_search(PlDev d, int N, int n, int 
 }
 
 void launch_line_search(PlOcpHandle* h) {
-  PL_DISPATCH_DYN(h->oc.dyn, k_line_search, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->np);
+  PL_DISPATCH_DYN(h->oc.dyn, k_line_search, dim3(h->B), dim3(64), 0, h->stream, h->d, h->N, h->n, h->m, h->np);
 }
 
 // ---------------------------------------------------------------------------

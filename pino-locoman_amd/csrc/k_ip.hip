@@ -572,9 +572,10 @@ __global__ __launch_bounds__(256) void k_ip_step(PlDev d, int N, int n, int m, i
   __syncthreads();
   int t = 0;
   __shared__ double kst[PL_KIN_STORE * 64];
+  __shared__ double ored[256];
   for (t = 0; t < st.ls_max; ++t) {
     const double a = amax * ldexp(1.0, -t);
-    const double ft = objective_wg<false>(d, b, N, n, np, x, dx, a, nullptr);
+    const double ft = objective_wg<false>(d, b, N, n, np, x, dx, a, nullptr, ored);
     TrialEmit e{s, ds, a, 0, 0.0, 0.0};
     if (threadIdx.x < 64) {
       for (int i = threadIdx.x; i < N; i += 64) {
