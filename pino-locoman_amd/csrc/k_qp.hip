@@ -471,11 +471,27 @@ __global__ __launch_bounds__(256) void k_admm_init(PlDev d, int N, int n, int m,
   const double* xa = d.xa + (size_t)b * n;
   const double* qs = d.qs + (size_t)b * n;
   double* rhs = d.rhs + (size_t)b * n;
+  // gathers in chunks of CK entries (index words, then the operands, then the FMAs in
+  // entry order: the same arithmetic as one entry at a time, see k_check_part)
+  constexpr int CK = 8;
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
     double acc = sigma * xa[j] - qs[j];
-    for (int q = d.gc_ptr[j]; q < d.gc_ptr[j + 1]; ++q) {
-      const int2 er = d.gc_er[q];
-      acc += As[er.x] * (rho[er.y] * za[er.y] - ya[er.y]);
+    const int q0 = d.gc_ptr[j], q1 = d.gc_ptr[j + 1];
+    for (int q = q0; q < q1; q += CK) {
+      int2 er[CK];
+      double av[CK], rv[CK], zv[CK], yv[CK];
+#pragma unroll
+      for (int k = 0; k < CK; ++k) er[k] = d.gc_er[min(q + k, q1 - 1)];
+#pragma unroll
+      for (int k = 0; k < CK; ++k) {
+        av[k] = As[er[k].x];
+        rv[k] = rho[er[k].y];
+        zv[k] = za[er[k].y];
+        yv[k] = ya[er[k].y];
+      }
+#pragma unroll
+      for (int k = 0; k < CK; ++k)
+        if (q + k < q1) acc += av[k] * (rv[k] * zv[k] - yv[k]);
     }
     rhs[j] = acc;
   }
