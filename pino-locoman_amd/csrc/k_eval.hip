@@ -335,14 +335,13 @@ __global__ __launch_bounds__(64) void k_mpc_prepare(PlDev d, int k, int N, int n
   if (k == 0) return;
   double* x = d.x + (size_t)b * n;
   const int fo = pl::u_force_off(O);
-  for (int i = 0; i < N; ++i) {
+  for (int idx = threadIdx.x; idx < N * O.nf; idx += blockDim.x) {  // (node, force component) on the lanes
+    const int i = idx / O.nf, c = idx - i * O.nf;
     const int base = d.nodes[i].x_off + O.ndx + fo;
-    for (int c = threadIdx.x; c < O.nf; c += blockDim.x) {
-      int foot = c / 3;
-      double fd = pl::f_des_comp(M, O, p, c);
-      if (foot < 4 && p[O.P.contact + 4 * i + foot] == 0.0) fd = 0.0;
-      x[base + c] = fd;
-    }
+    int foot = c / 3;
+    double fd = pl::f_des_comp(M, O, p, c);
+    if (foot < 4 && p[O.P.contact + 4 * i + foot] == 0.0) fd = 0.0;
+    x[base + c] = fd;
   }
 }
 
