@@ -6,7 +6,9 @@ gait schedule + x_init update, warm start, sqp_data (node evaluation and dual
 Jacobians), OSQP update (Ruiz scaling + block KKT factor), ADMM (<= 100 iterations,
 termination checks every 25), Armijo/filter line search and the state update
 x <- integrate(x, DX[1]) (run_mpc.py:127-143).  Inputs are resident in HBM when
-the timed region starts; nothing crosses PCIe inside it.
+the timed region starts; nothing crosses PCIe inside it.  A second, shorter timed pass
+adds the per-step download of the controller output [u_0, x_state] (the "host_io" object:
+the PCIe-inclusive rate, never `value`).
 
 Multi-GPU: one process per GPU (torchrun), problems [rank*B, (rank+1)*B) with
 seeds from the global problem index (weak scaling, no data-path collective); the
@@ -49,17 +51,26 @@ TRAFFIC_SOURCES = ("pino-locoman_amd/csrc/k_admm.hip", "pino-locoman_amd/csrc/ad
                    "pino-locoman_amd/csrc/state.h")
 
 
-def admm_bytes_per_problem_iter(sz, node_table, padded=False):
-    """Algorithmic HBM bytes of one ADMM iteration of one problem (roofline):
-    the two sweeps read every factor block S_i once each, except S_0 and S_N which the
-    fused turnaround steps read once per iteration; A is read once, and the vectors
-    x, rhs, bt, q (7n) and z, y, l, u, rho (7m) are read / written once.
+def admm_bytes_per_problem_iter(sz, node_table, padded=False, kernel="sweep", ndx=None):
+    """Algorithmic HBM bytes of one ADMM iteration of one problem (roofline),
+    per GPU mapping of the linear solve:
 
-    A factor block is the stored lower triangle nw (nw + 1) / 2 of S_i; padded=True
-    counts the 4x4 lane-tile slots the kernel actually streams (K x 64 lanes x 16)."""
+    * "sweep" (k_admm) and "sweep2" (k_admm2): the two sweeps read every factor block S_i
+      once each, except S_0 and S_N which the fused turnaround steps read once per
+      iteration;
+    * "chain" (k_admm_rc): every S_i once, plus the reduced-chain blocks F_i, F_i^T, G_i
+      (3 ndx^2 doubles) of the N nodes with a successor (k_admm_rc.hip header);
+
+    and for all of them A read once, and the vectors x, rhs, bt, q (7n) and z, y, l, u, rho
+    (7m) read / written once.  A factor block is the stored lower triangle nw (nw + 1) / 2
+    of S_i; padded=True counts the 4x4 lane-tile slots the kernels actually stream
+    (K x 64 lanes x 16)."""
     nw = node_table[:, 0].astype(float)
     blk = node_table[:, 9].astype(float) * 64 * 16 if padded else nw * (nw + 1) / 2
-    return 8.0 * (2 * blk.sum() - blk[0] - blk[-1] + sz["nnz"] + 7 * sz["n"] + 7 * sz["m"])
+    vec = sz["nnz"] + 7 * sz["n"] + 7 * sz["m"]
+    if kernel == "chain":
+        return 8.0 * (blk.sum() + 3.0 * (len(nw) - 1) * float(ndx) ** 2 + vec)
+    return 8.0 * (2 * blk.sum() - blk[0] - blk[-1] + vec)
 
 
 def traffic_source_sha():
@@ -200,7 +211,11 @@ def main():
     ap.add_argument("--solver", default="osqp", choices=["osqp", "fatrop"],
                     help="osqp: the headline SQP + OSQP path; fatrop: the interior-point restatement (no CPU baseline)")
     ap.add_argument("--dry-run", action="store_true", help="gloo plumbing only, no GPU")
+    ap.add_argument("--host-io-steps", type=int, default=None,
+                    help="extra steps timed with the per-step D2H of [u_0, x_state] (default min(steps, 10))")
     args = ap.parse_args()
+    if args.host_io_steps is None:
+        args.host_io_steps = min(args.steps, 10)
 
     world, rank, local_rank = pdist.env_ranks()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -270,16 +285,39 @@ def main():
         torch.cuda.synchronize()
         assert allp.shape[0] == B * world
 
+    host_io = None
+    if args.host_io_steps > 0:
+        # PCIe-inclusive rate (never `value`): each step followed by the D2H of the per-problem
+        # controller output [u_0, x_state] into host memory and a wait for it, as a real-time
+        # loop reads it (run_mpc.py:138-141); SURVEY 8(d)
+        buf = np.zeros((B, lay.nu[0] + lay.nx))
+        k0 = args.warmup + 2 * args.steps
+        barrier_sync()
+        t1 = time.perf_counter()
+        for k in range(k0, k0 + args.host_io_steps):
+            bo.mpc_step(k)
+            bo.mpc_download(buf)
+        barrier_sync()
+        e1 = pdist.max_over_ranks(time.perf_counter() - t1, dist)
+        assert np.all(np.isfinite(buf))
+        host_io = {"value": B * world * args.host_io_steps / e1, "unit": "solves/s",
+                   "ms_per_step": e1 / args.host_io_steps * 1e3, "steps": args.host_io_steps,
+                   "d2h_bytes_per_step": int(buf.nbytes),
+                   "what": "per step: pl_mpc_step + pl_mpc_download ([u_0, x_state] of every problem to "
+                           "host memory) + wait; inputs resident, the state stays on the device"}
+
+    kernel = bo.admm_kernel()
+    kname = {"sweep": "k_admm", "sweep2": "k_admm2", "chain": "k_admm_rc"}[kernel]
     sz = bo.sizes()
     ntab = bo.node_table()
-    bytes_it = admm_bytes_per_problem_iter(sz, ntab)
-    bytes_it_padded = admm_bytes_per_problem_iter(sz, ntab, padded=True)
+    bytes_it = admm_bytes_per_problem_iter(sz, ntab, kernel=kernel, ndx=lay.ndx)
+    bytes_it_padded = admm_bytes_per_problem_iter(sz, ntab, padded=True, kernel=kernel, ndx=lay.ndx)
     iters_per_launch = prof["problem_iters"] / max(1, prof["launches"])
     per_launch_bytes = bytes_it * iters_per_launch
     avg_launch_s = prof["admm_ms"] / max(1, prof["launches"]) / 1e3
     achieved = per_launch_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     workload = f"{args.robot} {args.dynamics} N={args.nodes} MPC step"
-    tj = measured_traffic(B, args.nodes, workload)
+    tj = measured_traffic(B, args.nodes, workload) if kernel == "sweep" else None
     # PMC bytes per problem-iteration x this run's problem-iterations per launch
     traffic = tj["bytes_per_problem_iter"] * iters_per_launch if tj else None
 
@@ -304,7 +342,8 @@ def main():
                        "solver": ("osqp-sqp (1 SQP iteration, max_iter 100)" if args.solver == "osqp" else
                                   "fatrop-equivalent interior point (max_iter 10, tol 1e-3, mu_init 1e-4)"),
                        "parallelism": f"batch-sharded dp{world}"},
-            "roofline": {"bound": "hbm", "kernel": {"sweep": "k_admm", "sweep2": "k_admm2", "chain": "k_admm_rc"}[bo.admm_kernel()], "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": kname, "byte_model": kernel, "achieved": achieved,
+                         "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": per_launch_bytes,
                          "bytes_per_problem_iter": bytes_it, "bytes_per_problem_iter_padded": bytes_it_padded,
@@ -313,6 +352,8 @@ def main():
                          "traffic_source": (f"profiles/traffic/admm_traffic.json (k_admm src {tj['src_sha']})"
                                             if tj else None)},
         }
+        if host_io is not None:
+            out["host_io"] = host_io
         if base is not None:
             out["cpu_baseline"] = base
         if args.solver == "fatrop":

@@ -218,6 +218,14 @@ int pl_mpc_get_stats(pl_ocp* o, pl_stats* stats);
 /* Copy the first control input row u_0 [batch][nu_0] and x_state into a
  * caller-owned DEVICE buffer (for collectives): layout [batch][nu_0 + nx]. */
 int pl_mpc_export(pl_ocp* o, void* device_dst);
+/* The same rows [batch][nu_0 + nx] into caller-owned HOST memory, through a pinned staging
+ * buffer of the handle; returns after the copy landed (the per-step controller output
+ * run_mpc.py:138-141 reads: u_0 and the next state).  bench.py times it beside the step
+ * for the PCIe-inclusive rate. */
+int pl_mpc_download(pl_ocp* o, double* host_dst);
+/* MPC-step HIP graph state: out[0] captures, out[1] graph launches, out[2] = 1 when the
+ * step fell back to eager launches (a capture or replay failed, or PL_MPC_GRAPH=0). */
+int pl_mpc_graph_info(const pl_ocp* o, long long* out);
 int pl_ocp_sync(pl_ocp* o);
 
 /* Host-side state maps, x = [q, v], dx = [dq, dv]

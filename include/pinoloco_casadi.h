@@ -15,8 +15,11 @@
  * [nrow, ncol, colind[ncol+1], row[nnz]]), so ca.external("sqp_data", <libpinoloco.so>)
  * works unchanged once pl_casadi_bind() (include/pinoloco.h) has bound the OCP.
  * Evaluations run on the bound handle's GPU (problem slot 0); J_g is in CasADi CCS order
- * over the library's structural pattern (a superset of the symbolic one: extra entries
- * evaluate to 0).  Return value 0 = success.
+ * over the structural-dependency pattern of jacobian(g, x) -- the library's entries that
+ * are non-zero at a generic point (one dual-number probe per node type at bind time) --
+ * so the reference's A pattern from J_g.sparsity() (optimization/ocp.py:305-306) and the
+ * J_g.nonzeros() it feeds OSQP (ocp.py:391) have the same length and order: swapping in
+ * ca.external is the one-line change of ocp.py:299-302.  Return value 0 = success.
  */
 #ifndef PINOLOCO_CASADI_H
 #define PINOLOCO_CASADI_H

@@ -95,18 +95,27 @@ extern "C" int pl_casadi_bind(pl_ocp* o, int retract_steps) {
   c.sp_m1 = dense_sp(h.m, 1);
   c.sp_11 = dense_sp(1, 1);
   c.sp_xinit = dense_sp(h.nx, 1);
-  // J_g: compressed columns of the library pattern
+  // J_g: compressed columns of the structural-dependency pattern, the one CasADi's symbolic
+  // J_g = jacobian(g, x) reports (ocp.py:283) and the reference sets OSQP's A up with
+  // (ocp.py:305-306): the library's entries that are non-zero at a generic point
+  // (jac_pattern, one dual probe per node type).  The library's own pattern (a superset:
+  // kinematic dependencies, e.g. the base position columns RNEA never reads) stays internal.
   struct T { int col, row, e; };
   std::vector<T> t;
   t.reserve(h.nnz);
+  std::vector<uint8_t> pat[3];
   for (int i = 0; i < h.N; ++i) {
     const PlNode& nd = o->nodes[i];
     const PlNode& nn = o->nodes[i + 1];
     const int* cp = o->colptr.data() + nd.colptr_off;
+    const int type = pl::node_type(h.oc, i);
+    if (pat[type].empty()) jac_pattern(h, o->nodes, i, pat[type]);
     for (int lc = 0; lc < nd.ncol; ++lc)
       for (int e = cp[lc]; e < cp[lc + 1]; ++e) {
+        const int r = o->rowidx[nd.ent_off + e];
+        if (!pat[type][(size_t)lc * nd.nrow + r]) continue;
         const int col = lc < nd.nw ? nd.x_off + lc : nn.x_off + (lc - nd.nw);
-        t.push_back({col, nd.row_off + o->rowidx[nd.ent_off + e], nd.ent_off + e});
+        t.push_back({col, nd.row_off + r, nd.ent_off + e});
       }
   }
   std::sort(t.begin(), t.end(), [](const T& a, const T& b) { return a.col != b.col ? a.col < b.col : a.row < b.row; });

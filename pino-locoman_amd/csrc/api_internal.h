@@ -41,6 +41,9 @@ struct pl_ocp {
   std::vector<unsigned char> mpc_key;  // bytes of `h` the graph was captured with (or last seen)
   int mpc_graph_off = 0;               // 1: capture failed or PL_MPC_GRAPH=0: launch eagerly
   long long mpc_captures = 0;
+  long long mpc_replays = 0;           // graph launches (pl_mpc_graph_info)
+  void* dl_host = nullptr;             // pinned staging of pl_mpc_download
+  size_t dl_bytes = 0;
 };
 
 template <class T>
@@ -73,3 +76,4 @@ int build_factor_prog(pl_ocp* o);
 int build_jac_list(pl_ocp* o, std::vector<int2>& list);
 // api_casadi.hip: drop the CasADi binding of an OCP that is being destroyed
 void cas_forget(const pl_ocp* o);
+void jac_pattern(const PlOcpHandle& h, const std::vector<PlNode>& nodes, int i, std::vector<uint8_t>& nz);

@@ -166,6 +166,7 @@ struct PlDev {
   int* gc_ptr;       // global CSC of A: column j's (entry, row) pairs at gc_er[gc_ptr[j] ..)
   int2* gc_er;
   uint32_t* erc;         // (global row << 16 | global column) of each entry, for k_ruiz_fused (n, m < 65536)
+  uint32_t* erl;         // (local row << 16 | local column) of each entry in its node (k_check_part)
   PlAdmmNode* anodes;    // N + 1 node tables (ADMM and factor programs)
   uint16_t* aprog;       // distinct ADMM programs, concatenated
   uint16_t* fprog;       // distinct factor programs, concatenated

@@ -399,6 +399,18 @@ class BatchedOCP:
     def mpc_export(self, device_ptr):
         _lib.check(_lib.lib().pl_mpc_export(self.h, C.c_void_p(device_ptr)))
 
+    def mpc_download(self, out=None):
+        """[u_0, x_state] per problem into host memory ([batch][nu_0 + nx]); returns after the copy."""
+        if out is None:
+            out = np.zeros((self.batch, self.layout.nu[0] + self.layout.nx))
+        _lib.check(_lib.lib().pl_mpc_download(self.h, _lib.dptr(out)))
+        return out
+
+    def mpc_graph_info(self):
+        out = (C.c_longlong * 3)()
+        _lib.check(_lib.lib().pl_mpc_graph_info(self.h, out))
+        return {"captures": int(out[0]), "replays": int(out[1]), "eager_fallback": int(out[2])}
+
     def sync(self):
         _lib.check(_lib.lib().pl_ocp_sync(self.h))
 

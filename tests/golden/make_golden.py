@@ -40,9 +40,9 @@ SYN8 = [("syn", k) for k in range(8)]
 SQP_CONFIGS = [
     ("go2_rnea_n20", "go2", "whole_body_rnea", 20, SYN8, 4, "trot", {}, 2),
     ("go2_cv_n20", "go2", "centroidal_vel", 20, SYN8, 4, "trot", {}, 2),
-    ("b2_aba_n40", "b2", "whole_body_aba", 40, SYN8, 1, "trot", {}, 2),
-    ("b2g_acc_n50", "b2g", "whole_body_acc", 50, SYN8, 1, "trot", {}, 1),
-    ("b2g_rnea_n50", "b2g", "whole_body_rnea", 50, SYN8, 1, "trot", {}, 1),
+    ("b2_aba_n40", "b2", "whole_body_aba", 40, SYN8, 4, "trot", {}, 2),
+    ("b2g_acc_n50", "b2g", "whole_body_acc", 50, SYN8, 4, "trot", {}, 1),
+    ("b2g_rnea_n50", "b2g", "whole_body_rnea", 50, SYN8, 4, "trot", {}, 1),
     # edge cases of the reference's own code paths (reference settings)
     ("go2_rnea_n20_walk", "go2", "whole_body_rnea", 20, [("syn", 20), ("syn", 21), ("yaw", 22, 170.0)], 4, "walk",
      {}, 0),

@@ -5,19 +5,19 @@ waves per problem) and "chain" (k_admm_rc: the reduced-chain form, one workgroup
 problem) run the same OSQP 0.6 iteration (osqp.solve(), optimization/ocp.py:401) on the
 same block factor; they differ only in summation order.  Bars:
 
-* every golden fixture with the chain kernel: the bars of test_gpu.py (solver outcome
-  exact, dx / new iterate <= step_tol -- 1e-9 but for two named edge fixtures --,
-  violation metric <= 1e-10 at the returned point);
+* every golden fixture with every kernel forced, and the device MPC loops with the sweep
+  and chain kernels: test_gpu.py (test_sqp_step_matches_golden,
+  test_device_mpc_loop_matches_oracle_loop, test_device_mpc_loop_inside_benchmark_batch);
 * the kernels against each other on the BASELINE fixtures: outcome exact, dx <= 1e-9;
 * chain-kernel batch invariance and repeatability: bit-exact (a problem gives the same bits
   in any batch that runs this kernel; across kernels the order of the sums differs);
-* the device MPC loop and the interior-point branch with the chain kernel.
+* the interior-point branch with the chain kernel.
 """
 import numpy as np
 import pytest
 
 from conftest import golden, make_robot
-from test_gpu import ACCF, CONFIGS, EDGE, FD, _batched, _kw, _rel, step_tol
+from test_gpu import CONFIGS, _batched, _rel
 
 pytestmark = pytest.mark.gpu
 
@@ -31,46 +31,6 @@ def _solve(name, rname, dyn, N, kernel, B=None):
     out = (st, bo.get_step(), bo.get_x())
     bo.close()
     return G, R, out
-
-
-@pytest.mark.parametrize("name,rname,dyn,N", CONFIGS + EDGE + ACCF)
-def test_chain_sqp_step_matches_golden(name, rname, dyn, N):
-    from oracle.ocp import OracleOCP
-    G, R, (st, dx, xn) = _solve(name, rname, dyn, N, "chain")
-    o = OracleOCP(R, dyn, N, include_base=bool(int(G["include_base"])) if "include_base" in G else True)
-    for b in range(G["P"].shape[0]):
-        assert st["status"][b] == G["status"][b], b
-        assert st["admm_iters"][b] == G["iters"][b], b
-        assert st["ls_accepted"][b] == G["accepted"][b], b
-        assert st["ls_branch"][b] == G["branch"][b], b
-        assert st["ls_trials"][b] == G["trials"][b], b
-        assert st["ls_alpha"][b] == G["alpha"][b], b
-        if np.all(np.isnan(G["dx"][b])):
-            assert np.all(np.isnan(dx[b])) and np.array_equal(xn[b], G["X"][b])
-        else:
-            assert _rel(dx[b], G["dx"][b]) < step_tol(name), b
-        assert _rel(xn[b], G["x_new"][b]) < step_tol(name), b
-        g, l, u = o.eval_g(xn[b], G["P"][b])
-        assert st["viol_max"][b] == pytest.approx(o.violation_max(g, l, u), rel=1e-10, abs=1e-14), b
-
-
-@pytest.mark.parametrize("name,rname,dyn,N", FD)
-@pytest.mark.parametrize("kernel", ["sweep", "sweep2"])
-def test_general_coupling_sweeps_match_golden(name, rname, dyn, N, kernel):
-    """whole_body_rnea include_acc=False: the RNEA rows of node i read dv_{i+1}, so the
-    factor takes the general coupling program (E_{i+1} = Wc^T Z Wc) and the sweeps the
-    coupling lists with several entries per dx_{i+1} column; the test_gpu.py bars."""
-    from oracle.ocp import OracleOCP
-    G, R, (st, dx, xn) = _solve(name, rname, dyn, N, kernel)
-    o = OracleOCP(R, dyn, N, **_kw(G))
-    for b in range(G["P"].shape[0]):
-        for key, gk in (("status", "status"), ("admm_iters", "iters"), ("ls_branch", "branch"),
-                        ("ls_trials", "trials"), ("ls_alpha", "alpha")):
-            assert st[key][b] == G[gk][b], (key, b)
-        assert _rel(dx[b], G["dx"][b]) < step_tol(name), b
-        assert _rel(xn[b], G["x_new"][b]) < step_tol(name), b
-        g, l, u = o.eval_g(xn[b], G["P"][b])
-        assert st["viol_max"][b] == pytest.approx(o.violation_max(g, l, u), rel=1e-10, abs=1e-14), b
 
 
 def test_general_coupling_refuses_chain_kernel():
@@ -151,21 +111,6 @@ def test_auto_kernel_choice():
         bo = BatchedOCP(R, "whole_body_aba", 10, batch=B, device=0)
         assert bo.admm_kernel() == want, (B, bo.admm_kernel())
         bo.close()
-
-
-@pytest.mark.parametrize("name,rname,dyn,N", [CONFIGS[0], CONFIGS[1], EDGE[0]])
-def test_chain_device_mpc_loop(name, rname, dyn, N):
-    G = golden(f"sqp_{name}.npz")
-    R, bo = _batched(rname, dyn, N, G, B=1)
-    bo.set_admm_kernel("chain")
-    bo.mpc_setup(G["XS"][:1], G["T0"][:1])
-    for k, want in enumerate(G["loop_states"]):
-        bo.mpc_step(k)
-        assert _rel(bo.mpc_state()[0], want) < 1e-7, k
-        st = bo.mpc_stats()
-        assert [st["status"][0], st["admm_iters"][0], st["ls_branch"][0], st["ls_trials"][0]] == \
-            G["loop_stats"][k].tolist(), k
-    bo.close()
 
 
 def test_chain_interior_point_agrees_with_sweep():

@@ -108,14 +108,25 @@ def test_eval_sqp_data_matches_golden(name, rname, dyn, N):
     bo.close()
 
 
-@pytest.mark.parametrize("name,rname,dyn,N", CONFIGS + EDGE + ACCF + FD)
-def test_sqp_step_matches_golden(name, rname, dyn, N):
-    """One SQP iteration per problem: solver outcome exact, step <= step_tol; the max
-    violation at the returned point <= 1e-10 against the oracle's metric at the same
-    point (and <= 1e-6 against the golden value, which sits at the oracle's own x)."""
+# The GPU mappings of the ADMM linear solve (pl_ocp_set_admm_kernel): "sweep" (k_admm, the
+# kernel bench.py times at B = 1024), "sweep2" (k_admm2) and "chain" (k_admm_rc, AUTO's choice
+# at the fixtures' batch sizes).  Every fixture runs through each of them; the chain kernel
+# refuses the general coupling of include_acc=False (test_admm_kernels.py).
+KERNELS = ("sweep", "sweep2", "chain")
+STEP_CASES = [pytest.param(*c, k, id=f"{c[0]}-{k}") for c in CONFIGS + EDGE + ACCF + FD for k in KERNELS
+              if not (k == "chain" and c in FD)]
+
+
+@pytest.mark.parametrize("name,rname,dyn,N,kernel", STEP_CASES)
+def test_sqp_step_matches_golden(name, rname, dyn, N, kernel):
+    """One SQP iteration per problem with the ADMM kernel forced: solver outcome exact, step
+    <= step_tol; the max violation at the returned point <= 1e-10 against the oracle's metric
+    at the same point (and <= 1e-6 against the golden value, which sits at the oracle's own x)."""
     from oracle.ocp import OracleOCP
     G = golden(f"sqp_{name}.npz")
     R, bo = _batched(rname, dyn, N, G)
+    bo.set_admm_kernel(kernel)
+    assert bo.admm_kernel() == kernel
     st = bo.solve()
     dx = bo.get_step()
     xn = bo.get_x()
@@ -159,22 +170,64 @@ def test_fixture_coverage():
     assert gaits == {"trot", "walk", "stand"} and trace > 0
 
 
-@pytest.mark.parametrize("name,rname,dyn,N", [CONFIGS[0], CONFIGS[1], EDGE[0], EDGE[1], EDGE[4], ACCF[0], ACCF[1],
-                                               ACCF[5], ACCF[6], FD[0]])
-def test_device_mpc_loop_matches_oracle_loop(name, rname, dyn, N):
-    """run_mpc.py:127-143 executed on the device (gait, x_init, warm start, solve,
-    x <- integrate(x, DX[1])) vs the oracle's closed loop in the golden file: states
-    <= 1e-7 and each step's solver outcome (status, ADMM iterations, branch, trials)."""
-    G = golden(f"sqp_{name}.npz")
-    R, bo = _batched(rname, dyn, N, G, B=1)
-    bo.mpc_setup(G["XS"][:1], G["T0"][:1])
+LOOP_FIXTURES = [CONFIGS[0], CONFIGS[1], CONFIGS[2], CONFIGS[3], CONFIGS[4], EDGE[0], EDGE[1], EDGE[4], ACCF[0],
+                 ACCF[1], ACCF[5], ACCF[6], FD[0]]
+LOOP_CASES = [pytest.param(*c, k, id=f"{c[0]}-{k}") for c in LOOP_FIXTURES for k in ("sweep", "chain")
+              if not (k == "chain" and c in FD)]
+
+
+def _check_loop(bo, G, b=0):
+    """Run the fixture's closed loop on problem b of the handle's batch: states <= 1e-7 and
+    each step's solver outcome (status, ADMM iterations, branch, trials) exact."""
     for k, want in enumerate(G["loop_states"]):
         bo.mpc_step(k)
-        got = bo.mpc_state()[0]
+        got = bo.mpc_state()[b]
         assert _rel(got, want) < 1e-7, k
         st = bo.mpc_stats()
-        assert [st["status"][0], st["admm_iters"][0], st["ls_branch"][0], st["ls_trials"][0]] == \
+        assert [st["status"][b], st["admm_iters"][b], st["ls_branch"][b], st["ls_trials"][b]] == \
             G["loop_stats"][k].tolist(), k
+    return st
+
+
+@pytest.mark.parametrize("name,rname,dyn,N,kernel", LOOP_CASES)
+def test_device_mpc_loop_matches_oracle_loop(name, rname, dyn, N, kernel):
+    """run_mpc.py:127-143 executed on the device (gait, x_init, warm start, solve,
+    x <- integrate(x, DX[1])) vs the oracle's closed loop in the golden file, with the ADMM
+    kernel forced: states <= 1e-7 and each step's solver outcome exact."""
+    G = golden(f"sqp_{name}.npz")
+    assert G["loop_states"].shape[0] >= 3, name
+    R, bo = _batched(rname, dyn, N, G, B=1)
+    bo.set_admm_kernel(kernel)
+    bo.mpc_setup(G["XS"][:1], G["T0"][:1])
+    _check_loop(bo, G)
+    bo.close()
+
+
+@pytest.mark.parametrize("name,rname,dyn,N,B", [("b2g_rnea_n50", "b2g", "whole_body_rnea", 50, 1024),
+                                               ("b2g_acc_n50", "b2g", "whole_body_acc", 50, 1024),
+                                               ("b2_aba_n40", "b2", "whole_body_aba", 40, 256)])
+def test_device_mpc_loop_inside_benchmark_batch(name, rname, dyn, N, B):
+    """The loop exactly as bench.py drives it: the BASELINE config's batch (synthetic problems
+    0..B-1, problem 0 = the fixture's problem 0), set_x / init_solver / mpc_setup, then
+    pl_mpc_step with AUTO's ADMM kernel for that batch (k_admm at 1024, k_admm_rc at 256) and
+    the HIP-graph replay; problem 0 follows the oracle's closed loop (states <= 1e-7, outcome
+    exact), and every problem of the batch ends finite with an OSQP status in {1, 2, -2}."""
+    from pinoloco.ocp import BatchedOCP
+    from pinoloco.synthetic import build_batch
+    G = golden(f"sqp_{name}.npz")
+    R = make_robot(rname)
+    lay, P, X, XS, T0 = build_batch(R, dyn, N, B, 0)
+    assert np.array_equal(P[0], G["P"][0]) and np.array_equal(X[0], G["X"][0])
+    assert np.array_equal(XS[0], G["XS"][0]) and T0[0] == G["T0"][0]
+    bo = BatchedOCP(R, dyn, N, batch=B, device=0, gait_type="trot", gait_period=0.8)
+    assert bo.admm_kernel() == ("sweep" if B >= 1024 else "chain")
+    bo.set_params(P)
+    bo.set_x(X)
+    bo.init_solver()
+    bo.mpc_setup(XS, T0)
+    st = _check_loop(bo, G)
+    assert np.all(np.isfinite(bo.mpc_state()))
+    assert set(np.unique(st["status"])) <= {1, 2, -2}
     bo.close()
 
 
@@ -423,6 +476,16 @@ def test_casadi_external_functions_match_golden():
     assert np.array_equal(lbg.ravel(), G["lbg"][0]) and np.array_equal(ubg.ravel(), G["ubg"][0])
     Jg = sp.csr_matrix((G["J_data_0"], G["J_indices_0"], G["J_indptr_0"]), shape=J.shape)
     assert abs(J - Jg).max() <= 1e-12 * abs(Jg).max()
+    # the reference's OSQP setup (ocp.py:305-306, 391): A's pattern from J_g.sparsity(), its
+    # values from J_g.nonzeros() -- equal lengths, same order (CasADi compressed columns)
+    sp_J = casadi_ext.ExternalFunction("sqp_data").sp_out[1]
+    A_rows = sp_J[3]
+    assert J.nnz == len(A_rows) == len(J.data) and np.array_equal(J.indices, A_rows)
+    # the library's internal pattern is wider; its extra entries are 0 at this point (to round-off)
+    _, Jlib, _, _, _ = bo.eval_sqp_data()
+    rows, cols = bo.pattern()
+    inside = np.asarray(sp.csc_matrix((np.ones(len(A_rows)), A_rows, sp_J[2]), shape=J.shape)[rows, cols]).ravel() > 0
+    assert (~inside).sum() > 0 and np.abs(Jlib[0][~inside]).max() <= 1e-14 * np.abs(Jlib[0]).max()
     f, grad2 = casadi_ext.ExternalFunction("f_data")(x, p)
     assert float(f[0, 0]) == pytest.approx(float(G["f"][0]), rel=1e-12)
     assert np.array_equal(grad2, grad)

@@ -1,7 +1,8 @@
 """MPC-step graph replay (pl_mpc_step, api.hip): the OSQP-SQP launches of a step are
 captured once into a HIP graph and replayed.  A replay must be the eager launch sequence:
 states, iterates and solver statistics bit-identical to a handle created with
-PL_MPC_GRAPH=0, including across a setter that changes the handle mid-loop (re-capture)."""
+PL_MPC_GRAPH=0, including across a setter that changes the handle mid-loop (re-capture), and the capture /
+replay counters (pl_mpc_graph_info) show that the graph path ran."""
 import os
 
 import numpy as np
@@ -38,8 +39,9 @@ def _loop(R, dyn, N, B, steps, graph, switch_at=None):
         st = bo.mpc_stats()
         stats.append({key: np.array(v).copy() for key, v in st.items()})
     x = bo.get_x().copy()
+    info = bo.mpc_graph_info()
     bo.close()
-    return states, stats, x
+    return states, stats, x, info
 
 
 @pytest.mark.parametrize("rname,dyn,N,B,switch_at", [
@@ -56,3 +58,11 @@ def test_graph_replay_is_bit_identical_to_eager(rname, dyn, N, B, switch_at):
         for key in eager[1][k]:
             assert np.array_equal(eager[1][k][key], graph[1][k][key], equal_nan=True), (k, key)
     assert np.array_equal(eager[2], graph[2])
+    # the replay path really ran: step 0 eager (first sighting of the handle state), step 1
+    # captures and launches the graph, later steps replay it; set_sqp_iters changes the state,
+    # so that step runs eagerly and the next one captures again
+    assert eager[3] == {"captures": 0, "replays": 0, "eager_fallback": 1}
+    if switch_at is None:
+        assert graph[3] == {"captures": 1, "replays": 5, "eager_fallback": 0}, graph[3]
+    else:
+        assert graph[3] == {"captures": 2, "replays": 6 - 2, "eager_fallback": 0}, graph[3]
