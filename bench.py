@@ -158,6 +158,40 @@ def cpu_baseline(robot, dynamics, N, per_core=4, n_steps=2):
             "omp_num_threads_env": env, "cgroup_cpu_quota": _cgroup_cpu_quota()}
 
 
+def cpu_baseline_ip(robot, dynamics, N, per_core=1, n_steps=1):
+    """The compiled C++ restatement of the interior-point stand-in for the reference's Fatrop
+    branch (oracle/cpu/sqp_cpu.cpp restating oracle/ip_ref.py: exact Lagrangian Hessian by
+    hyper-dual node passes over the structurally non-zero pairs, QDLDL on the IP's
+    quasi-definite KKT, inertia correction, filter line search; OpenMP over problems), same
+    workload and seeds as the GPU run.  Not Fatrop (absent from the image and the reference).
+    Sample: per_core problems per thread x n_steps MPC steps (the first solve of the loop,
+    cold lam_g).  Runs before the GPU is initialised."""
+    sys.path.insert(0, HERE)
+    from oracle.cpu_baseline import CpuOCP  # noqa: E402  (baseline leg only)
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    threads = max(1, min(avail, int(env))) if env else avail
+    R = robots.ROBOTS[robot]()
+    R.set_gait_sequence("trot", 0.8)
+    B = per_core * threads
+    lay, P, X, XS, T0 = build_batch(R, dynamics, N, B, 0)
+    c = CpuOCP(R, dynamics, N, gait_type="trot", gait_period=0.8)
+    pairs = c.hess_pairs()
+    wall, _, st = c.ip_mpc(P, X, XS, T0, n_steps, threads=threads)
+    return {"value": B * n_steps / wall, "unit": "solves/s", "cores": threads, "kind": "port",
+            "sample": f"{B} problems x {n_steps} MPC step(s) of the same workload (seeds 0..{B - 1}, the loop's first "
+                      f"solve: cold lam_g) on {threads} OpenMP threads; compiled C++ restatement of the interior-point "
+                      f"stand-in for the reference's Fatrop branch (oracle/cpu/sqp_cpu.cpp restating oracle/ip_ref.py: "
+                      f"exact Lagrangian Hessian by hyper-dual passes over {pairs} column pairs, QDLDL LDL^T on the "
+                      f"KKT, IPOPT inertia correction, filter line search), not Fatrop; g++ -O3 -march=x86-64-v3",
+            "per_thread_s_per_solve": wall * threads / (B * n_steps), "mean_iter": float(st[:, :, 1].mean()),
+            "cpu_model": _cpu_model(), "host_cpus_visible": avail, "omp_num_threads_env": env,
+            "cgroup_cpu_quota": _cgroup_cpu_quota()}
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -209,7 +243,7 @@ def main():
     ap.add_argument("--nodes", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--solver", default="osqp", choices=["osqp", "fatrop"],
-                    help="osqp: the headline SQP + OSQP path; fatrop: the interior-point restatement (no CPU baseline)")
+                    help="osqp: the headline SQP + OSQP path; fatrop: the interior-point restatement")
     ap.add_argument("--dry-run", action="store_true", help="gloo plumbing only, no GPU")
     ap.add_argument("--host-io-steps", type=int, default=None,
                     help="extra steps timed with the per-step D2H of [u_0, x_state] (default min(steps, 10))")
@@ -225,8 +259,11 @@ def main():
     if args.dry_run:
         return dry_run(args, world, rank)
     base = None
-    if not args.no_cpu_baseline and world == 1 and args.solver == "osqp":
-        base = cpu_baseline(args.robot, args.dynamics, args.nodes)  # before the GPU is initialised
+    if not args.no_cpu_baseline and world == 1:  # before the GPU is initialised
+        if args.solver == "osqp":
+            base = cpu_baseline(args.robot, args.dynamics, args.nodes)
+        else:
+            base = cpu_baseline_ip(args.robot, args.dynamics, args.nodes)
     dist = pdist.init("nccl")
 
     R = robots.ROBOTS[args.robot]()

@@ -62,6 +62,25 @@ struct ViolEmit {
 
 inline double limit(double v) { return v < MIN_SCALING ? 1.0 : (v > MAX_SCALING ? MAX_SCALING : v); }
 
+// Upper-triangular CSC pattern of a symmetric K x K matrix and its symbolic LDL^T.
+struct Kkt {
+  int K = 0;
+  std::vector<int> Kp, Ki;
+  std::vector<int> etree, Lnz, Lp;
+};
+
+struct LdlWork {  // numeric LDL^T of one Kkt
+  std::vector<double> Kx, Lx, Dd, Dinv, buf;
+  std::vector<int> Li, yMark, yIdx, elim, nextc;
+  void init(const Kkt& k) {
+    Kx.assign(k.Ki.size(), 0.0);
+    Lx.assign(k.Lp[k.K], 0.0);
+    Li.assign(k.Lp[k.K], 0);
+    for (auto* v : {&Dd, &Dinv, &buf}) v->assign(k.K, 0.0);
+    for (auto* v : {&yMark, &yIdx, &elim, &nextc}) v->assign(k.K, 0);
+  }
+};
+
 // Shared (read-only) structure of one OCP: layout, A pattern (CSC), KKT pattern.
 struct Problem {
   PlModel M;
@@ -78,37 +97,33 @@ struct Problem {
   std::vector<std::pair<int, int>> jc_list;    // (local row, CSC slot)
   // KKT: permuted index of x_j and of row r; upper-triangular CSC pattern; value maps
   std::vector<int> perm_x, perm_z;
-  int K;
-  std::vector<int> Kp, Ki;
+  Kkt kkt;
   std::vector<int> kdiag_x, kdiag_z, kA;      // KKT slot of (x_j, x_j), (z_r, z_r), A entry e
-  // symbolic LDL^T
-  std::vector<int> etree, Lnz, Lp;
+  // interior point (built by cpu_ip_prepare): Lagrangian Hessian pairs per node type and the
+  // KKT [H + H_L + d I, J^T; J, -W^-1] with the w_i blocks of H_L in its pattern
+  bool ip_ready = false;
+  std::vector<std::pair<int, int>> hpairs[3];  // (j, k), j <= k, structurally non-zero (probe)
+  Kkt ipk;
+  std::vector<int> ik_diag_x, ik_diag_z, ik_A;
+  std::vector<int> ik_H_off, ik_H;            // per node: first slot index into ik_H; KKT slot per pair
 };
 
 struct Work {  // per-thread scratch
-  std::vector<double> g, lbg, ubg, grad, Ax, A, tan, P, q, l, u, xs_, zs_, ys_, D, E, rho, rinv, Kx, Lx, Dd, Dinv, rhs,
-      sol, xt, zt, dx, dy, x_prev, z_prev, Axv, Aty, step, xtrial, buf;
-  std::vector<int> Li, yMark, yIdx, elim, nextc;
+  std::vector<double> g, lbg, ubg, grad, Ax, A, tan, P, q, l, u, xs_, zs_, ys_, D, E, rho, rinv, rhs, sol, xt, zt, dx,
+      dy, x_prev, z_prev, Axv, Aty, step, xtrial, buf;
+  LdlWork ldl;
   void init(const Problem& pr) {
-    const int n = pr.n, m = pr.m, K = pr.K;
+    const int n = pr.n, m = pr.m, K = pr.kkt.K;
     for (auto* v : {&g, &lbg, &ubg, &l, &u, &zs_, &ys_, &E, &rho, &rinv, &zt, &dy, &z_prev, &Axv})
       v->assign(m, 0.0);
     for (auto* v : {&grad, &P, &q, &xs_, &D, &xt, &dx, &x_prev, &Aty, &step, &xtrial}) v->assign(n, 0.0);
     Ax.assign(pr.nnz, 0.0);
     A.assign(pr.nnz, 0.0);
     tan.assign(512, 0.0);
-    Kx.assign(pr.Ki.size(), 0.0);
-    Lx.assign(pr.Lp[K], 0.0);
-    Li.assign(pr.Lp[K], 0);
-    Dd.assign(K, 0.0);
-    Dinv.assign(K, 0.0);
+    ldl.init(pr.kkt);
     rhs.assign(K, 0.0);
     sol.assign(K, 0.0);
-    buf.assign(K, 0.0);
-    yMark.assign(K, 0);
-    yIdx.assign(K, 0);
-    elim.assign(K, 0);
-    nextc.assign(K, 0);
+    buf.assign(std::max(K, m), 0.0);
   }
 };
 
@@ -199,38 +214,38 @@ double objective(const Problem& pr, const double* p, const double* x, const doub
 }
 
 // ---------------------------------------------------------------- LDL^T (QDLDL algorithm)
-void ldl_symbolic(Problem& pr) {
-  const int K = pr.K;
+void ldl_symbolic(Kkt& kk) {
+  const int K = kk.K;
   std::vector<int> work(K);
-  pr.etree.assign(K, -1);
-  pr.Lnz.assign(K, 0);
+  kk.etree.assign(K, -1);
+  kk.Lnz.assign(K, 0);
   for (int j = 0; j < K; ++j) {
     work[j] = j;
-    for (int q = pr.Kp[j]; q < pr.Kp[j + 1]; ++q) {
-      int i = pr.Ki[q];
+    for (int q = kk.Kp[j]; q < kk.Kp[j + 1]; ++q) {
+      int i = kk.Ki[q];
       if (i == j) continue;
       while (work[i] != j) {
-        if (pr.etree[i] == -1) pr.etree[i] = j;
-        pr.Lnz[i]++;
+        if (kk.etree[i] == -1) kk.etree[i] = j;
+        kk.Lnz[i]++;
         work[i] = j;
-        i = pr.etree[i];
+        i = kk.etree[i];
       }
     }
   }
-  pr.Lp.assign(K + 1, 0);
-  for (int i = 0; i < K; ++i) pr.Lp[i + 1] = pr.Lp[i] + pr.Lnz[i];
+  kk.Lp.assign(K + 1, 0);
+  for (int i = 0; i < K; ++i) kk.Lp[i + 1] = kk.Lp[i] + kk.Lnz[i];
 }
 
 // Up-looking numeric factorization of the upper-triangular CSC (Kp, Ki, Kx).
-bool ldl_numeric(const Problem& pr, Work& w) {
-  const int K = pr.K;
+bool ldl_numeric(const Kkt& kk, LdlWork& w) {
+  const int K = kk.K;
   double* y = w.buf.data();
-  for (int i = 0; i < K; ++i) { w.yMark[i] = 0; y[i] = 0.0; w.nextc[i] = pr.Lp[i]; }
+  for (int i = 0; i < K; ++i) { w.yMark[i] = 0; y[i] = 0.0; w.nextc[i] = kk.Lp[i]; }
   for (int k = 0; k < K; ++k) {
     int nnzY = 0;
     w.Dd[k] = 0.0;
-    for (int q = pr.Kp[k]; q < pr.Kp[k + 1]; ++q) {
-      const int b = pr.Ki[q];
+    for (int q = kk.Kp[k]; q < kk.Kp[k + 1]; ++q) {
+      const int b = kk.Ki[q];
       if (b == k) { w.Dd[k] = w.Kx[q]; continue; }
       y[b] = w.Kx[q];
       int nx = b;
@@ -238,12 +253,12 @@ bool ldl_numeric(const Problem& pr, Work& w) {
         w.yMark[nx] = 1;
         w.elim[0] = nx;
         int ne = 1;
-        nx = pr.etree[b];
+        nx = kk.etree[b];
         while (nx != -1 && nx < k) {
           if (w.yMark[nx]) break;
           w.yMark[nx] = 1;
           w.elim[ne++] = nx;
-          nx = pr.etree[nx];
+          nx = kk.etree[nx];
         }
         while (ne) w.yIdx[nnzY++] = w.elim[--ne];
       }
@@ -252,7 +267,7 @@ bool ldl_numeric(const Problem& pr, Work& w) {
       const int c = w.yIdx[t];
       const int tmp = w.nextc[c];
       const double yc = y[c];
-      for (int j = pr.Lp[c]; j < tmp; ++j) y[w.Li[j]] -= w.Lx[j] * yc;
+      for (int j = kk.Lp[c]; j < tmp; ++j) y[w.Li[j]] -= w.Lx[j] * yc;
       w.Li[tmp] = k;
       w.Lx[tmp] = yc * w.Dinv[c];
       w.Dd[k] -= yc * w.Lx[tmp];
@@ -266,13 +281,13 @@ bool ldl_numeric(const Problem& pr, Work& w) {
   return true;
 }
 
-void ldl_solve(const Problem& pr, const Work& w, double* x) {
-  const int K = pr.K;
+void ldl_solve(const Kkt& kk, const LdlWork& w, double* x) {
+  const int K = kk.K;
   for (int i = 0; i < K; ++i)
-    for (int j = pr.Lp[i]; j < pr.Lp[i + 1]; ++j) x[w.Li[j]] -= w.Lx[j] * x[i];
+    for (int j = kk.Lp[i]; j < kk.Lp[i + 1]; ++j) x[w.Li[j]] -= w.Lx[j] * x[i];
   for (int i = 0; i < K; ++i) x[i] *= w.Dinv[i];
   for (int i = K - 1; i >= 0; --i)
-    for (int j = pr.Lp[i]; j < pr.Lp[i + 1]; ++j) x[i] -= w.Lx[j] * x[w.Li[j]];
+    for (int j = kk.Lp[i]; j < kk.Lp[i + 1]; ++j) x[i] -= w.Lx[j] * x[w.Li[j]];
 }
 
 // ---------------------------------------------------------------- OSQP 0.6
@@ -346,12 +361,13 @@ OsqpInfo osqp_update_solve(const Problem& pr, Work& w, OsqpState& st, const doub
     rinv[r] = 1.0 / rho[r];
   }
   // KKT values + LDL^T
-  std::fill(w.Kx.begin(), w.Kx.end(), 0.0);
-  for (int j = 0; j < n; ++j) w.Kx[pr.kdiag_x[j]] = P[j] + S.sigma;
-  for (int r = 0; r < m; ++r) w.Kx[pr.kdiag_z[r]] = -rinv[r];
-  for (int e = 0; e < nnz; ++e) w.Kx[pr.kA[e]] = A[e];
+  std::vector<double>& Kx = w.ldl.Kx;
+  std::fill(Kx.begin(), Kx.end(), 0.0);
+  for (int j = 0; j < n; ++j) Kx[pr.kdiag_x[j]] = P[j] + S.sigma;
+  for (int r = 0; r < m; ++r) Kx[pr.kdiag_z[r]] = -rinv[r];
+  for (int e = 0; e < nnz; ++e) Kx[pr.kA[e]] = A[e];
   OsqpInfo info{UNSOLVED, 0, 0.0, 0.0};
-  if (!ldl_numeric(pr, w)) {
+  if (!ldl_numeric(pr.kkt, w.ldl)) {
     info.status = NON_CVX;
   }
   double* x = st.x.data();
@@ -462,7 +478,7 @@ OsqpInfo osqp_update_solve(const Problem& pr, Work& w, OsqpState& st, const doub
       // rhs = [sigma x - q; z - rho^-1 y] in the KKT ordering
       for (int j = 0; j < n; ++j) rhs[pr.perm_x[j]] = sig * x[j] - q[j];
       for (int r = 0; r < m; ++r) rhs[pr.perm_z[r]] = z[r] - rinv[r] * y[r];
-      ldl_solve(pr, w, rhs);
+      ldl_solve(pr.kkt, w.ldl, rhs);
       for (int j = 0; j < n; ++j) {
         xt[j] = rhs[pr.perm_x[j]];
         const double xn = al * xt[j] + (1.0 - al) * x[j];
@@ -638,6 +654,507 @@ void run_problem(const Problem& pr, Work& w, const double* P0, const double* X0,
   for (int j = 0; j < pr.O.nx; ++j) xs_out[j] = xs[j];
 }
 
+
+// ---------------------------------------------------------------- interior point (Fatrop branch)
+// A compiled restatement of oracle/ip_ref.py (the IPOPT-style primal-dual barrier method
+// with a filter line search that stands in for Fatrop, run_mpc.py:34-37, ocp.py:248-263,
+// 360-373): same settings, slack formulation, reduced Newton system, inertia correction,
+// monotone barrier rule, filter line search and termination.  The Newton system is solved
+// through the quasi-definite KKT [H + H_L + d_w I, J^T; J, -W^-1] by the QDLDL LDL^T (the
+// reduced matrix H + H_L + d_w I + J^T W J is positive definite iff the KKT has exactly n
+// positive pivots, Sylvester's law of inertia); H_L = sum_r lam_r d^2 g_r / dw_i^2 by
+// hyper-dual node passes over the structurally non-zero column pairs of each w_i block (the
+// same technique as the GPU's k_lag_hess).  Fatrop itself is not available: this is a
+// restatement, timed as the CPU baseline of bench.py --solver fatrop.
+constexpr double IP_KAPPA_EPS = 10.0, IP_KAPPA_MU = 0.2, IP_THETA_MU = 1.5, IP_TAU_MIN = 0.99, IP_S_MAX = 100.0;
+constexpr double IP_KAPPA_SIGMA = 1e10, IP_GAMMA_THETA = 1e-5, IP_GAMMA_PHI = 1e-8, IP_DELTA = 1.0, IP_S_THETA = 1.1;
+constexpr double IP_S_PHI = 2.3, IP_ETA_PHI = 1e-8, IP_W_MIN = 1e-20;
+enum { IP_CONVERGED = 1, IP_MAX_ITER = -1, IP_LS_FAIL = -2, IP_NONFINITE = -3 };
+
+struct IpSettings {
+  double tol, mu_init, bound_push, bound_frac, warm_push, delta_w, delta_c;
+  int max_iter, ls_max, n_refine, inertia_cap;
+};
+
+struct HEmit {
+  const double* lam;
+  double acc;
+  int r;
+  void operator()(const HDual& v, double, double) {
+    acc = fma(lam[r], v.c, acc);
+    ++r;
+  }
+};
+
+template <int DYN>
+void probe_pairs(const Problem& pr, int i, std::vector<std::pair<int, int>>& out) {
+  const PlOcpConst& O = pr.O;
+  uint64_t st = 0x2545f4914f6cdd1dull ^ (uint64_t)(i + 7);
+  auto rnd = [&]() {  // uniform in (0.5, 1.5)
+    st ^= st >> 12; st ^= st << 25; st ^= st >> 27;
+    return 0.5 + (double)((st * 0x2545f4914f6cdd1dull) >> 11) / 9007199254740992.0;
+  };
+  std::vector<double> p(O.P.np);
+  for (double& v : p) v = rnd();
+  p[O.P.dt_min] = 0.02;
+  p[O.P.dt_max] = 0.05;
+  for (int k = 0; k < 4 * O.N; ++k) { p[O.P.contact + k] = 0.5; p[O.P.swing + k] = 0.3; }
+  p[O.P.n_contacts] = 2.0;
+  p[O.P.swing_period] = 0.4;
+  p[O.P.swing_vel_limits + 1] = -0.2;
+  const int qo = PL_IS_CV(O.dyn) ? 9 : 3;
+  double qn = 0.0;
+  for (int k = 0; k < 4; ++k) qn += p[O.P.x_init + qo + k] * p[O.P.x_init + qo + k];
+  for (int k = 0; k < 4; ++k) p[O.P.x_init + qo + k] /= sqrt(qn);
+  const int nw = pr.nw[i], ndx = O.ndx;
+  std::vector<double> xw(nw + ndx), lam(pr.nrow[i]);
+  for (double& v : xw) v = 0.2 * (rnd() - 1.0);
+  for (size_t r = 0; r < lam.size(); ++r) lam[r] = (r & 1) ? rnd() : -rnd();
+  HDual kst[PL_KIN_STORE];
+  out.clear();
+  for (int k = 0; k < nw; ++k)
+    for (int j = 0; j <= k; ++j) {
+      pl::VecIn<HDual> dx{xw.data(), nullptr, 0.0, j, k};
+      pl::VecIn<HDual> u{xw.data() + ndx, nullptr, 0.0, j - ndx, k - ndx};
+      pl::VecIn<HDual> dxn{xw.data() + nw, nullptr, 0.0, j - nw, k - nw};
+      HEmit e{lam.data(), 0.0, 0};
+      pl::node_rows<HDual, DYN>(pr.M, O, i, p.data(), dx, u, dxn, e, kst, 1);
+      if (e.acc != 0.0) out.push_back({j, k});
+    }
+}
+
+// H_L blocks at (x, lam): hv[pair] = sum_r lam_r g_r.c over the node's rows
+template <int DYN>
+void lag_hess(const Problem& pr, const double* p, const double* x, const double* lam, double* hv) {
+  HDual kst[PL_KIN_STORE];
+  const int ndx = pr.O.ndx;
+  for (int i = 0; i < pr.N; ++i) {
+    const auto& pl_ = pr.hpairs[pl::node_type(pr.O, i)];
+    const int xo = pr.x_off[i], xn = pr.x_off[i + 1], nw = pr.nw[i];
+    for (size_t q = 0; q < pl_.size(); ++q) {
+      const int j = pl_[q].first, k = pl_[q].second;
+      pl::VecIn<HDual> dx{x + xo, nullptr, 0.0, j, k};
+      pl::VecIn<HDual> u{x + xo + ndx, nullptr, 0.0, j - ndx, k - ndx};
+      pl::VecIn<HDual> dxn{x + xn, nullptr, 0.0, j - nw, k - nw};
+      HEmit e{lam + pr.row_off[i], 0.0, 0};
+      pl::node_rows<HDual, DYN>(pr.M, pr.O, i, p, dx, u, dxn, e, kst, 1);
+      hv[pr.ik_H_off[i] + q] = e.acc;
+    }
+  }
+}
+
+template <int DYN>
+void ip_prepare(Problem& pr) {
+  const int n = pr.n, m = pr.m, N = pr.N;
+  for (int i = 0; i < N; ++i) {
+    const int t = pl::node_type(pr.O, i);
+    if (pr.hpairs[t].empty()) probe_pairs<DYN>(pr, i, pr.hpairs[t]);
+  }
+  // KKT pattern: the OSQP branch's (diagonal + A) plus the H_L pairs, same ordering
+  Kkt& kk = pr.ipk;
+  kk.K = n + m;
+  std::vector<std::vector<std::pair<int, int>>> cols(kk.K);  // (row, tag)
+  for (int j = 0; j < n; ++j) cols[pr.perm_x[j]].push_back({pr.perm_x[j], -1 - j});
+  for (int r = 0; r < m; ++r) cols[pr.perm_z[r]].push_back({pr.perm_z[r], -1 - n - r});
+  for (int j = 0; j < n; ++j)
+    for (int k = pr.Ap[j]; k < pr.Ap[j + 1]; ++k) {
+      const int a = pr.perm_x[j], b = pr.perm_z[pr.Ai[k]];
+      cols[std::max(a, b)].push_back({std::min(a, b), k});
+    }
+  const int tagH = 1 << 30;  // pair tags: tagH + running pair index
+  pr.ik_H_off.assign(N + 1, 0);
+  int npair = 0;
+  for (int i = 0; i < N; ++i) {
+    pr.ik_H_off[i] = npair;
+    for (auto& jk : pr.hpairs[pl::node_type(pr.O, i)]) {
+      const int a = pr.perm_x[pr.x_off[i] + jk.first], b = pr.perm_x[pr.x_off[i] + jk.second];
+      cols[std::max(a, b)].push_back({std::min(a, b), tagH + npair});
+      ++npair;
+    }
+  }
+  pr.ik_H_off[N] = npair;
+  pr.ik_H.assign(npair, 0);
+  pr.ik_diag_x.assign(n, 0);
+  pr.ik_diag_z.assign(m, 0);
+  pr.ik_A.assign(pr.nnz, 0);
+  kk.Kp.assign(kk.K + 1, 0);
+  kk.Ki.clear();
+  for (int c = 0; c < kk.K; ++c) {
+    std::sort(cols[c].begin(), cols[c].end());
+    int last = -1, slot = -1;
+    for (auto& e : cols[c]) {
+      if (e.first != last) {  // a diagonal pair (j, j) shares the (x_j, x_j) slot
+        slot = (int)kk.Ki.size();
+        kk.Ki.push_back(e.first);
+        last = e.first;
+      }
+      if (e.second >= tagH) pr.ik_H[e.second - tagH] = slot;
+      else if (e.second >= 0) pr.ik_A[e.second] = slot;
+      else if (-1 - e.second < n) pr.ik_diag_x[-1 - e.second] = slot;
+      else pr.ik_diag_z[-1 - e.second - n] = slot;
+    }
+    kk.Kp[c + 1] = (int)kk.Ki.size();
+  }
+  ldl_symbolic(kk);
+  pr.ip_ready = true;
+}
+
+struct IpStats {
+  int status, iter, trials;
+  double err, f;
+};
+
+struct IpWork {
+  LdlWork ldl;
+  std::vector<double> g, lbg, ubg, grad, gt, lt, ut, J, H, s, sl, su, zl, zu, lam, c, rx, W, bs, rhat, rhs, dx, dl, ds,
+      dzl, dzu, sol, jdx, res, xt, st, tmp, hv;
+  std::vector<char> eq, hl, hu;
+  void init(const Problem& pr) {
+    const int n = pr.n, m = pr.m;
+    ldl.init(pr.ipk);
+    for (auto* v : {&g, &lbg, &ubg, &gt, &lt, &ut, &s, &sl, &su, &zl, &zu, &lam, &c, &W, &bs, &rhat, &dl, &ds, &dzl,
+                    &dzu, &jdx, &st})
+      v->assign(m, 0.0);
+    for (auto* v : {&grad, &H, &rhs, &dx, &res, &xt, &tmp, &rx}) v->assign(n, 0.0);
+    J.assign(pr.nnz, 0.0);
+    sol.assign(pr.ipk.K, 0.0);
+    hv.assign(pr.ik_H_off.back(), 0.0);
+    eq.assign(m, 0);
+    hl.assign(m, 0);
+    hu.assign(m, 0);
+  }
+};
+
+// J (CSC over pr.Ap / pr.Ai) products
+void jt_mul(const Problem& pr, const double* J, const double* v, double* out) {  // out = J^T v
+  for (int j = 0; j < pr.n; ++j) {
+    double a = 0.0;
+    for (int q = pr.Ap[j]; q < pr.Ap[j + 1]; ++q) a += J[q] * v[pr.Ai[q]];
+    out[j] = a;
+  }
+}
+void j_mul(const Problem& pr, const double* J, const double* v, double* out) {  // out = J v
+  for (int r = 0; r < pr.m; ++r) out[r] = 0.0;
+  for (int j = 0; j < pr.n; ++j)
+    for (int q = pr.Ap[j]; q < pr.Ap[j + 1]; ++q) out[pr.Ai[q]] += J[q] * v[j];
+}
+
+// fraction to the boundary: max alpha in (0, 1] with v + alpha dv >= (1 - tau) v on the mask
+double ftb(const std::vector<double>& v, const std::vector<double>& dv, double sgn, double tau,
+           const std::vector<char>& mask) {
+  double a = 1.0;
+  for (size_t r = 0; r < v.size(); ++r)
+    if (mask[r] && sgn * dv[r] < 0) a = std::min(a, -tau * v[r] / (sgn * dv[r]));
+  return a;
+}
+
+// One interior-point solve from x (in / out); lam (in / out) is the lam_g warm start when warm.
+template <int DYN>
+IpStats ip_solve(const Problem& pr, Work& w, IpWork& iw, const IpSettings& S, const double* p, const double* Pd,
+                 double* x, double* lam_io, bool warm) {
+  const int n = pr.n, m = pr.m;
+  double mu = S.mu_init;
+  const double tol = S.tol, dc = S.delta_c;
+  double dw_last = 0.0;
+  std::vector<double>& H = iw.H;
+  for (int j = 0; j < n; ++j) H[j] = Pd[j] + S.delta_w;
+  eval_values<DYN>(pr, p, x, nullptr, 0.0, iw.g.data(), iw.lbg.data(), iw.ubg.data());
+  const double* lbg = iw.lbg.data();
+  const double* ubg = iw.ubg.data();
+  auto& eq = iw.eq;
+  auto& hl = iw.hl;
+  auto& hu = iw.hu;
+  int nb = 0;
+  for (int r = 0; r < m; ++r) {
+    eq[r] = lbg[r] == ubg[r];
+    hl[r] = !eq[r] && std::isfinite(lbg[r]);
+    hu[r] = !eq[r] && std::isfinite(ubg[r]);
+    nb += hl[r] + hu[r];
+  }
+  auto lbv = [&](int r) { return hl[r] ? lbg[r] : 0.0; };
+  auto ubv = [&](int r) { return hu[r] ? ubg[r] : 0.0; };
+  // slacks pushed into the interior (push_slacks)
+  for (int r = 0; r < m; ++r) {
+    const double lb = lbv(r), ub = ubv(r);
+    double pl_ = S.bound_push * fmax(1.0, fabs(lb)), pu = S.bound_push * fmax(1.0, fabs(ub));
+    if (hl[r] && hu[r]) {
+      pl_ = fmin(pl_, S.bound_frac * (ub - lb));
+      pu = fmin(pu, S.bound_frac * (ub - lb));
+    }
+    double sv = iw.g[r];
+    if (hl[r]) sv = fmax(sv, lb + pl_);
+    if (hu[r]) sv = fmin(sv, ub - pu);
+    iw.s[r] = eq[r] ? 0.0 : sv;
+    iw.sl[r] = hl[r] ? iw.s[r] - lb : 1.0;
+    iw.su[r] = hu[r] ? ub - iw.s[r] : 1.0;
+  }
+  double* lam = iw.lam.data();
+  for (int r = 0; r < m; ++r) {
+    if (!warm) {
+      lam[r] = 0.0;
+      iw.zl[r] = hl[r] ? mu / iw.sl[r] : 0.0;
+      iw.zu[r] = hu[r] ? mu / iw.su[r] : 0.0;
+    } else {
+      lam[r] = lam_io[r];
+      iw.zl[r] = hl[r] ? fmax(fmax(-lam[r], 0.0), S.warm_push) : 0.0;
+      iw.zu[r] = hu[r] ? fmax(fmax(lam[r], 0.0), S.warm_push) : 0.0;
+    }
+  }
+  auto cval = [&](const double* g, const double* s_, int r) { return eq[r] ? g[r] - (eq[r] ? lbg[r] : 0.0) : g[r] - s_[r]; };
+  double theta0 = 0.0;
+  for (int r = 0; r < m; ++r) theta0 += fabs(cval(iw.g.data(), iw.s.data(), r));
+  const double theta_max = 1e4 * fmax(1.0, theta0), theta_min = 1e-4 * fmax(1.0, theta0);
+  auto phi_of = [&](double f, const double* sl, const double* su) {
+    double a = 0.0, b = 0.0;
+    for (int r = 0; r < m; ++r) if (hl[r]) a += log(sl[r]);
+    for (int r = 0; r < m; ++r) if (hu[r]) b += log(su[r]);
+    return f - mu * (a + b);
+  };
+  std::vector<std::pair<double, double>> filt;
+  IpStats out{IP_MAX_ITER, 0, 0, INFINITY, NAN};
+  double f = NAN, err = INFINITY;
+  for (int k = 0; k <= S.max_iter; ++k) {
+    out.iter = k;
+    f = objective(pr, p, x, nullptr, 0.0, iw.grad.data());
+    eval_values<DYN>(pr, p, x, nullptr, 0.0, iw.g.data(), iw.lt.data(), iw.ut.data());
+    eval_jac<DYN>(pr, p, x, w, iw.J.data());
+    for (int r = 0; r < m; ++r) iw.c[r] = cval(iw.g.data(), iw.s.data(), r);
+    jt_mul(pr, iw.J.data(), lam, iw.rx.data());
+    for (int j = 0; j < n; ++j) iw.rx[j] += iw.grad[j];
+    double sum_lam = 0.0, sum_z = 0.0;
+    for (int r = 0; r < m; ++r) { sum_lam += fabs(lam[r]); sum_z += iw.zl[r] + iw.zu[r]; }
+    const double sd = fmax(IP_S_MAX, (sum_lam + sum_z) / std::max(m + nb, 1)) / IP_S_MAX;
+    const double sc = fmax(IP_S_MAX, sum_z / std::max(nb, 1)) / IP_S_MAX;
+    auto nlp_err = [&](double mu_) {
+      double comp = 0.0, erx = 0.0, ers = 0.0, ec = 0.0;
+      for (int r = 0; r < m; ++r) {
+        if (hl[r]) comp = fmax(comp, fabs(iw.sl[r] * iw.zl[r] - mu_));
+        if (hu[r]) comp = fmax(comp, fabs(iw.su[r] * iw.zu[r] - mu_));
+        if (!eq[r]) ers = fmax(ers, fabs(-lam[r] - iw.zl[r] + iw.zu[r]));
+        ec = fmax(ec, fabs(iw.c[r]));
+      }
+      for (int j = 0; j < n; ++j) erx = fmax(erx, fabs(iw.rx[j]));
+      return fmax(fmax(erx / sd, ers / sd), fmax(ec, comp / sc));
+    };
+    err = nlp_err(0.0);
+    if (!std::isfinite(err)) { out.status = IP_NONFINITE; break; }
+    if (err <= tol) { out.status = IP_CONVERGED; break; }
+    if (k == S.max_iter) { out.status = IP_MAX_ITER; break; }
+    for (int t = 0; t < 4; ++t) {  // monotone barrier update
+      if (nlp_err(mu) > IP_KAPPA_EPS * mu) break;
+      const double mu_new = fmax(tol / 10.0, fmin(IP_KAPPA_MU * mu, pow(mu, IP_THETA_MU)));
+      if (mu_new == mu) break;
+      mu = mu_new;
+      filt.clear();
+    }
+    // reduced Newton system through the quasi-definite KKT
+    for (int r = 0; r < m; ++r) {
+      const double sig = (hl[r] ? iw.zl[r] / iw.sl[r] : 0.0) + (hu[r] ? iw.zu[r] / iw.su[r] : 0.0);
+      double Wr = eq[r] ? 1.0 / dc : sig / (1.0 + dc * sig);
+      iw.W[r] = fmax(Wr, IP_W_MIN);
+      iw.bs[r] = eq[r] ? 0.0 : lam[r] + (hl[r] ? mu / iw.sl[r] : 0.0) - (hu[r] ? mu / iw.su[r] : 0.0);
+      const double sig_safe = eq[r] ? 1.0 : sig;
+      iw.rhat[r] = eq[r] ? iw.c[r] : iw.c[r] - iw.bs[r] / sig_safe;
+    }
+    std::vector<double>& Kx = iw.ldl.Kx;
+    lag_hess<DYN>(pr, p, x, lam, iw.hv.data());
+    auto assemble = [&](double dwi) {
+      std::fill(Kx.begin(), Kx.end(), 0.0);
+      for (int j = 0; j < n; ++j) Kx[pr.ik_diag_x[j]] += H[j] + dwi;
+      for (int r = 0; r < m; ++r) Kx[pr.ik_diag_z[r]] = -1.0 / iw.W[r];
+      for (int e = 0; e < pr.nnz; ++e) Kx[pr.ik_A[e]] = iw.J[e];
+      for (size_t q = 0; q < iw.hv.size(); ++q) Kx[pr.ik_H[q]] += iw.hv[q];
+    };
+    auto inertia_ok = [&]() {
+      if (!ldl_numeric(pr.ipk, iw.ldl)) return false;
+      int pos = 0;
+      for (int q = 0; q < pr.ipk.K; ++q) pos += iw.ldl.Dd[q] > 0.0;
+      return pos == n;
+    };
+    double dwi = 0.0;
+    int tries = 0;
+    assemble(0.0);
+    while (true) {  // inertia correction (ip_ref.py)
+      if (inertia_ok()) {
+        if (dwi > 0.0) dw_last = dwi;
+        break;
+      }
+      if (tries >= S.inertia_cap) break;
+      dwi = dwi == 0.0 ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0)) : dwi * (dw_last == 0.0 ? 100.0 : 8.0);
+      ++tries;
+      assemble(dwi);
+    }
+    auto kkt_solve = [&](const double* r_x, double* out_x) {
+      for (int j = 0; j < n; ++j) iw.sol[pr.perm_x[j]] = r_x[j];
+      for (int r = 0; r < m; ++r) iw.sol[pr.perm_z[r]] = 0.0;
+      ldl_solve(pr.ipk, iw.ldl, iw.sol.data());
+      for (int j = 0; j < n; ++j) out_x[j] = iw.sol[pr.perm_x[j]];
+    };
+    for (int r = 0; r < m; ++r) iw.st[r] = iw.W[r] * iw.rhat[r];
+    jt_mul(pr, iw.J.data(), iw.st.data(), iw.rhs.data());
+    for (int j = 0; j < n; ++j) iw.rhs[j] = -iw.rx[j] - iw.rhs[j];
+    kkt_solve(iw.rhs.data(), iw.dx.data());
+    // H_L dx for the refinement residual: the KKT's upper-left block (H + dwi + H_L) times dx
+    auto hl_mul = [&](const double* v, double* outv) {  // (H + dwi + H_L) v over the stored pairs
+      for (int j = 0; j < n; ++j) outv[j] = (H[j] + dwi) * v[j];
+      for (int i = 0; i < pr.N; ++i) {
+        const auto& pl_ = pr.hpairs[pl::node_type(pr.O, i)];
+        const int xo = pr.x_off[i];
+        for (size_t q = 0; q < pl_.size(); ++q) {
+          const int a = xo + pl_[q].first, b = xo + pl_[q].second;
+          const double hv = iw.hv[pr.ik_H_off[i] + q];
+          if (a == b) {
+            outv[a] += hv * v[a];
+          } else {
+            outv[a] += hv * v[b];
+            outv[b] += hv * v[a];
+          }
+        }
+      }
+    };
+    std::vector<double> Hdx(n), corr(n);
+    for (int t = 0; t < S.n_refine; ++t) {
+      j_mul(pr, iw.J.data(), iw.dx.data(), iw.jdx.data());
+      for (int r = 0; r < m; ++r) iw.st[r] = lam[r] + iw.W[r] * (iw.jdx[r] + iw.rhat[r]);
+      jt_mul(pr, iw.J.data(), iw.st.data(), iw.res.data());
+      hl_mul(iw.dx.data(), Hdx.data());
+      for (int j = 0; j < n; ++j) iw.res[j] = -(iw.grad[j] + iw.res[j]) - Hdx[j];
+      kkt_solve(iw.res.data(), corr.data());
+      for (int j = 0; j < n; ++j) iw.dx[j] += corr[j];
+    }
+    j_mul(pr, iw.J.data(), iw.dx.data(), iw.jdx.data());
+    bool finite = true;
+    for (int r = 0; r < m; ++r) {
+      iw.dl[r] = iw.W[r] * (iw.jdx[r] + iw.rhat[r]);
+      const double sig = (hl[r] ? iw.zl[r] / iw.sl[r] : 0.0) + (hu[r] ? iw.zu[r] / iw.su[r] : 0.0);
+      iw.ds[r] = eq[r] ? 0.0 : (iw.bs[r] + iw.dl[r]) / sig;
+      iw.dzl[r] = hl[r] ? mu / iw.sl[r] - iw.zl[r] - iw.zl[r] / iw.sl[r] * iw.ds[r] : 0.0;
+      iw.dzu[r] = hu[r] ? mu / iw.su[r] - iw.zu[r] + iw.zu[r] / iw.su[r] * iw.ds[r] : 0.0;
+      finite &= std::isfinite(iw.dl[r]);
+    }
+    for (int j = 0; j < n; ++j) finite &= std::isfinite(iw.dx[j]);
+    if (!finite) { out.status = IP_NONFINITE; break; }
+    const double tau = fmax(IP_TAU_MIN, 1.0 - mu);
+    const double amax = fmin(ftb(iw.sl, iw.ds, 1.0, tau, hl), ftb(iw.su, iw.ds, -1.0, tau, hu));
+    const double az = fmin(ftb(iw.zl, iw.dzl, 1.0, tau, hl), ftb(iw.zu, iw.dzu, 1.0, tau, hu));
+    double theta = 0.0;
+    for (int r = 0; r < m; ++r) theta += fabs(iw.c[r]);
+    const double phi = phi_of(f, iw.sl.data(), iw.su.data());
+    double dphi = 0.0, sds = 0.0;
+    for (int j = 0; j < n; ++j) dphi += iw.grad[j] * iw.dx[j];
+    for (int r = 0; r < m; ++r) sds += (hl[r] ? -mu / iw.sl[r] : 0.0) * iw.ds[r] + (hu[r] ? mu / iw.su[r] : 0.0) * iw.ds[r];
+    dphi += sds;
+    bool accepted = false, ftype = false;
+    double a = amax;
+    int t = 0;
+    std::vector<double> slt(m), sut(m);
+    for (t = 0; t < S.ls_max; ++t) {
+      a = amax * pow(0.5, t);
+      const double ft = objective(pr, p, x, iw.dx.data(), a, nullptr);
+      eval_values<DYN>(pr, p, x, iw.dx.data(), a, iw.gt.data(), iw.lt.data(), iw.ut.data());
+      double th_t = 0.0;
+      for (int r = 0; r < m; ++r) {
+        const double stt = iw.s[r] + a * iw.ds[r];
+        iw.st[r] = stt;
+        slt[r] = hl[r] ? stt - lbv(r) : 1.0;
+        sut[r] = hu[r] ? ubv(r) - stt : 1.0;
+        th_t += fabs(cval(iw.gt.data(), iw.st.data(), r));
+      }
+      const double ph_t = phi_of(ft, slt.data(), sut.data());
+      if (!(std::isfinite(th_t) && std::isfinite(ph_t)) || th_t > theta_max) continue;
+      bool dominated = false;
+      for (auto& fp : filt) dominated |= th_t >= fp.first && ph_t >= fp.second;
+      if (dominated) continue;
+      const bool switching = dphi < 0 && a * pow(-dphi, IP_S_PHI) > IP_DELTA * pow(theta, IP_S_THETA);
+      if (theta <= theta_min && switching) {
+        if (ph_t <= phi + IP_ETA_PHI * a * dphi) { accepted = ftype = true; break; }
+      } else if (th_t <= (1 - IP_GAMMA_THETA) * theta || ph_t <= phi - IP_GAMMA_PHI * theta) {
+        accepted = true;
+        break;
+      }
+    }
+    out.trials += std::min(t + 1, S.ls_max);
+    if (!accepted) { out.status = IP_LS_FAIL; break; }
+    if (!ftype) filt.push_back({(1 - IP_GAMMA_THETA) * theta, phi - IP_GAMMA_PHI * theta});
+    for (int j = 0; j < n; ++j) x[j] = x[j] + a * iw.dx[j];
+    for (int r = 0; r < m; ++r) {
+      iw.s[r] = iw.s[r] + a * iw.ds[r];
+      lam[r] = lam[r] + a * iw.dl[r];
+      double zl = iw.zl[r] + az * iw.dzl[r], zu = iw.zu[r] + az * iw.dzu[r];
+      iw.sl[r] = hl[r] ? iw.s[r] - lbv(r) : 1.0;
+      iw.su[r] = hu[r] ? ubv(r) - iw.s[r] : 1.0;
+      iw.zl[r] = hl[r] ? fmin(fmax(zl, mu / (IP_KAPPA_SIGMA * iw.sl[r])), IP_KAPPA_SIGMA * mu / iw.sl[r]) : 0.0;
+      iw.zu[r] = hu[r] ? fmin(fmax(zu, mu / (IP_KAPPA_SIGMA * iw.su[r])), IP_KAPPA_SIGMA * mu / iw.su[r]) : 0.0;
+    }
+  }
+  out.err = err;
+  out.f = f;
+  for (int r = 0; r < m; ++r) lam_io[r] = lam[r];
+  return out;
+}
+
+template <int DYN>
+void run_problem_ip(const Problem& pr, Work& w, IpWork& iw, const IpSettings& S, const double* P0, const double* X0,
+                    const double* XS0, double t0, int steps, double* xs_out, int* stats_out) {
+  const PlOcpConst& O = pr.O;
+  std::vector<double> p(P0, P0 + pr.np), x(X0, X0 + pr.n), xs(XS0, XS0 + O.nx), Pd(pr.n), lam(pr.m, 0.0);
+  hess_diag(pr, p.data(), Pd.data());
+  for (int k = 0; k < steps; ++k) {
+    for (int j = 0; j < O.nx; ++j) p[O.P.x_init + j] = xs[j];
+    pl::gait_schedule(O, pr.S.gait_type, pr.S.gait_period, pr.S.swing_period, t0 + k * p[O.P.dt_min], p.data(),
+                      p.data() + O.P.contact, p.data() + O.P.swing);
+    if (k > 0) {  // warm start (ocp_whole_body_rnea.py:207-235): forces reset to f_des on stance
+      const int fo = pl::u_force_off(O);
+      for (int i = 0; i < pr.N; ++i) {
+        const int base = pr.x_off[i] + O.ndx + fo;
+        for (int c = 0; c < O.nf; ++c) {
+          double fd = pl::f_des_comp(pr.M, O, p.data(), c);
+          if (c / 3 < 4 && p[O.P.contact + 4 * i + c / 3] == 0.0) fd = 0.0;
+          x[base + c] = fd;
+        }
+      }
+    }
+    IpStats s = ip_solve<DYN>(pr, w, iw, S, p.data(), Pd.data(), x.data(), lam.data(), k > 0);
+    const double* dx1 = x.data() + pr.x_off[1];
+    double qn[PL_MAXQ];
+    if (PL_IS_CV(O.dyn)) {
+      pl::VecIn<double> acc{dx1 + 6, nullptr, 0.0, -1};
+      pl::integrate_q<double>(pr.M, xs.data() + 6, acc, qn);
+      for (int j = 0; j < 6; ++j) xs[j] += dx1[j];
+      for (int j = 0; j < O.nq; ++j) xs[6 + j] = qn[j];
+    } else {
+      pl::VecIn<double> acc{dx1, nullptr, 0.0, -1};
+      pl::integrate_q<double>(pr.M, xs.data(), acc, qn);
+      for (int j = 0; j < O.nq; ++j) xs[j] = qn[j];
+      for (int j = 0; j < O.nv; ++j) xs[O.nq + j] += dx1[O.nv + j];
+    }
+    if (stats_out) {
+      stats_out[2 * k] = s.status;
+      stats_out[2 * k + 1] = s.iter;
+    }
+  }
+  for (int j = 0; j < O.nx; ++j) xs_out[j] = xs[j];
+}
+
+IpSettings ip_settings_from(const double* v) {
+  IpSettings S;
+  S.tol = v[0]; S.mu_init = v[1]; S.bound_push = v[2]; S.bound_frac = v[3]; S.warm_push = v[4];
+  S.delta_w = v[5]; S.delta_c = v[6]; S.max_iter = (int)v[7]; S.ls_max = (int)v[8]; S.n_refine = (int)v[9];
+  S.inertia_cap = (int)v[10];
+  return S;
+}
+
+#define PL_CPU_DISPATCH(DYNV, CALL)                                         \
+  switch (DYNV) {                                                           \
+    case PL_DYN_RNEA: { constexpr int D_ = PL_DYN_RNEA; CALL; } break;     \
+    case PL_DYN_ACC: { constexpr int D_ = PL_DYN_ACC; CALL; } break;       \
+    case PL_DYN_ABA: { constexpr int D_ = PL_DYN_ABA; CALL; } break;       \
+    case PL_DYN_CA: { constexpr int D_ = PL_DYN_CA; CALL; } break;         \
+    case PL_DYN_ACCNB: { constexpr int D_ = PL_DYN_ACCNB; CALL; } break;   \
+    case PL_DYN_CVNB: { constexpr int D_ = PL_DYN_CVNB; CALL; } break;     \
+    default: { constexpr int D_ = PL_DYN_CV; CALL; } break;                \
+  }
+
 }  // namespace
 
 // ---------------------------------------------------------------- C entry points (ctypes)
@@ -696,7 +1213,8 @@ extern "C" void* cpu_create(const void* model, const void* oc, int N, int n, int
     for (auto& pr2 : lists[c]) pr->jc_list.push_back(pr2);
   }
   // KKT ordering: node by node, the node's variables then the node's rows
-  pr->K = n + m;
+  Kkt& kk = pr->kkt;
+  kk.K = n + m;
   pr->perm_x.assign(n, 0);
   pr->perm_z.assign(m, 0);
   int idx = 0;
@@ -705,7 +1223,7 @@ extern "C" void* cpu_create(const void* model, const void* oc, int N, int n, int
     for (int r = 0; r < nrow[i]; ++r) pr->perm_z[row_off[i] + r] = idx++;
   }
   // upper-triangular CSC of the permuted KKT
-  std::vector<std::vector<std::pair<int, int>>> cols(pr->K);  // (row, tag)
+  std::vector<std::vector<std::pair<int, int>>> cols(kk.K);  // (row, tag)
   for (int j = 0; j < n; ++j) cols[pr->perm_x[j]].push_back({pr->perm_x[j], -1 - j});
   for (int r = 0; r < m; ++r) cols[pr->perm_z[r]].push_back({pr->perm_z[r], -1 - n - r});
   for (int j = 0; j < n; ++j)
@@ -713,28 +1231,28 @@ extern "C" void* cpu_create(const void* model, const void* oc, int N, int n, int
       const int a = pr->perm_x[j], b = pr->perm_z[pr->Ai[k]];
       cols[std::max(a, b)].push_back({std::min(a, b), k});
     }
-  pr->Kp.assign(pr->K + 1, 0);
+  kk.Kp.assign(kk.K + 1, 0);
   pr->kdiag_x.assign(n, 0);
   pr->kdiag_z.assign(m, 0);
   pr->kA.assign(nnz, 0);
-  for (int c = 0; c < pr->K; ++c) {
+  for (int c = 0; c < kk.K; ++c) {
     std::sort(cols[c].begin(), cols[c].end());
     for (auto& e : cols[c]) {
-      const int slot = (int)pr->Ki.size();
-      pr->Ki.push_back(e.first);
+      const int slot = (int)kk.Ki.size();
+      kk.Ki.push_back(e.first);
       if (e.second >= 0) pr->kA[e.second] = slot;
       else if (-1 - e.second < n) pr->kdiag_x[-1 - e.second] = slot;
       else pr->kdiag_z[-1 - e.second - n] = slot;
     }
-    pr->Kp[c + 1] = (int)pr->Ki.size();
+    kk.Kp[c + 1] = (int)kk.Ki.size();
   }
-  ldl_symbolic(*pr);
+  ldl_symbolic(kk);
   return pr;
 }
 
 extern "C" void cpu_destroy(void* h) { delete (Problem*)h; }
 
-extern "C" long long cpu_factor_nnz(void* h) { return ((Problem*)h)->Lp.back(); }
+extern "C" long long cpu_factor_nnz(void* h) { return ((Problem*)h)->kkt.Lp.back(); }
 
 // B problems x `steps` MPC steps on `threads` OpenMP threads (one problem per thread
 // at a time).  Returns the wall seconds of the parallel region; xs_out [B][nx],
@@ -797,4 +1315,60 @@ extern "C" int cpu_sqp_step(void* h, const double* p, double* x, double* dx, int
   stats[0] = s.status; stats[1] = s.iter; stats[2] = s.branch; stats[3] = s.trials;
   *alpha = s.alpha;
   return 0;
+}
+
+// Interior point: build the Hessian pair lists and the KKT pattern (once per OCP).
+extern "C" long long cpu_ip_prepare(void* h) {
+  Problem& pr = *(Problem*)h;
+  if (pr.O.dyn == PL_DYN_RNEAFD) return -1;  // the Fatrop branch keeps a in u (ocp_whole_body_rnea.py:21)
+  if (!pr.ip_ready) PL_CPU_DISPATCH(pr.O.dyn, ip_prepare<D_>(pr));
+  return pr.ik_H_off.back();
+}
+
+// One interior-point solve of one problem from x (in / out); lam [m] in / out (the warm
+// start when warm != 0); stats = (status, iterations, line-search trials); err_f = (err, f).
+extern "C" int cpu_ip_solve(void* h, const double* p, double* x, double* lam, int warm, const double* settings,
+                            int* stats, double* err_f) {
+  Problem& pr = *(Problem*)h;
+  if (cpu_ip_prepare(h) < 0) return -1;
+  const IpSettings S = ip_settings_from(settings);
+  Work w;
+  w.init(pr);
+  IpWork iw;
+  iw.init(pr);
+  std::vector<double> Pd(pr.n);
+  hess_diag(pr, p, Pd.data());
+  IpStats s{};
+  PL_CPU_DISPATCH(pr.O.dyn, s = ip_solve<D_>(pr, w, iw, S, p, Pd.data(), x, lam, warm != 0));
+  stats[0] = s.status; stats[1] = s.iter; stats[2] = s.trials;
+  err_f[0] = s.err; err_f[1] = s.f;
+  return 0;
+}
+
+// B problems x `steps` MPC steps with the interior-point solver (lam_g carried across the
+// steps, run_mpc.py:115-143 with the Fatrop branch) on `threads` OpenMP threads.  Returns
+// the wall seconds; xs_out [B][nx], stats [B][steps][2] = (status, iterations).
+extern "C" double cpu_ip_mpc_batch(void* h, int B, const double* P, const double* X, const double* XS,
+                                   const double* T0, int steps, int threads, const double* settings, double* xs_out,
+                                   int* stats) {
+  Problem& pr = *(Problem*)h;
+  if (cpu_ip_prepare(h) < 0) return -1.0;
+  const IpSettings S = ip_settings_from(settings);
+  const int nx = pr.O.nx;
+  if (threads > 0) omp_set_num_threads(threads);
+  const auto t0 = std::chrono::steady_clock::now();
+#pragma omp parallel
+  {
+    Work w;
+    w.init(pr);
+    IpWork iw;
+    iw.init(pr);
+#pragma omp for schedule(dynamic, 1)
+    for (int b = 0; b < B; ++b) {
+      int* sb = stats ? stats + (size_t)b * steps * 2 : nullptr;
+      PL_CPU_DISPATCH(pr.O.dyn, run_problem_ip<D_>(pr, w, iw, S, P + (size_t)b * pr.np, X + (size_t)b * pr.n,
+                                                   XS + (size_t)b * nx, T0[b], steps, xs_out + (size_t)b * nx, sb));
+    }
+  }
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }

@@ -2,7 +2,9 @@
 
 A compiled C++ restatement of the reference's CPU solve path (OSQP 0.6 with the
 QDLDL LDL^T on the quasi-definite KKT, the Armijo / filter line search, the MPC
-loop of run_mpc.py:127-143), run with OpenMP over independent problems.  bench.py
+loop of run_mpc.py:127-143), and of the interior-point stand-in for its Fatrop
+branch (oracle/ip_ref.py: exact Lagrangian Hessian, QDLDL on the IP's KKT), run with
+OpenMP over independent problems.  bench.py
 times it on the GPU box's host cores beside the GPU run (``cpu_baseline``);
 tests/test_cpu_baseline.py checks it against the numpy oracle's golden vectors.
 Only tests/, bench.py's cpu_baseline leg and __graft_entry__ use this module.
@@ -61,6 +63,11 @@ def lib():
         L.cpu_mpc_batch.restype = C.c_double
         L.cpu_mpc_batch.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp, C.c_int, C.c_int, _dp, _ip]
         L.cpu_sqp_step.argtypes = [C.c_void_p, _dp, _dp, _dp, _ip, _dp]
+        L.cpu_ip_prepare.restype = C.c_longlong
+        L.cpu_ip_prepare.argtypes = [C.c_void_p]
+        L.cpu_ip_solve.argtypes = [C.c_void_p, _dp, _dp, _dp, C.c_int, _dp, _ip, _dp]
+        L.cpu_ip_mpc_batch.restype = C.c_double
+        L.cpu_ip_mpc_batch.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp, C.c_int, C.c_int, _dp, _dp, _ip]
         _lib = L
     return _lib
 
@@ -122,6 +129,51 @@ class CpuOCP:
         xs = np.zeros((B, self.nx))
         stats = np.zeros((B, steps, 4), dtype=np.int32)
         wall = lib().cpu_mpc_batch(self.h, B, _d(P), _d(X), _d(XS), _d(T0), steps, threads, _d(xs), _i(stats))
+        return wall, xs, stats
+
+    @staticmethod
+    def _ip_settings(settings=None):
+        from oracle.ip_ref import IP_SETTINGS
+        s = dict(IP_SETTINGS)
+        s.update(settings or {})
+        if s["hessian"] != "exact":
+            raise ValueError("the CPU interior point restates the exact-Hessian form only")
+        return np.array([s["tol"], s["mu_init"], s["bound_push"], s["bound_frac"], s["warm_start_mult_bound_push"],
+                         s["delta_w"], s["delta_c"], s["max_iter"], s["ls_max"], s["n_refine"], s["inertia_cap"]],
+                        dtype=np.float64)
+
+    def hess_pairs(self):
+        """Number of Lagrangian-Hessian column pairs over the horizon (structural probe)."""
+        n = int(lib().cpu_ip_prepare(self.h))
+        if n < 0:
+            raise ValueError("the interior-point restatement needs include_acc=True")
+        return n
+
+    def ip_solve(self, x, p, lam0=None, settings=None):
+        """One interior-point solve (oracle/ip_ref.py IPRef.solve restated in C++):
+        returns x, lam, dict(status, iter, trials, err, f)."""
+        x = np.ascontiguousarray(np.array(x, dtype=np.float64))
+        p = np.ascontiguousarray(np.asarray(p, dtype=np.float64))
+        lam = np.zeros(self.m) if lam0 is None else np.ascontiguousarray(np.array(lam0, dtype=np.float64))
+        st = self._ip_settings(settings)
+        stats = np.zeros(3, dtype=np.int32)
+        ef = np.zeros(2)
+        if lib().cpu_ip_solve(self.h, _d(p), _d(x), _d(lam), int(lam0 is not None), _d(st), _i(stats), _d(ef)) != 0:
+            raise ValueError("the interior-point restatement needs include_acc=True")
+        return x, lam, dict(status=int(stats[0]), iter=int(stats[1]), trials=int(stats[2]), err=float(ef[0]),
+                            f=float(ef[1]))
+
+    def ip_mpc(self, P, X, XS, T0, steps, threads=0, settings=None):
+        """`steps` MPC steps of every problem with the interior point (lam_g carried);
+        returns (wall seconds, final states, stats [B][steps][2] = (status, iterations))."""
+        B = P.shape[0]
+        P, X, XS = (np.ascontiguousarray(a, dtype=np.float64) for a in (P, X, XS))
+        T0 = np.ascontiguousarray(T0, dtype=np.float64)
+        xs = np.zeros((B, self.nx))
+        stats = np.zeros((B, steps, 2), dtype=np.int32)
+        st = self._ip_settings(settings)
+        wall = lib().cpu_ip_mpc_batch(self.h, B, _d(P), _d(X), _d(XS), _d(T0), steps, threads, _d(st), _d(xs),
+                                      _i(stats))
         return wall, xs, stats
 
     def __del__(self):

@@ -59,3 +59,33 @@ def test_cpu_mpc_loop_matches_golden(name, rname, dyn, N):
     assert np.abs(xs[0] - want).max() <= 1e-8 * np.abs(want).max()
     assert np.array_equal(stats[0], G["loop_stats"])
     assert wall > 0
+
+
+def _cpu_ip(name, rname, dyn, N):
+    from oracle.cpu_baseline import CpuOCP
+    G = golden(f"{name}.npz")
+    gait = str(G["gait"])
+    kw = {"include_base": bool(int(G["include_base"]))} if "include_base" in G else {}
+    return G, CpuOCP(make_robot(rname, gait), dyn, N, gait_type=gait, **kw)
+
+
+@pytest.mark.parametrize("name,rname,dyn,N,probs", [
+    ("ip_go2_rnea_n20", "go2", "whole_body_rnea", 20, [0, 2]),
+    ("ip_go2_rnea_n20_stand", "go2", "whole_body_rnea", 20, [0]),
+    ("ip_go2_cv_nb_n20", "go2", "centroidal_vel", 20, [1]),
+])
+def test_cpu_interior_point_matches_golden(name, rname, dyn, N, probs):
+    """The C++ interior point (the CPU baseline of bench.py --solver fatrop) against the
+    numpy restatement oracle/ip_ref.py: status, iterations and line-search trials exact,
+    x and lam_g <= 1e-7 relative (QDLDL on the quasi-definite KKT against splu on the
+    reduced system; measured ~1e-10); the lam_g warm-started solve of ip_go2_rnea_n20."""
+    G, c = _cpu_ip(name, rname, dyn, N)
+    for b in probs:
+        x, lam, st = c.ip_solve(G["X"][b], G["P"][b])
+        assert (st["status"], st["iter"], st["trials"]) == (G["status"][b], G["iter"][b], G["trials"][b]), b
+        assert np.abs(x - G["x_out"][b]).max() <= 1e-7 * np.abs(G["x_out"][b]).max(), b
+        assert np.abs(lam - G["lam"][b]).max() <= 1e-7 * max(1.0, np.abs(G["lam"][b]).max()), b
+        if "warm_x" in G and b < G["warm_x"].shape[0]:
+            xw, lw, sw = c.ip_solve(x, G["P"][b], lam0=lam)
+            assert (sw["status"], sw["iter"]) == (G["warm_status"][b], G["warm_iter"][b]), b
+            assert np.abs(xw - G["warm_x"][b]).max() <= 1e-7 * np.abs(G["warm_x"][b]).max(), b
