@@ -412,6 +412,7 @@ int build_admm_prog(pl_ocp* o) {
     for (int q = 0; q < nq; ++q) P.push_back((uint16_t)re[q]);
     bytes(a.rowc, nq, [&](int q) { return ecol[re[q]]; });
     bytes(a.colr, nd.nent, [&](int e) { return rid[e]; });
+    bytes(a.ecol, nd.nent, [&](int e) { return ecol[e]; });  // the entry-order scatters of k_admm
     // coupling rows split into their w part and their dx_{i+1} part
     std::vector<int> cwp{0}, cxp{0};
     std::vector<std::pair<int, int>> cw, cx;

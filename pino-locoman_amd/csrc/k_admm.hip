@@ -16,9 +16,10 @@
 // backward 0 with the next iteration's forward 0 (S_0 stays in registers).  Per
 // iteration 2N factor blocks are streamed instead of 2(N+1).
 //
-// MI355X mapping.  The kernel is HBM-bound on the factor stream (4.5 MB per
-// problem-iteration for B2G whole_body_rnea N=50), so the design goal is to keep
-// the whole batch resident with one factor block per problem in flight:
+// MI355X mapping.  The kernel streams the factor (4.14 MB algorithmic per problem-iteration
+// for B2G whole_body_rnea N=50, 4.69 MB measured with the tile padding and vector gathers),
+// so the design goal is to keep the whole batch resident with one factor block per problem
+// in flight:
 //   * one 64-lane wave per problem, PPW problems per workgroup: 1024 problems =
 //     256 workgroups x 4 waves = one wave per SIMD on every CU, all resident
 //     (the previous 256-thread-per-problem kernel fit only 2 problems per CU and
@@ -32,11 +33,14 @@
 //   * every distinct node program (u16 gather lists) is LDS-resident for the whole
 //     launch and shared by the PPW waves.
 // The symmetric mat-vec uses the packed lower 4x4 tiles: each tile gives 4 row
-// partials (accumulated per lane over the lane's run of tiles in a tile row, one
-// LDS "segment" per (lane, tile row)) and 4 column partials (one LDS slot per
-// tile); every output sums its segments and the column partials of its tile
-// column in a fixed order, so results are bit-identical for a problem regardless
-// of the batch or workgroup it runs in.
+// partials (accumulated per lane over the lane's run of tiles in a tile row) and, off the
+// diagonal, 4 column partials; both go straight into a per-wave LDS accumulator with
+// ds_add_f64 (PL_ADMM_ATOMIC, r02e; the segment / column-partial arrays of r01 remain as
+// the #else branch).  The backward step's A x~ and A^T (rho z - y) scatter the node's
+// entries in storage order into LDS row / column sums (r04; PL_ADMM_CHUNKED=1 keeps the
+// chunked CSR / CSC gathers).  The lanes of one ds_add instruction and the instructions
+// of one wave apply in a fixed order, so results are bit-identical for a problem
+// regardless of the batch or workgroup it runs in.
 #include <algorithm>
 #include <type_traits>
 
@@ -74,7 +78,7 @@ struct AdmmLds {
 
 }  // namespace
 
-template <int PPW, int ASR, bool TIMING>
+template <int PPW, int ASR, bool TIMING, bool SC>
 __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int n, int m, int nnz, int ndx,
                                                       int S_stride, int cpl_stride, AdmmLds lm, int niter, int check,
                                                       int fwd_asb, double sigma, double alpha) {
@@ -517,8 +521,31 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     }
     if (bw) {
       with_A(ne, Ai, [&](auto A) __attribute__((always_inline)) {
-        // ---- z~ = A x~ over balanced row chunks
-        {
+        // ---- z~ = A x~
+        if constexpr (SC) {
+          // entry-order scatter: entry e = lane + 64 k (storage order: column-major, so the lanes
+          // of one instruction mostly hit distinct rows) adds A_e x~_c into row r with ds_add_f64;
+          // every load is independent (one LDS round trip deep), and row r sums its entries in
+          // column order (the lanes of an instruction and the instructions of the wave apply in
+          // a fixed order: deterministic)
+          const uint8_t* er8 = reinterpret_cast<const uint8_t*>(P + an[i].colr);
+          const uint8_t* ec8 = reinterpret_cast<const uint8_t*>(P + an[i].ecol);
+          for (int o = lane; o < an[i].nrow; o += 64) part[o] = 0.0;
+          wsync();
+          for (int e0 = 0; e0 < ne; e0 += 256) {
+            double t[4];
+            int r[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int e = min(e0 + 64 * u + lane, ne - 1);
+              r[u] = er8[e];
+              t[u] = A(e) * y[ec8[e]];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (e0 + 64 * u + lane < ne) lds_add(part + r[u], t[u]);
+          }
+        } else {
           const uint16_t* rowe = P + an[i].rowe;
           const uint8_t* rowc = reinterpret_cast<const uint8_t*>(P + an[i].rowc);
           const uint32_t* rch = reinterpret_cast<const uint32_t*>(P + an[i].rch);
@@ -588,8 +615,29 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
         }
         wsync();
         T(6);
-        // ---- A^T (rho z - y) over column chunks
-        {
+        // ---- A^T (rho z - y)
+        if constexpr (SC) {
+          // entry-order scatter into the columns (w_i, then the dx_{i+1} part a2); a column's
+          // entries are contiguous, so the lanes of one instruction share a few column addresses
+          // (applied in lane order); column c sums its rows in row order
+          const uint8_t* er8 = reinterpret_cast<const uint8_t*>(P + an[i].colr);
+          const uint8_t* ec8 = reinterpret_cast<const uint8_t*>(P + an[i].ecol);
+          for (int o = lane; o < an[i].ncol; o += 64) part[o] = 0.0;
+          wsync();
+          for (int e0 = 0; e0 < ne; e0 += 256) {
+            double t[4];
+            int c[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int e = min(e0 + 64 * u + lane, ne - 1);
+              c[u] = ec8[e];
+              t[u] = A(e) * trow[er8[e]];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (e0 + 64 * u + lane < ne) lds_add(part + c[u], t[u]);
+          }
+        } else {
           const uint8_t* colr = reinterpret_cast<const uint8_t*>(P + an[i].colr);
           const uint32_t* cch = reinterpret_cast<const uint32_t*>(P + an[i].cch);
           const int cchn = an[i].cchn;
@@ -819,8 +867,10 @@ AdmmCfg admm_config(const PlOcpHandle* h) {
   const int matv = segn + T * (T - 1) / 2 * 4;
   lm.colp = o + segn;
 #endif
-  lm.trow = o + up2(h->chunk_max);
-  o += up2(std::max(std::max(matv, up2(h->chunk_max) + h->nrow_max), std::max(h->ncpl_max, 1)));
+  // `part` holds the chunk sums (chunked gathers) or the row / column sums (scatters)
+  const int partn = up2(std::max(h->chunk_max, std::max(h->nrow_max, h->ncol_max)));
+  lm.trow = o + partn;
+  o += up2(std::max(std::max(matv, partn + h->nrow_max), std::max(h->ncpl_max, 1)));
   lm.asb = o;
   // problems per workgroup: 4 puts one wave on every SIMD of every CU once B >= 4 x 256
   c.ppw = h->B >= 1024 ? 4 : (h->B >= 512 ? 2 : 1);
@@ -833,23 +883,26 @@ AdmmCfg admm_config(const PlOcpHandle* h) {
   return c;
 }
 
-template <int PPW, int ASR, bool TIMING = false>
+template <int PPW, int ASR, bool TIMING = false, bool SC = true>
 void launch_admm_t(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)k_admm<PPW, ASR, TIMING>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void*)k_admm<PPW, ASR, TIMING, SC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024);
     attr = true;
   }
   const int grid = (h->B + PPW - 1) / PPW;
-  hipLaunchKernelGGL((k_admm<PPW, ASR, TIMING>), dim3(grid), dim3(64 * PPW), c.lds, h->stream, h->d, h->B, h->N, h->n, h->m,
+  hipLaunchKernelGGL((k_admm<PPW, ASR, TIMING, SC>), dim3(grid), dim3(64 * PPW), c.lds, h->stream, h->d, h->B, h->N, h->n, h->m,
                      h->nnz, h->ndx, h->S_stride, std::max(h->ncpl_max, 1), c.lm, niter, check, h->admm_fwd_asb,
                      h->set.sigma, h->set.alpha);
 }
 
 template <int ASR>
 void launch_admm_a(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
-  if (c.ppw == 4 && ASR == 16 && h->d.dbg) launch_admm_t<4, 16, true>(h, niter, check, c);
+  if (c.ppw == 4 && ASR == 16 && h->d.dbg) {
+    if (h->admm_chunked) launch_admm_t<4, 16, true, false>(h, niter, check, c);
+    else launch_admm_t<4, 16, true, true>(h, niter, check, c);
+  } else if (c.ppw == 4 && ASR == 16 && h->admm_chunked) launch_admm_t<4, 16, false, false>(h, niter, check, c);
   else if (c.ppw == 4) launch_admm_t<4, ASR>(h, niter, check, c);
   else if (c.ppw == 2) launch_admm_t<2, ASR>(h, niter, check, c);
   else launch_admm_t<1, ASR>(h, niter, check, c);

@@ -57,6 +57,35 @@ __global__ __launch_bounds__(64) void k_lag_hess(PlDev d, int N, int n, int m, i
   }
 }
 
+// The same Hessian with one pair per wave and one PROBLEM per lane (grid: pairs x problem
+// groups of 64): the seeds are wave-uniform, so the row code's seed tests (tree passes a pair
+// does not depend on are skipped) are scalar branches and every lane runs the same path.
+template <int DYN>
+__global__ __launch_bounds__(64) void k_lag_hess_pb(PlDev d, int B, int N, int n, int m, int np, long long hl_stride) {
+  const int b = blockIdx.y * 64 + threadIdx.x;
+  if (b >= B || !d.ipinfo[b].active) return;
+  const PlOcpConst& O = *d.oc;
+  const PlModel& M = *d.model;
+  const double* x = d.x + (size_t)b * n;
+  const double* p = d.p + (size_t)b * np;
+  const double* lam = d.ip_lam + (size_t)b * m;
+  double* H = d.Hlag + (size_t)b * hl_stride;
+  const int ndx = O.ndx;
+  HDual kst[PL_KIN_STORE];
+  const int2 w = d.hlist[blockIdx.x];
+  const int i = __builtin_amdgcn_readfirstlane(w.x);
+  const int jk = __builtin_amdgcn_readfirstlane(w.y);
+  const int j = jk & 0xffff, k = jk >> 16;
+  const PlNode nd = d.nodes[i];
+  const PlNode nn = d.nodes[i + 1];
+  VecIn<HDual> dx{x + nd.x_off, nullptr, 0.0, j, k};
+  VecIn<HDual> u{x + nd.x_off + ndx, nullptr, 0.0, j - ndx, k - ndx};
+  VecIn<HDual> dxn{x + nn.x_off, nullptr, 0.0, j - nd.nw, k - nd.nw};
+  HessEmit e{lam + nd.row_off, 0.0, 0};
+  pl::node_rows<HDual, DYN>(M, O, i, p, dx, u, dxn, e, kst, 1);
+  H[d.hoff[i] + k * (k + 1) / 2 + j] = e.acc;
+}
+
 #define PL_DISPATCH_DYN(dyn, KERNEL, ...)                                            \
   switch (dyn) {                                                                      \
     case PL_DYN_RNEA: hipLaunchKernelGGL(KERNEL<PL_DYN_RNEA>, __VA_ARGS__); break;   \
@@ -69,6 +98,11 @@ __global__ __launch_bounds__(64) void k_lag_hess(PlDev d, int N, int n, int m, i
   }
 
 void launch_lag_hess(PlOcpHandle* h) {
+  if (h->hess_pb) {
+    PL_DISPATCH_DYN(h->oc.dyn, k_lag_hess_pb, dim3(h->hl_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->N,
+                    h->n, h->m, h->np, h->hl_stride);
+    return;
+  }
   const int blocks = std::min((h->hl_len + 63) / 64, std::max(1, 2048 / std::max(h->B, 1)));
   PL_DISPATCH_DYN(h->oc.dyn, k_lag_hess, dim3(blocks, h->B), dim3(64), 0, h->stream, h->d, h->N, h->n, h->m, h->np,
                   h->hl_len, h->hl_stride);

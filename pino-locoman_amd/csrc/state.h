@@ -81,7 +81,7 @@ struct PlAdmmNode {
   unsigned kmagic;  // ceil(2^32 / K): t / K == umulhi(t, kmagic) for the tile counts used
   int x_off, row_off, ent_off, s_off;
   int prog, prog_len;
-  int rowe, rowc, colr, cwptr, cwp, cxptr, cxp, ccptr, ccp, xcptr, xcp;
+  int rowe, rowc, colr, ecol, cwptr, cwp, cxptr, cxp, ccptr, ccp, xcptr, xcp;  // ecol: local column of each entry (u8)
   int rchn, rch, rchptr, cchn, cch, cchptr, rchr, cchc;
   int fprog, flen, f_rowptr, f_cplr, f_rowp;
   int f_cwptr, f_cwp, f_xcptr, f_xcp, f_cxptr, f_cxp;  // coupling lists of the factor program
@@ -256,6 +256,7 @@ struct PlOcpHandle {
   int admm_waves;                   // ADMM sweep kernel: 2 = k_admm2 (two waves per problem), 1 = k_admm
   int ruiz_fused;                   // 1: all equilibration passes in k_ruiz_fused (PL_RUIZ_FUSED=0: per-pass kernels)
   int admm_rc;                      // 1: reduced-chain ADMM (k_admm_rc.hip) instead of the sweeps
+  int admm_chunked;                 // 1: k_admm's backward row / column sums by chunked gathers (PL_ADMM_CHUNKED=1) instead of entry-order scatters
   int rc_waves;                     // waves per problem of k_admm_rc (4 or 8)
   long long ch_stride;              // doubles of chain blocks per problem
   int chv_stride;                   // doubles of chain vectors per problem
@@ -264,6 +265,7 @@ struct PlOcpHandle {
   int ip_lam_warm;                  // 1: the next interior-point solve starts from lam = ip_lam0
   int ip_hess;                      // interior point: PL_IP_HESS_EXACT (Lagrangian) or PL_IP_HESS_GN
   int hl_len;                       // Lagrangian Hessian work list (k_lag_hess)
+  int hess_pb;                      // 1: k_lag_hess_pb (one pair per wave, one problem per lane; PL_HESS_PB=1)
   long long hl_stride;              // doubles per problem of d.Hlag
   int fac_hlag;                     // 1: k_fnode adds d.Hlag to Kt_ii and both factor kernels report pivots <= 0
   int fac_only;                     // 1: the factor kernels skip problems whose d.ip_iflag refactor flag is clear
