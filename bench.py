@@ -73,6 +73,34 @@ def admm_bytes_per_problem_iter(sz, node_table, padded=False, kernel="sweep", nd
     return 8.0 * (2 * blk.sum() - blk[0] - blk[-1] + vec)
 
 
+HESS_FLOPS_FILE = os.path.join(HERE, "profiles", "traffic", "hess_flops.json")
+HESS_SOURCES = ("pino-locoman_amd/csrc/k_hess.hip", "pino-locoman_amd/csrc/rows.h", "pino-locoman_amd/csrc/rbd.h",
+                "pino-locoman_amd/csrc/ad.h", "pino-locoman_amd/csrc/targets.h")
+FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 vector (MI355X_MICROARCH.md)
+
+
+def hess_source_sha():
+    h = hashlib.sha256()
+    for rel in HESS_SOURCES:
+        with open(os.path.join(HERE, rel), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def measured_hess_flops(batch, nodes, workload, mapping):
+    """F64 flops per k_lag_hess launch from a committed PMC pass (SQ_INSTS_VALU_{FMA,MUL,ADD}_F64
+    x 64 lanes, an FMA counted as 2), or None if taken on other sources / workload / mapping."""
+    try:
+        with open(HESS_FLOPS_FILE) as fh:
+            tj = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if (tj.get("src_sha") != hess_source_sha() or tj.get("batch") != batch or tj.get("nodes") != nodes
+            or tj.get("workload") != workload or tj.get("mapping") != mapping):
+        return None
+    return tj
+
+
 def traffic_source_sha():
     """sha256 of the k_admm sources: a PMC traffic measurement applies only to the
     kernel revision it was taken on."""
@@ -394,6 +422,21 @@ def main():
         if base is not None:
             out["cpu_baseline"] = base
         if args.solver == "fatrop":
+            # the IP step's dominant kernel is the Lagrangian Hessian (FP64 VALU-bound): its own
+            # roofline; the ADMM sweeps' HBM line above moves to admm_roofline
+            hp = bo.profile_read_hess()
+            h_avg = hp["hess_ms"] / max(1, hp["launches"])
+            mapping = "pb" if os.environ.get("PL_HESS_PB", "0") not in ("", "0") else "pairs"
+            hf = measured_hess_flops(B, args.nodes, workload, mapping)
+            ach = hf["flops_per_launch"] / (h_avg * 1e-3) / 1e12 if (hf and h_avg > 0) else None
+            out["admm_roofline"] = out["roofline"]
+            out["roofline"] = {"bound": "fp64_valu", "kernel": "k_lag_hess", "mapping": mapping, "achieved": ach,
+                               "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                               "frac": ach / FP64_PEAK_TFLOPS if ach is not None else None, "traffic": None,
+                               "avg_launch_ms": h_avg, "launches": hp["launches"],
+                               "flops_per_launch": hf["flops_per_launch"] if hf else None,
+                               "flops_source": (f"profiles/traffic/hess_flops.json (PMC F64 instruction counts, "
+                                                f"src {hf['src_sha']})" if hf else None)}
             ist = bo.ip_stats()  # the last MPC step's solves
             out["ip_stats"] = {"mean_iter": float(np.mean(ist["iter"])),
                                "status_counts": {int(k): int(v) for k, v in

@@ -294,6 +294,9 @@ int pl_ocp_get_admm_kernel(const pl_ocp* o);
  * largest node's A count]. */
 int pl_ocp_profile(pl_ocp* o, int enable);
 int pl_ocp_profile_read(pl_ocp* o, double* out);
+/* The same for the interior point's Lagrangian-Hessian launches (k_lag_hess): out[0] total ms,
+ * out[1] launches (bench.py --solver fatrop: the IP line's roofline kernel). */
+int pl_ocp_profile_read_hess(pl_ocp* o, double* out);
 int pl_ocp_sizes(const pl_ocp* o, long long* out);
 
 /* Test / parity access to internal per-problem arrays and the node table. */

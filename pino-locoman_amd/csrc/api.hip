@@ -1056,8 +1056,15 @@ extern "C" int pl_mpc_download(pl_ocp* o, double* host_dst) {
 }
 
 static void prof_collect(PlOcpHandle* h) {
-  if (!h->profile || h->prof_n == 0) return;
+  if (!h->profile || (h->prof_n == 0 && h->prof_hn == 0)) return;
   hipStreamSynchronize(h->stream);
+  for (int k = 0; k < h->prof_hn; ++k) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, h->prof_hev[k][0], h->prof_hev[k][1]);
+    h->prof_hess_ms += ms;
+    h->prof_hess_launches++;
+  }
+  h->prof_hn = 0;
   for (int k = 0; k < h->prof_n; ++k) {
     float ms = 0.f;
     hipEventElapsedTime(&ms, h->prof_ev[k][0], h->prof_ev[k][1]);
@@ -1086,12 +1093,19 @@ extern "C" int pl_ocp_profile(pl_ocp* o, int enable) {
       hipEventCreate(&h->prof_ev[k][0]);
       hipEventCreate(&h->prof_ev[k][1]);
     }
+    for (int k = 0; k < 16; ++k) {
+      hipEventCreate(&h->prof_hev[k][0]);
+      hipEventCreate(&h->prof_hev[k][1]);
+    }
   }
   h->profile = enable;
   h->prof_n = 0;
   h->prof_admm_ms = 0.0;
   h->prof_admm_launches = 0;
   h->prof_admm_iters = 0;
+  h->prof_hn = 0;
+  h->prof_hess_ms = 0.0;
+  h->prof_hess_launches = 0;
   if (enable) {
     launch_reset_prof(h);
     PL_CHECK_HIP(hipStreamSynchronize(h->stream));
@@ -1114,6 +1128,17 @@ extern "C" int pl_ocp_profile_read(pl_ocp* o, double* out) {
   out[0] = h->prof_admm_ms;
   out[1] = (double)h->prof_admm_launches;
   out[2] = (double)h->prof_admm_iters;
+  return 0;
+}
+
+// Per-launch timing of the interior point's Lagrangian Hessian (k_lag_hess), recorded with the
+// ADMM timing while pl_ocp_profile is on.  out: [total_ms, launches].
+extern "C" int pl_ocp_profile_read_hess(pl_ocp* o, double* out) {
+  REQUIRE_DEVICE(o);
+  if (!out) { pl_set_error("null argument"); return -1; }
+  prof_collect(&o->h);
+  out[0] = o->h.prof_hess_ms;
+  out[1] = (double)o->h.prof_hess_launches;
   return 0;
 }
 

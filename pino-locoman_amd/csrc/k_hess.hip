@@ -98,12 +98,18 @@ __global__ __launch_bounds__(64) void k_lag_hess_pb(PlDev d, int B, int N, int n
   }
 
 void launch_lag_hess(PlOcpHandle* h) {
+  const bool prof = h->profile && h->prof_hn < 16;
+  if (prof) hipEventRecord(h->prof_hev[h->prof_hn][0], h->stream);
   if (h->hess_pb) {
     PL_DISPATCH_DYN(h->oc.dyn, k_lag_hess_pb, dim3(h->hl_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->N,
                     h->n, h->m, h->np, h->hl_stride);
-    return;
+  } else {
+    const int blocks = std::min((h->hl_len + 63) / 64, std::max(1, 2048 / std::max(h->B, 1)));
+    PL_DISPATCH_DYN(h->oc.dyn, k_lag_hess, dim3(blocks, h->B), dim3(64), 0, h->stream, h->d, h->N, h->n, h->m, h->np,
+                    h->hl_len, h->hl_stride);
   }
-  const int blocks = std::min((h->hl_len + 63) / 64, std::max(1, 2048 / std::max(h->B, 1)));
-  PL_DISPATCH_DYN(h->oc.dyn, k_lag_hess, dim3(blocks, h->B), dim3(64), 0, h->stream, h->d, h->N, h->n, h->m, h->np,
-                  h->hl_len, h->hl_stride);
+  if (prof) {
+    hipEventRecord(h->prof_hev[h->prof_hn][1], h->stream);
+    h->prof_hn++;
+  }
 }

@@ -295,6 +295,10 @@ struct PlOcpHandle {
   double prof_admm_ms;
   long long prof_admm_launches;
   long long prof_admm_iters;   // problem-iterations executed by the timed launches (sum of PlProbInfo::iter_prof)
+  hipEvent_t prof_hev[16][2];  // the same for the interior point's Lagrangian-Hessian launches (k_lag_hess)
+  int prof_hn;
+  double prof_hess_ms;
+  long long prof_hess_launches;
 };
 
 // ---- kernel launchers (defined in the k_*.hip translation units)

@@ -90,6 +90,7 @@ EXPORTS = {
     "pl_mpc_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "pl_mpc_export": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pl_mpc_download": (C.c_int, [C.c_void_p, _dp]),
+    "pl_ocp_profile_read_hess": (C.c_int, [C.c_void_p, _dp]),
     "pl_mpc_graph_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong)]),
     "pl_ocp_sync": (C.c_int, [C.c_void_p]),
     "pl_state_integrate": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),

@@ -422,6 +422,11 @@ class BatchedOCP:
         _lib.check(_lib.lib().pl_ocp_profile_read(self.h, _lib.dptr(out)))
         return {"admm_ms": out[0], "launches": int(out[1]), "problem_iters": int(out[2])}
 
+    def profile_read_hess(self):
+        out = np.zeros(2)
+        _lib.check(_lib.lib().pl_ocp_profile_read_hess(self.h, _lib.dptr(out)))
+        return {"hess_ms": out[0], "launches": int(out[1])}
+
     def sizes(self):
         out = (C.c_longlong * 12)()
         _lib.check(_lib.lib().pl_ocp_sizes(self.h, out))
