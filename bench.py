@@ -337,6 +337,7 @@ def main():
             bo.mpc_step(k)
         bo.sync()
     prof = bo.profile_read()
+    hprof = bo.profile_read_hess() if args.solver == "fatrop" else None  # read before profile(0) clears
     bo.profile(0)
     elapsed = pdist.max_over_ranks(elapsed, dist)
     if dist is not None:
@@ -424,9 +425,9 @@ def main():
         if args.solver == "fatrop":
             # the IP step's dominant kernel is the Lagrangian Hessian (FP64 VALU-bound): its own
             # roofline; the ADMM sweeps' HBM line above moves to admm_roofline
-            hp = bo.profile_read_hess()
+            hp = hprof
             h_avg = hp["hess_ms"] / max(1, hp["launches"])
-            mapping = "pb" if os.environ.get("PL_HESS_PB", "0") not in ("", "0") else "pairs"
+            mapping = "pairs" if os.environ.get("PL_HESS_PB", "1") == "0" else "pb"
             hf = measured_hess_flops(B, args.nodes, workload, mapping)
             ach = hf["flops_per_launch"] / (h_avg * 1e-3) / 1e12 if (hf and h_avg > 0) else None
             out["admm_roofline"] = out["roofline"]

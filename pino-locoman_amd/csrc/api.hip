@@ -361,8 +361,8 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
     if (admm_select(o, kind)) { pl_ocp_destroy(o); return -2; }
   }
   o->mpc_graph_off = getenv("PL_MPC_GRAPH") && atoi(getenv("PL_MPC_GRAPH")) == 0;
-  o->h.admm_chunked = getenv("PL_ADMM_CHUNKED") && atoi(getenv("PL_ADMM_CHUNKED")) != 0;  // A/B of k_admm's gathers
-  o->h.hess_pb = getenv("PL_HESS_PB") && atoi(getenv("PL_HESS_PB")) != 0;  // A/B of the Hessian mapping
+  o->h.admm_scatter = getenv("PL_ADMM_SCATTER") ? atoi(getenv("PL_ADMM_SCATTER")) : 0;  // A/B of k_admm's gathers
+  o->h.hess_pb = !(getenv("PL_HESS_PB") && atoi(getenv("PL_HESS_PB")) == 0);  // Hessian mapping (PL_HESS_PB=0: pairs per lane)
   if (hipMemcpy(D.model, &h.model, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(D.oc, &h.oc, sizeof(PlOcpConst), hipMemcpyHostToDevice) != hipSuccess) {
     pl_set_error("upload of model tables failed");

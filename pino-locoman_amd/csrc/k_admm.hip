@@ -36,9 +36,9 @@
 // partials (accumulated per lane over the lane's run of tiles in a tile row) and, off the
 // diagonal, 4 column partials; both go straight into a per-wave LDS accumulator with
 // ds_add_f64 (PL_ADMM_ATOMIC, r02e; the segment / column-partial arrays of r01 remain as
-// the #else branch).  The backward step's A x~ and A^T (rho z - y) scatter the node's
-// entries in storage order into LDS row / column sums (r04; PL_ADMM_CHUNKED=1 keeps the
-// chunked CSR / CSC gathers).  The lanes of one ds_add instruction and the instructions
+// the #else branch).  The backward step's A x~ and A^T (rho z - y) are chunked CSR / CSC
+// gathers; PL_ADMM_SCATTER=1 / 2 (A/B experiments, r04) scatter the node's entries in
+// storage order into LDS row sums / row and column sums instead.  The lanes of one ds_add instruction and the instructions
 // of one wave apply in a fixed order, so results are bit-identical for a problem
 // regardless of the batch or workgroup it runs in.
 #include <algorithm>
@@ -78,7 +78,7 @@ struct AdmmLds {
 
 }  // namespace
 
-template <int PPW, int ASR, bool TIMING, bool SC>
+template <int PPW, int ASR, bool TIMING, int SC>
 __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int n, int m, int nnz, int ndx,
                                                       int S_stride, int cpl_stride, AdmmLds lm, int niter, int check,
                                                       int fwd_asb, double sigma, double alpha) {
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     if (bw) {
       with_A(ne, Ai, [&](auto A) __attribute__((always_inline)) {
         // ---- z~ = A x~
-        if constexpr (SC) {
+        if constexpr (SC >= 1) {
           // entry-order scatter: entry e = lane + 64 k (storage order: column-major, so the lanes
           // of one instruction mostly hit distinct rows) adds A_e x~_c into row r with ds_add_f64;
           // every load is independent (one LDS round trip deep), and row r sums its entries in
@@ -616,7 +616,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
         wsync();
         T(6);
         // ---- A^T (rho z - y)
-        if constexpr (SC) {
+        if constexpr (SC >= 2) {
           // entry-order scatter into the columns (w_i, then the dx_{i+1} part a2); a column's
           // entries are contiguous, so the lanes of one instruction share a few column addresses
           // (applied in lane order); column c sums its rows in row order
@@ -883,7 +883,7 @@ AdmmCfg admm_config(const PlOcpHandle* h) {
   return c;
 }
 
-template <int PPW, int ASR, bool TIMING = false, bool SC = true>
+template <int PPW, int ASR, bool TIMING = false, int SC = 0>
 void launch_admm_t(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
   static bool attr = false;
   if (!attr) {
@@ -899,10 +899,9 @@ void launch_admm_t(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
 
 template <int ASR>
 void launch_admm_a(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
-  if (c.ppw == 4 && ASR == 16 && h->d.dbg) {
-    if (h->admm_chunked) launch_admm_t<4, 16, true, false>(h, niter, check, c);
-    else launch_admm_t<4, 16, true, true>(h, niter, check, c);
-  } else if (c.ppw == 4 && ASR == 16 && h->admm_chunked) launch_admm_t<4, 16, false, false>(h, niter, check, c);
+  if (c.ppw == 4 && ASR == 16 && h->d.dbg) launch_admm_t<4, 16, true>(h, niter, check, c);
+  else if (c.ppw == 4 && ASR == 16 && h->admm_scatter == 1) launch_admm_t<4, 16, false, 1>(h, niter, check, c);
+  else if (c.ppw == 4 && ASR == 16 && h->admm_scatter == 2) launch_admm_t<4, 16, false, 2>(h, niter, check, c);
   else if (c.ppw == 4) launch_admm_t<4, ASR>(h, niter, check, c);
   else if (c.ppw == 2) launch_admm_t<2, ASR>(h, niter, check, c);
   else launch_admm_t<1, ASR>(h, niter, check, c);

@@ -256,7 +256,7 @@ struct PlOcpHandle {
   int admm_waves;                   // ADMM sweep kernel: 2 = k_admm2 (two waves per problem), 1 = k_admm
   int ruiz_fused;                   // 1: all equilibration passes in k_ruiz_fused (PL_RUIZ_FUSED=0: per-pass kernels)
   int admm_rc;                      // 1: reduced-chain ADMM (k_admm_rc.hip) instead of the sweeps
-  int admm_chunked;                 // 1: k_admm's backward row / column sums by chunked gathers (PL_ADMM_CHUNKED=1) instead of entry-order scatters
+  int admm_scatter;                 // k_admm's backward row / column sums: 0 chunked gathers, 1 / 2 entry-order scatters for the rows / rows and columns (PL_ADMM_SCATTER, A/B)
   int rc_waves;                     // waves per problem of k_admm_rc (4 or 8)
   long long ch_stride;              // doubles of chain blocks per problem
   int chv_stride;                   // doubles of chain vectors per problem
@@ -265,7 +265,7 @@ struct PlOcpHandle {
   int ip_lam_warm;                  // 1: the next interior-point solve starts from lam = ip_lam0
   int ip_hess;                      // interior point: PL_IP_HESS_EXACT (Lagrangian) or PL_IP_HESS_GN
   int hl_len;                       // Lagrangian Hessian work list (k_lag_hess)
-  int hess_pb;                      // 1: k_lag_hess_pb (one pair per wave, one problem per lane; PL_HESS_PB=1)
+  int hess_pb;                      // 1 (default): k_lag_hess_pb, one pair per wave and one problem per lane; 0 (PL_HESS_PB=0): one pair per lane
   long long hl_stride;              // doubles per problem of d.Hlag
   int fac_hlag;                     // 1: k_fnode adds d.Hlag to Kt_ii and both factor kernels report pivots <= 0
   int fac_only;                     // 1: the factor kernels skip problems whose d.ip_iflag refactor flag is clear
