@@ -362,6 +362,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   }
   o->mpc_graph_off = getenv("PL_MPC_GRAPH") && atoi(getenv("PL_MPC_GRAPH")) == 0;
   o->h.admm_scatter = getenv("PL_ADMM_SCATTER") ? atoi(getenv("PL_ADMM_SCATTER")) : 0;  // A/B of k_admm's gathers
+  o->h.admm_defer = !(getenv("PL_ADMM_DEFER") && atoi(getenv("PL_ADMM_DEFER")) == 0);  // k_admm's store placement (A/B)
   o->h.hess_pb = !(getenv("PL_HESS_PB") && atoi(getenv("PL_HESS_PB")) == 0);  // Hessian mapping (PL_HESS_PB=0: pairs per lane)
   if (hipMemcpy(D.model, &h.model, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(D.oc, &h.oc, sizeof(PlOcpConst), hipMemcpyHostToDevice) != hipSuccess) {

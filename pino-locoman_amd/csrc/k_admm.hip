@@ -78,7 +78,7 @@ struct AdmmLds {
 
 }  // namespace
 
-template <int PPW, int ASR, bool TIMING, int SC>
+template <int PPW, int ASR, bool TIMING, int SC, bool DS>
 __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int n, int m, int nnz, int ndx,
                                                       int S_stride, int cpl_stride, AdmmLds lm, int niter, int check,
                                                       int fwd_asb, double sigma, double alpha) {
@@ -349,12 +349,65 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     wsync();
   };
 
+  // ---------------- the stores of a step (bt of a forward step; rows z, y (dy) and columns x
+  // (dx), rhs of a backward step).  Issued at the step's end, the next step's vmcnt(0) also
+  // waits for their retirement (stores count in vmcnt, in issue order); with DS (default,
+  // PL_ADMM_DEFER=0 turns it off) they are issued right after that wait, from registers
+  // carried across the boundary, so the wait covers only loads and the stores retire
+  // behind a whole step (profiles/r04o: 24.12 -> 23.46 ms per launch at the headline).
+  struct StoreSet {
+    double kz[MR], ky[MR], kd[MR], kb[MV];
+    double2 pxa, pdx, prh;
+    double prn;
+    int kind, i;
+    bool delta;
+  };
+  StoreSet pend;
+  pend.kind = -1;
+  auto issue_stores = [&](const StoreSet& ss) __attribute__((always_inline)) {
+    const int kind = ss.kind, i = ss.i;
+    const bool bw = bwd_kind(kind);
+    const int nw = an[i].nw, x_off = an[i].x_off;
+    if (!bw || kind == KT0) {  // bt_i of a forward (part of a) step
+#pragma unroll
+      for (int mm = 0; mm < MV; ++mm)
+        if (lane + 64 * mm < nw) gst(bt, x_off + lane + 64 * mm, ss.kb[mm]);
+    }
+    if (bw) {  // rows of node i
+      const int nrow = an[i].nrow, ro = an[i].row_off;
+#pragma unroll
+      for (int mm = 0; mm < MR; ++mm) {
+        const int r = lane + 64 * mm;
+        if (r < nrow) {
+          gst(za, ro + r, ss.kz[mm]);
+          gst(ya, ro + r, ss.ky[mm]);
+          if (ss.delta) gst(dys, ro + r, ss.kd[mm]);
+        }
+      }
+    }
+    if (bw || kind == KTN) {  // x update and rhs of node i
+      const int xnx = bw ? an[i + 1].x_off : 0;
+#pragma unroll
+      for (int mm = 0; mm < MV; ++mm) {
+        const int c = lane + 64 * mm;
+        if (c < nw) {
+          gst(xa, x_off + c, sel2(ss.pxa, mm));
+          if (ss.delta) gst(dxs, x_off + c, sel2(ss.pdx, mm));
+          if (bw) {
+            if (c < ndx) gst(rhs, xnx + c, ss.prn);
+            if (!(c < ndx && i > 0)) gst(rhs, x_off + c, sel2(ss.prh, mm));
+          }
+        }
+      }
+    }
+  };
+
   // ---------------- one step of the schedule
   auto step = [&](int q) __attribute__((always_inline)) {
-    // Every store of a step is issued at its end: on CDNA4 a store's source VGPRs may be
-    // reused only after its vmcnt retires, so a mid-step store followed by register
-    // reuse would wait vmcnt(0) and drain the factor stream.  At the end the reuse
-    // happens after the next step's own vmcnt(0).
+    // No store is issued mid-step: on CDNA4 a store's source VGPRs may be reused only after
+    // its vmcnt retires, so a mid-step store followed by register reuse would wait and drain
+    // the factor stream.  The step's results go out after the next step's vmcnt(0) (DS, the
+    // default since r04: 24.1 -> 23.5 ms per launch) or at the step's end (DS off).
     double kz[MR], ky[MR], kd[MR], kb[MV];
 #pragma unroll
     for (int mm = 0; mm < MR; ++mm) kz[mm] = ky[mm] = kd[mm] = 0.0;
@@ -404,6 +457,9 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     E = En;
     LR = LRn;
     LC = LCn;
+    if constexpr (DS) {
+      if (pend.kind >= 0) issue_stores(pend);  // step q-1's stores, behind its wait
+    }
     if (bw) stage(ne, Ai);
     else if (fwd_asb && kind != KF0) stage(an[i - 1].nent, As + an[i - 1].ent_off);
     T(0);
@@ -745,38 +801,17 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
       fix1 = true;
     }
     wsync();
-    // ---- the step's stores
-    if (!bw || kind == KT0) {  // bt_i of a forward (part of a) step
+    // ---- the step's stores (now, or deferred behind the next step's wait)
+    {
+      StoreSet cur;
 #pragma unroll
-      for (int mm = 0; mm < MV; ++mm)
-        if (lane + 64 * mm < nw) gst(bt, x_off + lane + 64 * mm, kb[mm]);
-    }
-    if (bw) {  // rows of node i
-      const int nrow = an[i].nrow, ro = an[i].row_off;
+      for (int mm = 0; mm < MR; ++mm) { cur.kz[mm] = kz[mm]; cur.ky[mm] = ky[mm]; cur.kd[mm] = kd[mm]; }
 #pragma unroll
-      for (int mm = 0; mm < MR; ++mm) {
-        const int r = lane + 64 * mm;
-        if (r < nrow) {
-          gst(za, ro + r, kz[mm]);
-          gst(ya, ro + r, ky[mm]);
-          if (store_delta) gst(dys, ro + r, kd[mm]);
-        }
-      }
-    }
-    if (bw || kind == KTN) {  // x update and rhs of node i
-      const int xnx = bw ? an[i + 1].x_off : 0;
-#pragma unroll
-      for (int mm = 0; mm < MV; ++mm) {
-        const int c = lane + 64 * mm;
-        if (c < nw) {
-          gst(xa, x_off + c, sel2(pxa, mm));
-          if (store_delta) gst(dxs, x_off + c, sel2(pdx, mm));
-          if (bw) {
-            if (c < ndx) gst(rhs, xnx + c, prn);
-            if (!(c < ndx && i > 0)) gst(rhs, x_off + c, sel2(prh, mm));
-          }
-        }
-      }
+      for (int mm = 0; mm < MV; ++mm) cur.kb[mm] = kb[mm];
+      cur.pxa = pxa; cur.pdx = pdx; cur.prh = prh; cur.prn = prn;
+      cur.kind = kind; cur.i = i; cur.delta = store_delta;
+      if constexpr (DS) pend = cur;
+      else issue_stores(cur);
     }
     T(9);
   };
@@ -787,6 +822,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   prefetch_LC(KF0, 0, LCn);
   load_S(0, 0, SR);
   for (int q = 0; q < Q; ++q) step(q);
+  if constexpr (DS) issue_stores(pend);
   if (lane == 0) {
     info->iter += niter;
     info->iter_prof += niter;  // only problems still iterating reach here (done ones return above)
@@ -883,16 +919,16 @@ AdmmCfg admm_config(const PlOcpHandle* h) {
   return c;
 }
 
-template <int PPW, int ASR, bool TIMING = false, int SC = 0>
+template <int PPW, int ASR, bool TIMING = false, int SC = 0, bool DS = false>
 void launch_admm_t(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)k_admm<PPW, ASR, TIMING, SC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void*)k_admm<PPW, ASR, TIMING, SC, DS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024);
     attr = true;
   }
   const int grid = (h->B + PPW - 1) / PPW;
-  hipLaunchKernelGGL((k_admm<PPW, ASR, TIMING, SC>), dim3(grid), dim3(64 * PPW), c.lds, h->stream, h->d, h->B, h->N, h->n, h->m,
+  hipLaunchKernelGGL((k_admm<PPW, ASR, TIMING, SC, DS>), dim3(grid), dim3(64 * PPW), c.lds, h->stream, h->d, h->B, h->N, h->n, h->m,
                      h->nnz, h->ndx, h->S_stride, std::max(h->ncpl_max, 1), c.lm, niter, check, h->admm_fwd_asb,
                      h->set.sigma, h->set.alpha);
 }
@@ -900,6 +936,8 @@ void launch_admm_t(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
 template <int ASR>
 void launch_admm_a(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
   if (c.ppw == 4 && ASR == 16 && h->d.dbg) launch_admm_t<4, 16, true>(h, niter, check, c);
+  else if (c.ppw == 4 && ASR == 16 && h->admm_defer && h->admm_scatter == 1) launch_admm_t<4, 16, false, 1, true>(h, niter, check, c);
+  else if (c.ppw == 4 && ASR == 16 && h->admm_defer && h->admm_scatter == 0) launch_admm_t<4, 16, false, 0, true>(h, niter, check, c);
   else if (c.ppw == 4 && ASR == 16 && h->admm_scatter == 1) launch_admm_t<4, 16, false, 1>(h, niter, check, c);
   else if (c.ppw == 4 && ASR == 16 && h->admm_scatter == 2) launch_admm_t<4, 16, false, 2>(h, niter, check, c);
   else if (c.ppw == 4) launch_admm_t<4, ASR>(h, niter, check, c);

@@ -256,6 +256,7 @@ struct PlOcpHandle {
   int admm_waves;                   // ADMM sweep kernel: 2 = k_admm2 (two waves per problem), 1 = k_admm
   int ruiz_fused;                   // 1: all equilibration passes in k_ruiz_fused (PL_RUIZ_FUSED=0: per-pass kernels)
   int admm_rc;                      // 1: reduced-chain ADMM (k_admm_rc.hip) instead of the sweeps
+  int admm_defer;                   // 1 (default): k_admm issues a step's stores after the next step's wait; 0 (PL_ADMM_DEFER=0): at the step's end
   int admm_scatter;                 // k_admm's backward row / column sums: 0 chunked gathers, 1 / 2 entry-order scatters for the rows / rows and columns (PL_ADMM_SCATTER, A/B)
   int rc_waves;                     // waves per problem of k_admm_rc (4 or 8)
   long long ch_stride;              // doubles of chain blocks per problem
