@@ -723,16 +723,76 @@ void probe_pairs(const Problem& pr, int i, std::vector<std::pair<int, int>>& out
     }
 }
 
-// H_L blocks at (x, lam): hv[pair] = sum_r lam_r g_r.c over the node's rows
+// whole_body_rnea: the (dq, a) and (dq, f_feet) blocks of node i from two dual tree passes per
+// dq column (d/dq_k of M(q) lambda_tau and of -J_e(q) lambda_tau; the same restatement of the
+// linearity in a and f as the GPU's k_lag_hess_lin).  lin[k * nlin + c] for the columns
+// c = 0 .. na + 3 nfeet - 1 after dx.
+struct ZeroInH {
+  Dual operator[](int) const { return Dual(0.0, 0.0); }
+};
+struct LamInH {
+  const double* lb;
+  const double* lt;
+  Dual operator[](int k) const { return Dual(k < 6 ? lb[k] : (lt ? lt[k - 6] : 0.0), 0.0); }
+};
+void rnea_lin_block(const Problem& pr, const PlModel& M0, const double* p, const double* x, const double* lam, int i,
+                    double* lin) {
+  const PlOcpConst& O = pr.O;
+  const int t = pl::node_type(O, i);
+  int rbb = -1, rbt = -1, r = 0;
+  for (int bi = 0; bi < O.nblk[t]; ++bi) {
+    if (O.blk[t][bi].kind == PL_RB_RNEA_BASE) rbb = r;
+    if (O.blk[t][bi].kind == PL_RB_TAU_EQ) rbt = r;
+    r += O.blk[t][bi].count;
+  }
+  const double* ln = lam + pr.row_off[i];
+  const LamInH lt{ln + rbb, rbt >= 0 ? ln + rbt : nullptr};
+  const double* xi = p + O.P.x_init;
+  const int nv = O.nv, nlin = O.na + 3 * O.nfeet;
+  Dual kst[PL_KIN_STORE];
+  for (int k = 0; k < nv; ++k) {
+    double* row = lin + (size_t)k * nlin;
+    if (k < 3) {  // RNEA and the foot velocities ignore the base position
+      for (int c = 0; c < nlin; ++c) row[c] = 0.0;
+      continue;
+    }
+    const pl::VecIn<Dual> dq{x + pr.x_off[i], nullptr, 0.0, k};
+    Dual qb[7];
+    pl::integrate_ff<Dual>(xi, dq, qb);
+    const pl::RevQ<Dual, pl::VecIn<Dual>> qrev{xi, dq};
+    pl::NodeKin<Dual> kin;
+    kin.vst = reinterpret_cast<double*>(kst);
+    kin.dst = kin.vst + 1;
+    kin.vstride = kin.dstride = 2;
+    pl::tree_pass<Dual>(M0, O, qb, qrev, ZeroInH{}, lt, ZeroInH{}, true, false, kin);
+    for (int j = 0; j < nv; ++j) row[j] = j < 6 ? kin.tau[j].d : Dual(kin.tau_j(j - 6)).d;
+    pl::tree_pass<Dual>(pr.M, O, qb, qrev, lt, ZeroInH{}, ZeroInH{}, false, true, kin);
+    for (int e = 0; e < O.nfeet; ++e)
+      for (int c = 0; c < 3; ++c) row[O.na + 3 * e + c] = -Dual(kin.foot_vel(e, c)).d;
+  }
+}
+
+// H_L blocks at (x, lam): hv[pair] = sum_r lam_r g_r.c over the node's rows (whole_body_rnea:
+// the (dq, a) / (dq, f_feet) pairs from rnea_lin_block instead)
 template <int DYN>
 void lag_hess(const Problem& pr, const double* p, const double* x, const double* lam, double* hv) {
   HDual kst[PL_KIN_STORE];
   const int ndx = pr.O.ndx;
+  const bool lin = DYN == PL_DYN_RNEA;
+  const int nlin = pr.O.na + 3 * pr.O.nfeet;
+  std::vector<double> linb(lin ? (size_t)pr.O.nv * nlin : 0);
+  PlModel M0 = pr.M;
+  for (int k = 0; k < 3; ++k) M0.gravity[k] = 0.0;
   for (int i = 0; i < pr.N; ++i) {
     const auto& pl_ = pr.hpairs[pl::node_type(pr.O, i)];
     const int xo = pr.x_off[i], xn = pr.x_off[i + 1], nw = pr.nw[i];
+    if (lin) rnea_lin_block(pr, M0, p, x, lam, i, linb.data());
     for (size_t q = 0; q < pl_.size(); ++q) {
       const int j = pl_[q].first, k = pl_[q].second;
+      if (lin && j < pr.O.nv && k >= ndx && k < ndx + nlin) {
+        hv[pr.ik_H_off[i] + q] = linb[(size_t)j * nlin + (k - ndx)];
+        continue;
+      }
       pl::VecIn<HDual> dx{x + xo, nullptr, 0.0, j, k};
       pl::VecIn<HDual> u{x + xo + ndx, nullptr, 0.0, j - ndx, k - ndx};
       pl::VecIn<HDual> dxn{x + xn, nullptr, 0.0, j - nw, k - nw};

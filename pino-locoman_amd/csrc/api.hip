@@ -729,11 +729,17 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
     // Lagrangian Hessian work list (k_hess.hip): the structurally non-zero column pairs
     // j <= k of every w_i block (hess_pattern, one probe per node type); node blocks packed
     // lower, the pairs not listed stay 0
-    std::vector<int2> hl;
+    std::vector<int2> hl, hlin;
     std::vector<int> hoff;
     long long off = 0;
     const PlOcpConst& O = h->oc;
     std::vector<uint8_t> pat[3];
+    // whole_body_rnea: the rows are linear in a and in the contact forces, and only the RNEA rows
+    // couple them to q, so the (dq, a) and (dq, f_feet) blocks are d/dq of M(q) lambda_tau and
+    // of -J_e(q) lambda_tau (k_lag_hess_lin: two dual tree passes per dq column instead of one
+    // hyper-dual pass per pair); PL_HESS_LIN=0 keeps them as pairs
+    const bool lin = O.dyn == PL_DYN_RNEA && !(getenv("PL_HESS_LIN") && atoi(getenv("PL_HESS_LIN")) == 0);
+    const int lin_lo = O.ndx, lin_hi = O.ndx + O.na + 3 * O.nfeet;
     for (int i = 0; i <= h->N; ++i) {
       const int nw = o->nodes[i].nw;
       hoff.push_back((int)off);
@@ -742,14 +748,35 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
       const int type = pl::node_type(O, i);
       if (pat[type].empty()) hess_pattern(*h, o->nodes, i, pat[type]);
       for (int k = 0; k < nw; ++k)
-        for (int j = 0; j <= k; ++j)
+        for (int j = 0; j <= k; ++j) {
+          if (lin && j < O.nv && k >= lin_lo && k < lin_hi) continue;
           if (pat[type][(size_t)k * (k + 1) / 2 + j]) hl.push_back(make_int2(i, j | (k << 16)));
+        }
+      if (lin)
+        for (int k = 3; k < O.nv; ++k) hlin.push_back(make_int2(i, k));  // RNEA ignores the base position
+    }
+    for (int t = 0; t < 3; ++t) {  // first row of the RNEA base / joint-torque row blocks per node type
+      h->hl_rb_base[t] = h->hl_rb_tau[t] = -1;
+      int r = 0;
+      for (int bi = 0; bi < O.nblk[t]; ++bi) {
+        if (O.blk[t][bi].kind == PL_RB_RNEA_BASE) h->hl_rb_base[t] = r;
+        if (O.blk[t][bi].kind == PL_RB_TAU_EQ) h->hl_rb_tau[t] = r;
+        r += O.blk[t][bi].count;
+      }
     }
     h->hl_len = (int)hl.size();
+    h->hlin_len = (int)hlin.size();
     h->hl_stride = (off + 1) & ~1LL;
     if (upload(o, &h->d.hlist, hl) || upload(o, &h->d.hoff, hoff) ||
         dalloc(o, &h->d.Hlag, (size_t)h->B * h->hl_stride))
       return -2;
+    if (lin) {
+      PlModel m0 = h->model;
+      for (int k = 0; k < 3; ++k) m0.gravity[k] = 0.0;
+      if (upload(o, &h->d.hlin, hlin) || dalloc(o, &h->d.model0, 1) ||
+          hipMemcpy(h->d.model0, &m0, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess)
+        return -2;
+    }
   }
   h->solver = solver;
   return 0;

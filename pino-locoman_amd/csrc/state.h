@@ -224,6 +224,8 @@ struct PlDev {
   double* ip_lam0;   // lam_g warm start (opti.set_initial(opti.lam_g, lam_g), ocp_whole_body_rnea.py:234-235)
   // exact Lagrangian Hessian (k_hess.hip) and its inertia correction (k_ip.hip)
   int2* hlist;       // (node, j | k << 16) column pairs of the w_i blocks
+  int2* hlin;        // whole_body_rnea: (node, dq column k) of the linear-column Hessian blocks (k_lag_hess_lin)
+  PlModel* model0;   // the model with zero gravity (M(q) lambda by an RNEA pass at v = 0)
   int* hoff;         // packed-lower offset of node i's block
   double* Hlag;      // [B][hl_stride] sum_r lam_r d^2 g_r / dw_i^2, packed lower per node
   double* ip_dwi;    // [B][2]: the inertia shift of this Newton system, the last nonzero one
@@ -266,6 +268,8 @@ struct PlOcpHandle {
   int ip_lam_warm;                  // 1: the next interior-point solve starts from lam = ip_lam0
   int ip_hess;                      // interior point: PL_IP_HESS_EXACT (Lagrangian) or PL_IP_HESS_GN
   int hl_len;                       // Lagrangian Hessian work list (k_lag_hess)
+  int hlin_len;                     // k_lag_hess_lin work list (0: every pair by hyper-dual passes)
+  int hl_rb_base[3], hl_rb_tau[3];  // per node type: first row of the RNEA base / joint-torque rows (-1: none)
   int hess_pb;                      // 1 (default): k_lag_hess_pb, one pair per wave and one problem per lane; 0 (PL_HESS_PB=0): one pair per lane
   long long hl_stride;              // doubles per problem of d.Hlag
   int fac_hlag;                     // 1: k_fnode adds d.Hlag to Kt_ii and both factor kernels report pivots <= 0
