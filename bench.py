@@ -213,8 +213,9 @@ def cpu_baseline_ip(robot, dynamics, N, per_core=1, n_steps=1):
             "sample": f"{B} problems x {n_steps} MPC step(s) of the same workload (seeds 0..{B - 1}, the loop's first "
                       f"solve: cold lam_g) on {threads} OpenMP threads; compiled C++ restatement of the interior-point "
                       f"stand-in for the reference's Fatrop branch (oracle/cpu/sqp_cpu.cpp restating oracle/ip_ref.py: "
-                      f"exact Lagrangian Hessian by hyper-dual passes over {pairs} column pairs, QDLDL LDL^T on the "
-                      f"KKT, IPOPT inertia correction, filter line search), not Fatrop; g++ -O3 -march=x86-64-v3",
+                      f"exact Lagrangian Hessian by hyper-dual passes over {pairs} column pairs, whole_body_rnea's "
+                      f"(dq, a) / (dq, f_feet) blocks by dual passes as on the GPU, QDLDL LDL^T on the KKT, IPOPT "
+                      f"inertia correction, filter line search), not Fatrop; g++ -O3 -march=x86-64-v3",
             "per_thread_s_per_solve": wall * threads / (B * n_steps), "mean_iter": float(st[:, :, 1].mean()),
             "cpu_model": _cpu_model(), "host_cpus_visible": avail, "omp_num_threads_env": env,
             "cgroup_cpu_quota": _cgroup_cpu_quota()}
