@@ -935,7 +935,8 @@ void launch_admm_t(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
 
 template <int ASR>
 void launch_admm_a(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
-  if (c.ppw == 4 && ASR == 16 && h->d.dbg) launch_admm_t<4, 16, true>(h, niter, check, c);
+  if (c.ppw == 4 && ASR == 16 && h->d.dbg && h->admm_defer) launch_admm_t<4, 16, true, 0, true>(h, niter, check, c);
+  else if (c.ppw == 4 && ASR == 16 && h->d.dbg) launch_admm_t<4, 16, true>(h, niter, check, c);
   else if (c.ppw == 4 && ASR == 16 && h->admm_defer && h->admm_scatter == 1) launch_admm_t<4, 16, false, 1, true>(h, niter, check, c);
   else if (c.ppw == 4 && ASR == 16 && h->admm_defer && h->admm_scatter == 0) launch_admm_t<4, 16, false, 0, true>(h, niter, check, c);
   else if (c.ppw == 4 && ASR == 16 && h->admm_scatter == 1) launch_admm_t<4, 16, false, 1>(h, niter, check, c);
