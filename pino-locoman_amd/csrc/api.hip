@@ -303,13 +303,25 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= upload(o, &D.kfl, o->kfl);
   rc |= upload(o, &D.kcpl, o->kcpl);
   {
-    std::vector<int2> jl;
-    if (build_jac_list(o, jl)) {
+    std::vector<int2> jl, jlin;
+    // PL_JAC_LIN=0 keeps the rnea a / f columns as dual tree-pass lanes (A/B)
+    const bool use_lin = !(getenv("PL_JAC_LIN") && atoi(getenv("PL_JAC_LIN")) == 0);
+    if (build_jac_list(o, jl, jlin, use_lin)) {
       pl_ocp_destroy(o);
       return -1;
     }
     h.jl_len = (int)jl.size();
+    h.jlin_len = (int)jlin.size();
     rc |= upload(o, &D.jlist, jl);
+    D.jlin = nullptr;
+    D.model0 = nullptr;
+    if (!jlin.empty()) {
+      rc |= upload(o, &D.jlin, jlin);
+      PlModel m0 = h.model;  // zero gravity: the primal RNEA pass is then linear in (a, f)
+      for (int k = 0; k < 3; ++k) m0.gravity[k] = 0.0;
+      rc |= dalloc(o, &D.model0, 1);
+      if (!rc && hipMemcpy(D.model0, &m0, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess) rc = 1;
+    }
   }
   const size_t n = h.n, m = h.m, nnz = h.nnz;
   rc |= dalloc(o, &D.p, B * h.np);
@@ -773,8 +785,9 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
     if (lin) {
       PlModel m0 = h->model;
       for (int k = 0; k < 3; ++k) m0.gravity[k] = 0.0;
-      if (upload(o, &h->d.hlin, hlin) || dalloc(o, &h->d.model0, 1) ||
-          hipMemcpy(h->d.model0, &m0, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess)
+      if (upload(o, &h->d.hlin, hlin)) return -2;
+      if (!h->d.model0 && (dalloc(o, &h->d.model0, 1) ||
+                           hipMemcpy(h->d.model0, &m0, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess))
         return -2;
     }
   }

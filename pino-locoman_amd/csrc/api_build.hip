@@ -835,9 +835,10 @@ int build_factor_prog(pl_ocp* o) {
 // 64 per wave ACROSS node boundaries and padded to whole waves; then the columns that
 // skip it (dx_{i+1}; rnea tau_j; centroidal h), which are cheap.  The classification
 // mirrors node_rows' skip logic (rows.h); it only affects the schedule.
-int build_jac_list(pl_ocp* o, std::vector<int2>& list) {
+int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, bool use_lin) {
   const PlOcpConst& O = o->h.oc;
   std::vector<int2> ex, ch;
+  lin.clear();
   for (int i = 0; i < o->h.N; ++i) {
     const PlNode& nd = o->nodes[i];
     const int* cp = o->colptr.data() + nd.colptr_off;
@@ -851,6 +852,10 @@ int build_jac_list(pl_ocp* o, std::vector<int2>& list) {
       } else {
         const int k = lc - O.ndx;
         cheap = PL_IS_RNEA(O.dyn) && k >= O.na + O.nf;
+        if (use_lin && PL_IS_RNEA(O.dyn) && !cheap) {  // a / f: linear in the RNEA (k_eval_jac_lin)
+          lin.push_back(make_int2(i, lc));
+          continue;
+        }
       }
       (cheap ? ch : ex).push_back(make_int2(i, lc));
     }
@@ -867,5 +872,6 @@ int build_jac_list(pl_ocp* o, std::vector<int2>& list) {
   }
   list = ex;
   list.insert(list.end(), ch.begin(), ch.end());
+  while (lin.size() % 64) lin.push_back(make_int2(-1, -1));
   return 0;
 }

@@ -73,7 +73,8 @@ void build_blocks(PlOcpConst& O, bool has_ext, bool has_arm);
 int build_layout(pl_ocp* o);
 int build_admm_prog(pl_ocp* o);
 int build_factor_prog(pl_ocp* o);
-int build_jac_list(pl_ocp* o, std::vector<int2>& list);
+// lin (use_lin, rnea): the a / f columns, for k_eval_jac_lin, instead of tree-pass lanes in list
+int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, bool use_lin);
 // api_casadi.hip: drop the CasADi binding of an OCP that is being destroyed
 void cas_forget(const pl_ocp* o);
 void jac_pattern(const PlOcpHandle& h, const std::vector<PlNode>& nodes, int i, std::vector<uint8_t>& nz);

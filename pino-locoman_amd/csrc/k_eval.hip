@@ -134,6 +134,62 @@ void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz, int jl_len) {
                            kst_val + slot * PL_KIN_STORE_DUAL, aba_slot);
 }
 
+namespace {
+struct ZeroInD {
+  PL_HD double operator[](int) const { return 0.0; }
+};
+struct UnitIn {  // e_k (k < 0: zero)
+  int k;
+  PL_HD double operator[](int j) const { return j == k ? 1.0 : 0.0; }
+};
+}  // namespace
+
+// The RNEA's acceleration and contact-force columns (whole_body_rnea): tau is linear in a
+// and f, so d tau / d a_k = M(q) e_k and d tau / d f_c = -J_c(q)^T e_c are one primal
+// RNEA pass of the zero-gravity model at v = 0 with a = e_k (or f = e_c) instead of a dual
+// tree pass (ocp_whole_body_rnea.py:207-235, pin.rnea with the contact forces).  One lane =
+// one (node, column) of d.jlin (api_build.hip build_jac_list); the pass leaves the joint
+// torques in the first nj slots of the lane's store, which node_rows then reads as tangents.
+template <int DYN>
+__global__ __launch_bounds__(64) void k_eval_jac_lin(PlDev d, int B, int n, int np, int nnz, int len) {
+  const int b = blockIdx.y;
+  const int q = (int)blockIdx.x * 64 + threadIdx.x;
+  __shared__ double kst[PL_KIN_STORE * 64];
+  __shared__ double kval[PL_KIN_STORE];  // the (unused) values of the kinematic outputs
+  for (int k = threadIdx.x; k < PL_KIN_STORE; k += 64) kval[k] = 0.0;
+  __syncthreads();
+  if (q >= len) return;
+  const int2 jw = d.jlin[q];
+  if (jw.x < 0) return;
+  const int i = jw.x, lc = jw.y;
+  const PlOcpConst& O = *d.oc;
+  const PlNode nd = d.nodes[i];
+  const PlNode nn = d.nodes[i + 1];
+  const int ndx = O.ndx;
+  const double* x = d.x + (size_t)b * n;
+  const double* p = d.p + (size_t)b * np;
+  const double* xi = p + O.P.x_init;
+  const VecIn<double> dq{x + nd.x_off, nullptr, 0.0, -1};
+  double qb[7];
+  pl::integrate_ff<double>(xi, dq, qb);
+  const pl::RevQ<double, VecIn<double>> qrev{xi, dq};
+  pl::NodeKin<double> kp;
+  kp.store = kst + threadIdx.x;
+  kp.stride = 64;
+  const int k = lc - ndx;  // a_k, or force component k - na
+  pl::tree_pass<double>(*d.model0, O, qb, qrev, ZeroInD{}, UnitIn{k < O.na ? k : -1}, UnitIn{k - O.na}, true, false,
+                        kp);
+  double base[6];
+  for (int r = 0; r < 6; ++r) base[r] = kp.tau[r];
+  const int* cp = d.colptr + nd.colptr_off;
+  VecIn<Dual> dx{x + nd.x_off, nullptr, 0.0, lc};
+  VecIn<Dual> u{x + nd.x_off + ndx, nullptr, 0.0, lc - ndx};
+  VecIn<Dual> dxn{x + nn.x_off, nullptr, 0.0, lc - nd.nw};
+  JacEmit e{d.rowidx + nd.ent_off, d.Araw + (size_t)b * nnz + nd.ent_off, cp[lc], cp[lc + 1], 0};
+  pl::node_rows<Dual, DYN>(*d.model, O, i, p, dx, u, dxn, e, reinterpret_cast<Dual*>(kst + threadIdx.x), 64, kval,
+                           nullptr, base);
+}
+
 __global__ __launch_bounds__(256) void k_objective(PlDev d, int N, int n, int np) {
   const int b = blockIdx.x;
   __shared__ double red[256];
@@ -183,6 +239,15 @@ void launch_eval_values(PlOcpHandle* h, const double* xsrc) {
 }
 
 void launch_eval_jac(PlOcpHandle* h) {
+  if (h->jlin_len > 0) {
+    const dim3 g((h->jlin_len + 63) / 64, h->B);
+    if (h->oc.dyn == PL_DYN_RNEA)
+      hipLaunchKernelGGL(k_eval_jac_lin<PL_DYN_RNEA>, g, dim3(64), 0, h->stream, h->d, h->B, h->n, h->np, h->nnz,
+                         h->jlin_len);
+    else
+      hipLaunchKernelGGL(k_eval_jac_lin<PL_DYN_RNEAFD>, g, dim3(64), 0, h->stream, h->d, h->B, h->n, h->np, h->nnz,
+                         h->jlin_len);
+  }
   PL_DISPATCH_DYN(h->oc.dyn, k_eval_jac, dim3((h->jl_len + 63) / 64, h->B), dim3(64), 0, h->stream, h->d, h->B,
                   h->N, h->n, h->np, h->nnz, h->jl_len);
 }

@@ -142,10 +142,14 @@ PL_HD void chol_solve(const double* L, int n, double* x) {
 // null keeps values and tangents interleaved in kstore.  aba_sh (Dual, ABA only): the
 // node's shared primal (PL_ABA_SH); the ABA tangent then comes from the implicit
 // function M a' = [0; tau_j'] - RNEA'(q', v', f' | a) instead of a dual ABA.
+// lin_base (Dual, rnea, a column seeded on a or f only): the RNEA is linear in that input,
+// so the caller took the torque tangent from a primal pass instead of the dual tree pass:
+// lin_base holds the 6 base torques' tangents and the first nj tangent slots of kstore the
+// joint torques' (k_eval_jac_lin); every other kinematic tangent of such a column is zero.
 template <class S, int DYN, class Emit>
 PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double* p, const VecIn<S>& dx,
                      const VecIn<S>& u, const VecIn<S>& dxn, Emit& emit, S* kstore, int kstride,
-                     double* kvals = nullptr, const double* aba_sh = nullptr) {
+                     double* kvals = nullptr, const double* aba_sh = nullptr, const double* lin_base = nullptr) {
   const int nv = O.nv, nq = O.nq, nj = O.nj;
   constexpr bool CV = PL_IS_CV(DYN);
   constexpr bool CVNB = (DYN == PL_DYN_CVNB);  // v = [base_vel_dynamics(h, q, v_j), v_j]
@@ -228,8 +232,10 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
     // (without the base, h enters the kinematics through v_b; its centroidal pass ran above)
     const bool seed_h = DYN == PL_DYN_CV && seeded(dx, 0, 6);
     const bool seed_f = CV && seeded(u, f_off, f_off + O.nf);
-    tree = !(seed_dxn || seed_tau || seed_h || seed_f);
+    tree = !(seed_dxn || seed_tau || seed_h || seed_f) && !lin_base;
     cen = DYN == PL_DYN_CV && !(seed_dxn || seed_h);
+  } else {
+    (void)lin_base;
   }
   S comp[COMP ? 15 : 1];
   S aba_a[DYN == PL_DYN_ABA ? PL_MAXV : 1];
@@ -267,11 +273,14 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
       tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin);
     }
   } else {  // a skipped pass leaves zero (value and tangent) kinematic outputs
-    for (int k = 0; k < PL_KIN_STORE_DUAL; ++k) kin.clear(k);
+    for (int k = lin_base ? nj : 0; k < PL_KIN_STORE_DUAL; ++k) kin.clear(k);
     for (int k = 0; k < 3; ++k) kin.arm_vel[k] = S(0.0);
     for (int k = 0; k < 6; ++k) kin.tau[k] = S(0.0);
     if constexpr (COMP)
       for (int k = 0; k < 15; ++k) comp[k] = S(0.0);
+    if constexpr (std::is_same<S, Dual>::value)
+      if (lin_base)
+        for (int k = 0; k < 6; ++k) kin.tau[k] = Dual(0.0, lin_base[k]);
   }
   // acc family: the base acceleration (include_base = False) or the centroidal gap
   S abase[NB ? 6 : 1], cgap[DYN == PL_DYN_CA ? 6 : 1];

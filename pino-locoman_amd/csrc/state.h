@@ -179,6 +179,7 @@ struct PlDev {
   double* chv;           // reduced-chain vectors [B][chv_stride] (k_admm_rc)
   uint32_t* ttab;        // lane-tile tables [64][PL_ADMM_KM] per distinct (T, K): (I << 24) | (J << 16) | cidx
   int2* jlist;           // k_eval_jac work list: (node, local column), tree-pass columns first (whole waves)
+  int2* jlin;            // k_eval_jac_lin work list (rnea: the a / f columns, -1 padded to whole waves)
   // per problem [B][*]
   double* p;         // params
   double* x;         // SQP iterate (decision vector)
@@ -264,6 +265,7 @@ struct PlOcpHandle {
   long long ch_stride;              // doubles of chain blocks per problem
   int chv_stride;                   // doubles of chain vectors per problem
   int jl_len;                       // k_eval_jac work-list entries (a multiple of 64 before the cheap part)
+  int jlin_len;                     // k_eval_jac_lin work-list entries (0: those columns stay in jlist)
   int solver;                       // PL_SOLVER_OSQP (SQP + OSQP ADMM) or PL_SOLVER_IP (interior point)
   int ip_lam_warm;                  // 1: the next interior-point solve starts from lam = ip_lam0
   int ip_hess;                      // interior point: PL_IP_HESS_EXACT (Lagrangian) or PL_IP_HESS_GN
