@@ -2,6 +2,7 @@
 // variable / row / sparsity layout the reference gets from CasADi Opti
 // (optimization/ocp.py:38-44, 103-198, 283, 305), the ADMM and factor node programs and
 // the Jacobian work list.  Called by pl_ocp_create (api.hip).
+#include <algorithm>
 #include "api_internal.h"
 
 // ---------------------------------------------------------------------------
@@ -872,6 +873,30 @@ int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, b
   }
   list = ex;
   list.insert(list.end(), ch.begin(), ch.end());
+  if (!lin.empty()) {
+    // the chain a column's RNEA pass is confined to (k_eval_jac_lin: tree_pass only_ch; -1:
+    // a base acceleration, which moves every chain); the list is grouped by chain so that a
+    // wave's lanes walk the same chain.  .y = local column | (chain + 1) << 16.
+    const PlModel& Mo = o->h.model;
+    const auto chain_of = [&](int j) {
+      for (int c = 0; c < Mo.nchains; ++c)
+        if (j >= Mo.chain_first[c] && j < Mo.chain_first[c] + Mo.chain_len[c]) return c;
+      return -1;
+    };
+    for (int2& w : lin) {
+      const int k = w.y - O.ndx;
+      int c = -1;
+      if (k < O.na) {
+        for (int j = 2; j < Mo.njoints; ++j)
+          if (Mo.idx_v[j] == k) c = chain_of(j);
+      } else {
+        const int e = (k - O.na) / 3;
+        c = chain_of(e < O.nfeet ? O.feet[e].joint : O.ext.joint);
+      }
+      w.y |= (c + 1) << 16;
+    }
+    std::stable_sort(lin.begin(), lin.end(), [](const int2& a, const int2& b) { return (a.y >> 16) < (b.y >> 16); });
+  }
   while (lin.size() % 64) lin.push_back(make_int2(-1, -1));
   return 0;
 }

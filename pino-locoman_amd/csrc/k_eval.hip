@@ -148,8 +148,10 @@ struct UnitIn {  // e_k (k < 0: zero)
 // and f, so d tau / d a_k = M(q) e_k and d tau / d f_c = -J_c(q)^T e_c are one primal
 // RNEA pass of the zero-gravity model at v = 0 with a = e_k (or f = e_c) instead of a dual
 // tree pass (ocp_whole_body_rnea.py:207-235, pin.rnea with the contact forces).  One lane =
-// one (node, column) of d.jlin (api_build.hip build_jac_list); the pass leaves the joint
-// torques in the first nj slots of the lane's store, which node_rows then reads as tangents.
+// one (node, column) of d.jlin (api_build.hip build_jac_list), grouped by the one chain the
+// column moves (a joint acceleration or a foot force: the pass skips the other chains); the
+// pass leaves the joint torques in the first nj slots of the lane's store, which node_rows
+// then reads as tangents.
 template <int DYN>
 __global__ __launch_bounds__(64) void k_eval_jac_lin(PlDev d, int B, int n, int np, int nnz, int len) {
   const int b = blockIdx.y;
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(64) void k_eval_jac_lin(PlDev d, int B, int n, int 
   if (q >= len) return;
   const int2 jw = d.jlin[q];
   if (jw.x < 0) return;
-  const int i = jw.x, lc = jw.y;
+  const int i = jw.x, lc = jw.y & 0xffff, only_ch = (jw.y >> 16) - 1;
   const PlOcpConst& O = *d.oc;
   const PlNode nd = d.nodes[i];
   const PlNode nn = d.nodes[i + 1];
@@ -178,7 +180,7 @@ __global__ __launch_bounds__(64) void k_eval_jac_lin(PlDev d, int B, int n, int 
   kp.stride = 64;
   const int k = lc - ndx;  // a_k, or force component k - na
   pl::tree_pass<double>(*d.model0, O, qb, qrev, ZeroInD{}, UnitIn{k < O.na ? k : -1}, UnitIn{k - O.na}, true, false,
-                        kp);
+                        kp, nullptr, std::false_type{}, only_ch);
   double base[6];
   for (int r = 0; r < 6; ++r) base[r] = kp.tau[r];
   const int* cp = d.colptr + nd.colptr_off;

@@ -351,7 +351,7 @@ PL_HD void comp_add(S* comp, double m, const double* lever, const double* Ic, co
 template <class S, class QR, class VA, class InA, class InF, bool kComp = false>
 PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const QR& qrev, const VA& v, const InA& a,
                      const InF& forces, bool want_tau, bool want_vel, NodeKin<S>& out, S* comp = nullptr,
-                     std::integral_constant<bool, kComp> = {}) {
+                     std::integral_constant<bool, kComp> = {}, int only_ch = -1) {
   // ---- root (free-flyer, joint 1)
   S R0[9];
   quat_to_R(qb + 3, R0);
@@ -394,6 +394,13 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
   for (int ch = 0; ch < M.nchains; ++ch) {
     const int first = M.chain_first[ch];
     const int L = M.chain_len[ch];
+    if (only_ch >= 0 && ch != only_ch) {
+      // only_ch (k_eval_jac_lin, v = 0, zero gravity): a / f enter this chain alone, the
+      // other chains carry no acceleration and no force
+      if (want_tau)
+        for (int kk = 0; kk < L; ++kk) out.tau_j(M.idx_v[first + kk] - 6) = S(0.0);
+      continue;
+    }
     S pv[6], pa[6], oR[9], op[3];
     for (int k = 0; k < 6; ++k) { pv[k] = v1[k]; if (want_tau) pa[k] = a1[k]; }
     for (int k = 0; k < 9; ++k) oR[k] = R0[k];
