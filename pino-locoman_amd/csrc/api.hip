@@ -752,6 +752,40 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
     // hyper-dual pass per pair); PL_HESS_LIN=0 keeps them as pairs
     const bool lin = O.dyn == PL_DYN_RNEA && !(getenv("PL_HESS_LIN") && atoi(getenv("PL_HESS_LIN")) == 0);
     const int lin_lo = O.ndx, lin_hi = O.ndx + O.na + 3 * O.nfeet;
+    // rnea family: the chain of a w_i coordinate (-1: the base, or none).  The rows are sums of
+    // per-chain terms that read the base and their own chain only, so a pair with a coordinate
+    // of chain c has a mixed part from chain c's terms alone, and its pass skips the other
+    // chains (tree_pass only_ch, packed as .x = node | (chain + 1) << 16).  PL_HESS_CHAIN=0: off
+    const bool chains = PL_IS_RNEA(O.dyn) && !(getenv("PL_HESS_CHAIN") && atoi(getenv("PL_HESS_CHAIN")) == 0);
+    const PlModel& Mo = h->model;
+    const auto joint_chain = [&](int jt) {
+      for (int c = 0; c < Mo.nchains; ++c)
+        if (jt >= Mo.chain_first[c] && jt < Mo.chain_first[c] + Mo.chain_len[c]) return c;
+      return -1;
+    };
+    const auto vidx_chain = [&](int vi) {
+      if (vi < 6) return -1;
+      for (int jt = 2; jt < Mo.njoints; ++jt)
+        if (Mo.idx_v[jt] == vi) return joint_chain(jt);
+      return -1;
+    };
+    const auto coord_chain = [&](int c) {
+      if (c < O.ndx) return vidx_chain(c < O.nv ? c : c - O.nv);
+      const int k = c - O.ndx;
+      if (k < O.na) return vidx_chain(k);
+      if (k < O.na + O.nf) {
+        const int e = (k - O.na) / 3;
+        return joint_chain(e < O.nfeet ? O.feet[e].joint : O.ext.joint);
+      }
+      return vidx_chain(6 + k - O.na - O.nf);
+    };
+    const auto pair_chain = [&](int j, int k) {
+      if (!chains) return -1;
+      const int cj = coord_chain(j), ck = coord_chain(k);
+      if (cj < 0) return ck;
+      if (ck < 0 || ck == cj) return cj;
+      return -1;  // two chains: structurally zero, kept on the full pass
+    };
     for (int i = 0; i <= h->N; ++i) {
       const int nw = o->nodes[i].nw;
       hoff.push_back((int)off);
@@ -762,10 +796,11 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
       for (int k = 0; k < nw; ++k)
         for (int j = 0; j <= k; ++j) {
           if (lin && j < O.nv && k >= lin_lo && k < lin_hi) continue;
-          if (pat[type][(size_t)k * (k + 1) / 2 + j]) hl.push_back(make_int2(i, j | (k << 16)));
+          if (pat[type][(size_t)k * (k + 1) / 2 + j])
+            hl.push_back(make_int2(i | ((pair_chain(j, k) + 1) << 16), j | (k << 16)));
         }
-      if (lin)
-        for (int k = 3; k < O.nv; ++k) hlin.push_back(make_int2(i, k));  // RNEA ignores the base position
+      if (lin)  // RNEA ignores the base position
+        for (int k = 3; k < O.nv; ++k) hlin.push_back(make_int2(i, k | ((chains ? vidx_chain(k) + 1 : 0) << 16)));
     }
     for (int t = 0; t < 3; ++t) {  // first row of the RNEA base / joint-torque row blocks per node type
       h->hl_rb_base[t] = h->hl_rb_tau[t] = -1;

@@ -45,14 +45,14 @@ __global__ __launch_bounds__(64) void k_lag_hess(PlDev d, int N, int n, int m, i
   HDual kst[PL_KIN_STORE];
   for (int q = blockIdx.x * 64 + threadIdx.x; q < hl_len; q += gridDim.x * 64) {
     const int2 w = d.hlist[q];
-    const int i = w.x, j = w.y & 0xffff, k = w.y >> 16;
+    const int i = w.x & 0xffff, only_ch = (w.x >> 16) - 1, j = w.y & 0xffff, k = w.y >> 16;
     const PlNode nd = d.nodes[i];
     const PlNode nn = d.nodes[i + 1];
     VecIn<HDual> dx{x + nd.x_off, nullptr, 0.0, j, k};
     VecIn<HDual> u{x + nd.x_off + ndx, nullptr, 0.0, j - ndx, k - ndx};
     VecIn<HDual> dxn{x + nn.x_off, nullptr, 0.0, j - nd.nw, k - nd.nw};
     HessEmit e{lam + nd.row_off, 0.0, 0};
-    pl::node_rows<HDual, DYN>(M, O, i, p, dx, u, dxn, e, kst, 1);
+    pl::node_rows<HDual, DYN>(M, O, i, p, dx, u, dxn, e, kst, 1, nullptr, nullptr, nullptr, only_ch);
     H[d.hoff[i] + k * (k + 1) / 2 + j] = e.acc;
   }
 }
@@ -73,7 +73,8 @@ __global__ __launch_bounds__(64) void k_lag_hess_pb(PlDev d, int B, int N, int n
   const int ndx = O.ndx;
   HDual kst[PL_KIN_STORE];
   const int2 w = d.hlist[blockIdx.x];
-  const int i = __builtin_amdgcn_readfirstlane(w.x);
+  const int wx = __builtin_amdgcn_readfirstlane(w.x);
+  const int i = wx & 0xffff, only_ch = (wx >> 16) - 1;  // the pair's chain (api.hip set_solver)
   const int jk = __builtin_amdgcn_readfirstlane(w.y);
   const int j = jk & 0xffff, k = jk >> 16;
   const PlNode nd = d.nodes[i];
@@ -82,7 +83,7 @@ __global__ __launch_bounds__(64) void k_lag_hess_pb(PlDev d, int B, int N, int n
   VecIn<HDual> u{x + nd.x_off + ndx, nullptr, 0.0, j - ndx, k - ndx};
   VecIn<HDual> dxn{x + nn.x_off, nullptr, 0.0, j - nd.nw, k - nd.nw};
   HessEmit e{lam + nd.row_off, 0.0, 0};
-  pl::node_rows<HDual, DYN>(M, O, i, p, dx, u, dxn, e, kst, 1);
+  pl::node_rows<HDual, DYN>(M, O, i, p, dx, u, dxn, e, kst, 1, nullptr, nullptr, nullptr, only_ch);
   H[d.hoff[i] + k * (k + 1) / 2 + j] = e.acc;
 }
 
@@ -115,7 +116,8 @@ __global__ __launch_bounds__(64) void k_lag_hess_lin(PlDev d, int B, int n, int 
   const PlOcpConst& O = *d.oc;
   const int2 w = d.hlin[blockIdx.x];
   const int i = __builtin_amdgcn_readfirstlane(w.x);
-  const int k = __builtin_amdgcn_readfirstlane(w.y);
+  const int wy = __builtin_amdgcn_readfirstlane(w.y);
+  const int k = wy & 0xffff, only_ch = (wy >> 16) - 1;  // dq_k's chain (-1: a base coordinate)
   const PlNode nd = d.nodes[i];
   const double* p = d.p + (size_t)b * np;
   const double* lam = d.ip_lam + (size_t)b * m + nd.row_off;
@@ -137,13 +139,15 @@ __global__ __launch_bounds__(64) void k_lag_hess_lin(PlDev d, int B, int n, int 
   const int ndx = O.ndx, nv = O.nv;
   const auto slot = [&](int col) { return (size_t)col * (col + 1) / 2 + k; };  // (k, col) with k < col
   // (dq_k, a_j) = d/dq_k [M(q) lambda_tau]_j
-  pl::tree_pass<Dual>(*d.model0, O, qb, qrev, ZeroIn{}, lt, ZeroIn{}, true, false, kin);
+  pl::tree_pass<Dual>(*d.model0, O, qb, qrev, ZeroIn{}, lt, ZeroIn{}, true, false, kin, nullptr, std::false_type{},
+                      only_ch);
   for (int j = 0; j < nv; ++j) {
     const double t = j < 6 ? kin.tau[j].d : Dual(kin.tau_j(j - 6)).d;
     H[slot(ndx + j)] = t;
   }
   // (dq_k, f_e) = -d/dq_k [J_e(q) lambda_tau]   (feet)
-  pl::tree_pass<Dual>(*d.model, O, qb, qrev, lt, ZeroIn{}, ZeroIn{}, false, true, kin);
+  pl::tree_pass<Dual>(*d.model, O, qb, qrev, lt, ZeroIn{}, ZeroIn{}, false, true, kin, nullptr, std::false_type{},
+                      only_ch);
   const int f0 = ndx + O.na;
   for (int e = 0; e < O.nfeet; ++e)
     for (int c = 0; c < 3; ++c) H[slot(f0 + 3 * e + c)] = -Dual(kin.foot_vel(e, c)).d;

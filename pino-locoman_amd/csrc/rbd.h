@@ -395,10 +395,23 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
     const int first = M.chain_first[ch];
     const int L = M.chain_len[ch];
     if (only_ch >= 0 && ch != only_ch) {
-      // only_ch (k_eval_jac_lin, v = 0, zero gravity): a / f enter this chain alone, the
-      // other chains carry no acceleration and no force
+      // only_ch: the caller differentiates along coordinates of chain only_ch (and of the
+      // base) alone, so the other chains' outputs have zero tangents: they are skipped and
+      // their outputs zeroed, values included (k_eval_jac_lin: the a / f columns at v = 0 and
+      // zero gravity, where the other chains carry no acceleration and no force; k_lag_hess_pb:
+      // a pair with a chain coordinate, whose mixed part only that chain's terms carry)
       if (want_tau)
         for (int kk = 0; kk < L; ++kk) out.tau_j(M.idx_v[first + kk] - 6) = S(0.0);
+      if (want_vel) {
+        for (int e = 0; e < O.nfeet; ++e)
+          if (O.feet[e].joint >= first && O.feet[e].joint < first + L)
+            for (int c = 0; c < 3; ++c) out.foot_vel(e, c) = S(0.0);
+        if (O.arm.valid && O.arm.joint >= first && O.arm.joint < first + L)
+          for (int k = 0; k < 3; ++k) {
+            arm_lin[k] = S(0.0);
+            arm_pos[k] = S(0.0);
+          }
+      }
       continue;
     }
     S pv[6], pa[6], oR[9], op[3];

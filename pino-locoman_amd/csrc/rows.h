@@ -149,7 +149,8 @@ PL_HD void chol_solve(const double* L, int n, double* x) {
 template <class S, int DYN, class Emit>
 PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double* p, const VecIn<S>& dx,
                      const VecIn<S>& u, const VecIn<S>& dxn, Emit& emit, S* kstore, int kstride,
-                     double* kvals = nullptr, const double* aba_sh = nullptr, const double* lin_base = nullptr) {
+                     double* kvals = nullptr, const double* aba_sh = nullptr, const double* lin_base = nullptr,
+                     int only_ch = -1) {
   const int nv = O.nv, nq = O.nq, nj = O.nj;
   constexpr bool CV = PL_IS_CV(DYN);
   constexpr bool CVNB = (DYN == PL_DYN_CVNB);  // v = [base_vel_dynamics(h, q, v_j), v_j]
@@ -268,9 +269,9 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
     } else if constexpr (COMP) {
       tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin, comp, std::true_type{});
     } else if constexpr (FD) {
-      tree_pass<S>(M, O, qb, qrev, vel, afd, forces, want_tau, state_rows, kin);
+      tree_pass<S>(M, O, qb, qrev, vel, afd, forces, want_tau, state_rows, kin, nullptr, std::false_type{}, only_ch);
     } else {
-      tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin);
+      tree_pass<S>(M, O, qb, qrev, vel, a, forces, want_tau, state_rows, kin, nullptr, std::false_type{}, only_ch);
     }
   } else {  // a skipped pass leaves zero (value and tangent) kinematic outputs
     for (int k = lin_base ? nj : 0; k < PL_KIN_STORE_DUAL; ++k) kin.clear(k);
