@@ -306,7 +306,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
     std::vector<int2> jl, jlin;
     // PL_JAC_LIN=0 keeps the rnea a / f columns as dual tree-pass lanes (A/B)
     const bool use_lin = !(getenv("PL_JAC_LIN") && atoi(getenv("PL_JAC_LIN")) == 0);
-    if (build_jac_list(o, jl, jlin, use_lin)) {
+    if (build_jac_list(o, jl, jlin, use_lin, &h.jl_ex)) {
       pl_ocp_destroy(o);
       return -1;
     }
@@ -375,6 +375,10 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   o->mpc_graph_off = getenv("PL_MPC_GRAPH") && atoi(getenv("PL_MPC_GRAPH")) == 0;
   o->h.admm_scatter = getenv("PL_ADMM_SCATTER") ? atoi(getenv("PL_ADMM_SCATTER")) : 0;  // A/B of k_admm's gathers
   o->h.admm_defer = !(getenv("PL_ADMM_DEFER") && atoi(getenv("PL_ADMM_DEFER")) == 0);  // k_admm's store placement (A/B)
+  // the cheap Jacobian columns (dx_{i+1}, rnea tau_j, centroidal_vel h) have constant entries
+  // (+-1, -m): written by the first evaluation only (PL_JAC_CHEAP=1: every evaluation)
+  o->h.jac_cheap_every = getenv("PL_JAC_CHEAP") && atoi(getenv("PL_JAC_CHEAP")) == 1;
+  o->h.jac_cheap_ok = 0;
   o->h.hess_pb = !(getenv("PL_HESS_PB") && atoi(getenv("PL_HESS_PB")) == 0);  // Hessian mapping (PL_HESS_PB=0: pairs per lane)
   if (hipMemcpy(D.model, &h.model, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(D.oc, &h.oc, sizeof(PlOcpConst), hipMemcpyHostToDevice) != hipSuccess) {
@@ -729,6 +733,10 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
     pl_set_error("the interior-point solver needs include_acc=True (ocp_whole_body_rnea.py:21)");
     return -1;
   }
+  if (solver == PL_SOLVER_IP && h->nw_max > 192) {  // k_ip_refine's per-wave node vectors (PL_IP_NWMAX)
+    pl_set_error("interior point: node block width %d exceeds 192", h->nw_max);
+    return -1;
+  }
   if (solver == PL_SOLVER_IP && !h->d.ipinfo) {
     const size_t Bm = (size_t)h->B * h->m;
     if (dalloc(o, &h->d.ip_s, Bm) || dalloc(o, &h->d.ip_lam, Bm) || dalloc(o, &h->d.ip_lam0, Bm) ||
@@ -746,17 +754,19 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
     long long off = 0;
     const PlOcpConst& O = h->oc;
     std::vector<uint8_t> pat[3];
-    // whole_body_rnea: the rows are linear in a and in the contact forces, and only the RNEA rows
+    // whole_body_rnea / whole_body_acc: the rows are linear in a and in the contact forces, and only the RNEA rows
     // couple them to q, so the (dq, a) and (dq, f_feet) blocks are d/dq of M(q) lambda_tau and
     // of -J_e(q) lambda_tau (k_lag_hess_lin: two dual tree passes per dq column instead of one
     // hyper-dual pass per pair); PL_HESS_LIN=0 keeps them as pairs
-    const bool lin = O.dyn == PL_DYN_RNEA && !(getenv("PL_HESS_LIN") && atoi(getenv("PL_HESS_LIN")) == 0);
+    const bool lin = (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC) &&
+                     !(getenv("PL_HESS_LIN") && atoi(getenv("PL_HESS_LIN")) == 0);
     const int lin_lo = O.ndx, lin_hi = O.ndx + O.na + 3 * O.nfeet;
-    // rnea family: the chain of a w_i coordinate (-1: the base, or none).  The rows are sums of
+    // rnea family and whole_body_acc: the chain of a w_i coordinate (-1: the base, or none).  The rows are sums of
     // per-chain terms that read the base and their own chain only, so a pair with a coordinate
     // of chain c has a mixed part from chain c's terms alone, and its pass skips the other
     // chains (tree_pass only_ch, packed as .x = node | (chain + 1) << 16).  PL_HESS_CHAIN=0: off
-    const bool chains = PL_IS_RNEA(O.dyn) && !(getenv("PL_HESS_CHAIN") && atoi(getenv("PL_HESS_CHAIN")) == 0);
+    const bool chains = (PL_IS_RNEA(O.dyn) || O.dyn == PL_DYN_ACC) &&
+                        !(getenv("PL_HESS_CHAIN") && atoi(getenv("PL_HESS_CHAIN")) == 0);
     const PlModel& Mo = h->model;
     const auto joint_chain = [&](int jt) {
       for (int c = 0; c < Mo.nchains; ++c)
@@ -1259,6 +1269,10 @@ static int debug_rw(pl_ocp* o, const char* name, double* out, const double* in, 
       if ((size_t)count < it.len) { pl_set_error("buffer too small for %s (%zu)", name, it.len); return -1; }
       if (out) PL_CHECK_HIP(hipMemcpyAsync(out, it.p, it.len * 8, hipMemcpyDeviceToHost, h->stream));
       else PL_CHECK_HIP(hipMemcpyAsync(it.p, in, it.len * 8, hipMemcpyHostToDevice, h->stream));
+      if (in && it.p == h->d.Araw) {  // the constant entries are rewritten by the next (eager) step
+        h->jac_cheap_ok = 0;
+        o->mpc_key.clear();
+      }
       PL_CHECK_HIP(hipStreamSynchronize(h->stream));
       return (int)0;
     }

@@ -836,7 +836,7 @@ int build_factor_prog(pl_ocp* o) {
 // 64 per wave ACROSS node boundaries and padded to whole waves; then the columns that
 // skip it (dx_{i+1}; rnea tau_j; centroidal h), which are cheap.  The classification
 // mirrors node_rows' skip logic (rows.h); it only affects the schedule.
-int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, bool use_lin) {
+int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, bool use_lin, int* n_ex) {
   const PlOcpConst& O = o->h.oc;
   std::vector<int2> ex, ch;
   lin.clear();
@@ -853,7 +853,7 @@ int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, b
       } else {
         const int k = lc - O.ndx;
         cheap = PL_IS_RNEA(O.dyn) && k >= O.na + O.nf;
-        if (use_lin && PL_IS_RNEA(O.dyn) && !cheap) {  // a / f: linear in the RNEA (k_eval_jac_lin)
+        if (use_lin && (PL_IS_RNEA(O.dyn) || O.dyn == PL_DYN_ACC) && !cheap) {  // a / f: linear in the RNEA (k_eval_jac_lin)
           lin.push_back(make_int2(i, lc));
           continue;
         }
@@ -871,6 +871,7 @@ int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, b
       return -1;
     }
   }
+  *n_ex = (int)ex.size();
   list = ex;
   list.insert(list.end(), ch.begin(), ch.end());
   if (!lin.empty()) {

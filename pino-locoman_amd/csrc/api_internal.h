@@ -74,7 +74,8 @@ int build_layout(pl_ocp* o);
 int build_admm_prog(pl_ocp* o);
 int build_factor_prog(pl_ocp* o);
 // lin (use_lin, rnea): the a / f columns, for k_eval_jac_lin, instead of tree-pass lanes in list
-int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, bool use_lin);
+// n_ex: entries of list before the cheap columns (whole waves)
+int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, bool use_lin, int* n_ex);
 // api_casadi.hip: drop the CasADi binding of an OCP that is being destroyed
 void cas_forget(const pl_ocp* o);
 void jac_pattern(const PlOcpHandle& h, const std::vector<PlNode>& nodes, int i, std::vector<uint8_t>& nz);

@@ -144,7 +144,7 @@ struct UnitIn {  // e_k (k < 0: zero)
 };
 }  // namespace
 
-// The RNEA's acceleration and contact-force columns (whole_body_rnea): tau is linear in a
+// The RNEA's acceleration and contact-force columns (whole_body_rnea, whole_body_acc): tau is linear in a
 // and f, so d tau / d a_k = M(q) e_k and d tau / d f_c = -J_c(q)^T e_c are one primal
 // RNEA pass of the zero-gravity model at v = 0 with a = e_k (or f = e_c) instead of a dual
 // tree pass (ocp_whole_body_rnea.py:207-235, pin.rnea with the contact forces).  One lane =
@@ -246,12 +246,20 @@ void launch_eval_jac(PlOcpHandle* h) {
     if (h->oc.dyn == PL_DYN_RNEA)
       hipLaunchKernelGGL(k_eval_jac_lin<PL_DYN_RNEA>, g, dim3(64), 0, h->stream, h->d, h->B, h->n, h->np, h->nnz,
                          h->jlin_len);
+    else if (h->oc.dyn == PL_DYN_ACC)
+      hipLaunchKernelGGL(k_eval_jac_lin<PL_DYN_ACC>, g, dim3(64), 0, h->stream, h->d, h->B, h->n, h->np, h->nnz,
+                         h->jlin_len);
     else
       hipLaunchKernelGGL(k_eval_jac_lin<PL_DYN_RNEAFD>, g, dim3(64), 0, h->stream, h->d, h->B, h->n, h->np, h->nnz,
                          h->jlin_len);
   }
-  PL_DISPATCH_DYN(h->oc.dyn, k_eval_jac, dim3((h->jl_len + 63) / 64, h->B), dim3(64), 0, h->stream, h->d, h->B,
-                  h->N, h->n, h->np, h->nnz, h->jl_len);
+  // the cheap columns (after jl_ex) have constant entries: after the first evaluation their
+  // waves are not launched (the entries stay in d.Araw; nothing else writes them)
+  const int len = (h->jac_cheap_ok && !h->jac_cheap_every) ? h->jl_ex : h->jl_len;
+  if (len > 0)
+    PL_DISPATCH_DYN(h->oc.dyn, k_eval_jac, dim3((len + 63) / 64, h->B), dim3(64), 0, h->stream, h->d, h->B, h->N,
+                    h->n, h->np, h->nnz, h->jl_len);
+  h->jac_cheap_ok = 1;
 }
 
 void launch_objective(PlOcpHandle* h) {

@@ -364,7 +364,22 @@ __global__ __launch_bounds__(256) void k_ip_kkt(PlDev d, int N, int n, int m, in
 // W_E = 1 / delta_c = 1e4 one block-inverse solve agrees with the oracle's sparse LU to
 // ~1e-12 and the refinement keeps the step at that level as the multipliers grow
 // (at W_E = 1e6 the explicit inverses lose ~5 digits and the refinement diverges).
-__global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int n, int m, int nnz, double delta_w, int hlag,
+// H_i dx of a node block (r04): one wave per node (nodes w, w + 4, ...), the packed-lower
+// block read in storage order (coalesced) and both halves of every entry added into a
+// wave-private LDS vector by ds_add_f64 (fixed lane / instruction order: deterministic);
+// the per-column gather of the block (strided, uncoalesced) took 2.1 ms per call at the
+// headline size.
+#define PL_IP_NWMAX 192
+__device__ __forceinline__ void ip_lds_add(double* p, double v) {
+  typedef __attribute__((address_space(3))) double* LPtr;
+  __hip_atomic_fetch_add((LPtr)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+__device__ __forceinline__ void ip_wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int N, int n, int m, int nnz, double delta_w, int hlag,
                                                    long long hl_stride) {
   const int b = blockIdx.x;
   if (!d.ipinfo[b].active) return;
@@ -392,19 +407,42 @@ __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int n, int m, int nn
   for (int j = threadIdx.x; j < n; j += 256) dx[j] += xa[j];
   __syncthreads();
   const double* Hb = hlag ? d.Hlag + (size_t)b * hl_stride : nullptr;
+  if (Hb) {  // qs = H_i dx_{w_i} per node block (k_lag_hess's packed lower blocks; none on node N)
+    __shared__ double hy[4][PL_IP_NWMAX], hx[4][PL_IP_NWMAX];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* y = hy[wv];
+    double* xv = hx[wv];
+    for (int i = wv; i <= N; i += 4) {
+      const PlNode nd = d.nodes[i];
+      const int nw = nd.nw;
+      for (int c = lane; c < nw; c += 64) {
+        y[c] = 0.0;
+        xv[c] = dx[nd.x_off + c];
+      }
+      ip_wsync();
+      if (i < N) {
+        const double* Hi = Hb + d.hoff[i];
+        const int ne = nw * (nw + 1) / 2;
+        for (int e = lane; e < ne; e += 64) {
+          int r = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+          while (r * (r + 1) / 2 > e) --r;
+          while ((r + 1) * (r + 2) / 2 <= e) ++r;
+          const int c = e - r * (r + 1) / 2;
+          const double h = Hi[e];
+          ip_lds_add(y + r, h * xv[c]);
+          if (c != r) ip_lds_add(y + c, h * xv[r]);
+        }
+        ip_wsync();
+      }
+      for (int c = lane; c < nw; c += 64) qs[nd.x_off + c] = y[c];
+      ip_wsync();
+    }
+    __syncthreads();
+  }
   for (int j = threadIdx.x; j < n; j += 256) {
     const double dj = dx[j];
     double acc = grad[j] + (Ps[j] + delta_w) * dj;
-    if (Hb) {  // + H_i dx_{w_i}, node i's packed-lower block (k_lag_hess)
-      const int i = d.colnode[j];
-      const PlNode nd = d.nodes[i];
-      const int lc = j - nd.x_off;
-      const double* Hi = Hb + d.hoff[i];
-      for (int c = 0; c < nd.nw; ++c) {
-        const int r0 = max(lc, c), c0 = min(lc, c);
-        acc = fma(Hi[r0 * (r0 + 1) / 2 + c0], dx[nd.x_off + c], acc);
-      }
-    }
+    if (Hb) acc += qs[j];
     for (int q = d.gc_ptr[j]; q < d.gc_ptr[j + 1]; ++q) {
       const int2 er = d.gc_er[q];
       acc += A[er.x] * t[er.y];
@@ -722,7 +760,7 @@ static void ip_factor(PlOcpHandle* h) {
 }
 
 static void ip_refine(PlOcpHandle* h, const PlIpSettings& st) {
-  hipLaunchKernelGGL(k_ip_refine, dim3(h->B), dim3(256), 0, h->stream, h->d, h->n, h->m, h->nnz, st.delta_w,
+  hipLaunchKernelGGL(k_ip_refine, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz, st.delta_w,
                      h->ip_hess == PL_IP_HESS_EXACT ? 1 : 0, h->hl_stride);
 }
 

@@ -265,6 +265,8 @@ struct PlOcpHandle {
   long long ch_stride;              // doubles of chain blocks per problem
   int chv_stride;                   // doubles of chain vectors per problem
   int jl_len;                       // k_eval_jac work-list entries (a multiple of 64 before the cheap part)
+  int jl_ex;                        // jlist entries before the cheap columns
+  int jac_cheap_every;              // PL_JAC_CHEAP=1: evaluate them every time (A/B)
   int jlin_len;                     // k_eval_jac_lin work-list entries (0: those columns stay in jlist)
   int solver;                       // PL_SOLVER_OSQP (SQP + OSQP ADMM) or PL_SOLVER_IP (interior point)
   int ip_lam_warm;                  // 1: the next interior-point solve starts from lam = ip_lam0
@@ -297,6 +299,9 @@ struct PlOcpHandle {
   int* h_nodes_raw;
   // optional per-kernel timing of the ADMM launches (HIP events on the handle's stream)
   int profile;
+  // outside the MPC-graph key (api.hip kMpcKeyBytes): set by the first Jacobian evaluation,
+  // which runs eagerly; a debug write of Araw clears it and the key
+  int jac_cheap_ok;                 // the cheap columns' constant entries are in d.Araw
   hipEvent_t prof_ev[64][2];
   int prof_n;
   double prof_admm_ms;

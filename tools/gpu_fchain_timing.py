@@ -1,0 +1,30 @@
+"""Phase timing of the factor chain (k_fchain, s_memtime on thread 0, the last launch of a
+solve).  Run on the GPU box:  python tools/gpu_fchain_timing.py robot dynamics N B
+Slots (k_factor.hip T(k)): 7 staging, 0 X x X sweep, 1 S_ux, 2 S_uu, 3 Y / Z, 4 E, 6 final store."""
+import os
+import sys
+
+import numpy as np
+
+os.environ["PL_ADMM_TIMING"] = "1"
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "pino-locoman_amd"))
+from pinoloco import robots  # noqa: E402
+from pinoloco.ocp import BatchedOCP  # noqa: E402
+from pinoloco.synthetic import build_batch  # noqa: E402
+
+rob, dyn, N, B = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+R = robots.ROBOTS[rob]()
+R.set_gait_sequence("trot", 0.8)
+lay, P, X, XS, T0 = build_batch(R, dyn, N, B, 0)
+bo = BatchedOCP(R, dyn, N, batch=B, device=0)
+bo.set_params(P)
+bo.set_x(X)
+bo.init_solver()
+bo.solve()
+T = bo.debug("admm_t", B * 32)[16 * B:].reshape(B, 16)[:, :8] / (N + 1)
+names = {7: "staging", 0: "X sweep", 1: "S_ux", 2: "S_uu", 3: "Y / Z", 4: "E", 6: "store"}
+print(f"{rob} {dyn} N={N} B={B} kernel={bo.admm_kernel()}: k_fchain cycles per node (thread 0)")
+for k, nm in names.items():
+    print(f"  {nm:10s} {T[:, k].mean():10.1f}")
+print(f"  total      {T.sum(1).mean():10.1f}")
