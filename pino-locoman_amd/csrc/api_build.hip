@@ -815,11 +815,18 @@ int build_factor_prog(pl_ocp* o) {
   if (h.fac_gc) ny = std::max(ny, std::max(npc_max, X) * nc_max);
   ny = (ny + 1) & ~1;
   const int nE = (X * (X + 1) / 2 + 1) & ~1;
-  h.fchain_ny = ny;
   // short coupling-row lists (the integration rows of rnea / acc: 2 entries): E_{i+1} straight
-  // from S (4 products per entry) instead of through Y
-  h.fchain_short = !h.fac_gc && cwlen_max <= 4;
-  h.fchain_ncw = (ncw_max + 1) & ~1;
+  // from S (4 products per entry, the lists staged per row in LDS: 4 values | 4 columns)
+  // instead of through Y; longer lists (aba, centroidal): E_{i+1} = Wc S Wc^T on the f64 MFMA
+  // with Wc and Y = Wc S dense in the Y buffer ([X16][NWS] each, r04; PL_FCHAIN_MF=0: the
+  // list route)
+  const bool is_short = !h.fac_gc && cwlen_max <= 4;
+  const int X16 = (X + 15) & ~15, NWS = ((h.nw_max + 15) & ~15) + 1;
+  const bool mf = !h.fac_gc && !is_short && !(getenv("PL_FCHAIN_MF") && atoi(getenv("PL_FCHAIN_MF")) == 0);
+  if (mf) ny = std::max(ny, (2 * X16 * NWS + 1) & ~1);
+  h.fchain_ny = ny;
+  h.fchain_short = is_short ? 1 : (mf ? 2 : 0);
+  h.fchain_ncw = ((is_short ? std::max(ncw_max, 6 * X) : ncw_max) + 1) & ~1;
   h.fchain_nc = h.fac_gc ? nc_max : 0;
   h.fchain_nxc = h.fac_gc ? (nxc_max + 1) & ~1 : 0;
   const int ngc = h.fac_gc ? ((nc_max * nc_max + h.fchain_nxc + nc_max + 1) & ~1) : 0;

@@ -385,6 +385,8 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
   double* pb = Yb;        // pivot block rows [2][128][4] during the sweep (Yb is free then; ny >= 1024)
   double* Eb = Yb + ny;   // E_i, packed lower
   double* Acw = Eb + nE;  // A values of the coupling rows' w parts (ncw)
+  double* sv = Acw;       // short lists: [X][4] values | [X][4] w columns (int), in the Acw region
+  int* sk = reinterpret_cast<int*>(Acw + 4 * X);
   double* cv = Acw + ncw;   // rho_a A_{e_a} (X)
   double* ev = cv + X;      // A_{e_a} (X)
   // optional phase timing (thread 0, s_memtime): 8 accumulators + last stamp in LDS
@@ -441,7 +443,22 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
       for (int q = tid; q < nc; q += NT) rcl[q] = rhob[crow[q]];
     } else if (i < N) {
       const int ncwi = (int)cwptr[X];
-      for (int q = tid; q < ncwi; q += NT) Acw[q] = Asb[cwl[q] & 0xffff];
+      if (short_cw == 1) {
+        // per row: 4 values (0 past the list) | 4 w columns, so the E loop reads LDS only
+        // (the global list words in its inner loop were a chain of dependent loads)
+        for (int a = tid; a < X; a += NT) {
+          const int q0 = (int)cwptr[a], q1 = (int)cwptr[a + 1];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const bool ok = q0 + j < q1;
+            const uint32_t wq = cwl[ok ? q0 + j : q0];
+            sv[4 * a + j] = ok ? Asb[wq & 0xffff] : 0.0;
+            sk[4 * a + j] = ok ? (int)((wq >> 16) & 0xff) : 0;
+          }
+        }
+      } else {
+        for (int q = tid; q < ncwi; q += NT) Acw[q] = Asb[cwl[q] & 0xffff];
+      }
       for (int a = tid; a < X; a += NT) {
         const double ea = Asb[cent[a]];
         ev[a] = ea;
@@ -628,22 +645,82 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
       continue;
     }
     // ---- E_{i+1} = D - Kc S Kc^T, Kc row a = rho_a A_{e_a} w_{s_a}^T (one coupling row per column)
-    if (short_cw) {
+    if (short_cw == 1) {
       // short lists: E[a][b] = d_ab - c_a c_b sum_{q in a} A_q sum_{q' in b} A_q' S[c_q][c_q'] straight
-      // from S, in the FMA order of the Y route below (bit-identical)
+      // from S, in the FMA order of the Y route below (the zero-padded list slots add exact 0s)
       for (int o = tid; o < X * X; o += NT) {
         const int a = o / X, bb = o - a * X;
         if (bb > a) continue;
-        const int qb0 = (int)cwptr[bb], qb1 = (int)cwptr[bb + 1];
+        double vb[4];
+        int kb[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          vb[k] = sv[4 * bb + k];
+          kb[k] = sk[4 * bb + k];
+        }
         double acc = 0.0;
-        for (int q = (int)cwptr[a]; q < (int)cwptr[a + 1]; ++q) {
-          const int p = (int)((cwl[q] >> 16) & 0xff);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int p = sk[4 * a + j];
           double y = 0.0;
-          for (int q2 = qb0; q2 < qb1; ++q2) y = fma(Acw[q2], Sl[sidx(p, (cwl[q2] >> 16) & 0xff)], y);
-          acc = fma(Acw[q], y, acc);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) y = fma(vb[k], Sl[sidx(p, kb[k])], y);
+          acc = fma(sv[4 * a + j], y, acc);
         }
         const double ca = cv[a];
         Eb[lidx(a, bb)] = (a == bb ? ca * ev[a] : 0.0) - ca * cv[bb] * acc;
+      }
+      T(4);
+      continue;
+    }
+    if (short_cw == 2) {
+      // E_{i+1} = D - C (Wc S Wc^T) C on the f64 MFMA (r04): Wc (the coupling rows' w parts)
+      // dense [X16][NWS] and Y = Wc S [X16][NWS] in the Y buffer (NWS = w width rounded to 16,
+      // + 1 against bank conflicts); 16x16 tiles, wave w takes tiles w, w + 4, ...
+      constexpr int X16 = (X + 15) & ~15;
+      constexpr int MT = X16 / 16;
+      const int nw = X + U;
+      const int NWP = (nw + 15) & ~15, NWS = NWP + 1, NTl = NWP / 16;
+      double* Wd = Yb;
+      double* Yd = Yb + X16 * NWS;
+      for (int o = tid; o < X16 * NWS; o += NT) Wd[o] = 0.0;
+      __syncthreads();
+      for (int o = tid; o < X * NWP; o += NT) {  // (row, list slot) items: independent loads
+        const int a = o / NWP, j = o - a * NWP;
+        const int q = (int)cwptr[a] + j;
+        if (q < (int)cwptr[a + 1]) Wd[a * NWS + ((cwl[q] >> 16) & 0xff)] = Acw[q];
+      }
+      __syncthreads();
+      T(3);
+      for (int t = w; t < MT * NTl; t += 4) {  // Y = Wc S
+        const int mt = t / NTl, nt = t - mt * NTl;
+        const int ar = 16 * mt + (l & 15), bc = 16 * nt + (l & 15);
+        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+        for (int kk = 0; kk < NWP / 4; ++kk) {
+          const int kc = 4 * kk + (l >> 4);
+          const double bv0 = Sl[sidx(min(kc, nw - 1), min(bc, nw - 1))];
+          acc = mfma4(Wd[ar * NWS + kc], bv0 * ((kc < nw && bc < nw) ? 1.0 : 0.0), acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Yd[(16 * mt + (l >> 4) + 4 * r) * NWS + bc] = acc[r];
+      }
+      __syncthreads();
+      for (int t = w; t < MT * (MT + 1) / 2; t += 4) {  // E' = Y Wc^T, lower tiles
+        int mt = 0;
+        while ((mt + 1) * (mt + 2) / 2 <= t) ++mt;
+        const int nt = t - mt * (mt + 1) / 2;
+        const int ar = 16 * mt + (l & 15), br = 16 * nt + (l & 15);
+        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+        for (int kk = 0; kk < NWP / 4; ++kk) {
+          const int kc = 4 * kk + (l >> 4);
+          acc = mfma4(Yd[ar * NWS + kc], Wd[br * NWS + kc], acc);
+        }
+        const int cb = 16 * nt + (l & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ra = 16 * mt + (l >> 4) + 4 * r;
+          if (ra < X && cb <= ra) Eb[lidx(ra, cb)] = (ra == cb ? cv[ra] * ev[ra] : 0.0) - cv[ra] * cv[cb] * acc[r];
+        }
       }
       T(4);
       continue;

@@ -287,7 +287,7 @@ struct PlOcpHandle {
   int fac_gc;                       // 1: general coupling (rows of node i touch several dx_{i+1} columns:
                                     //    whole_body_rnea include_acc = False), E_{i+1} = Wc^T Z Wc in k_fchain
   int fchain_nc, fchain_nxc;        // general coupling: max coupling rows, max dx_{i+1} entries per node
-  int fchain_short;                 // 1: coupling rows' w lists <= 4 entries: k_fchain forms E without Y
+  int fchain_short;                 // k_fchain's E: 1 short coupling lists (straight from S), 2 MFMA, 0 lists via Y
   PlSettings set;
   PlModel model;
   PlOcpConst oc;
