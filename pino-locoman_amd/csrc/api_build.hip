@@ -857,6 +857,8 @@ int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, b
         cheap = !(O.dyn == PL_DYN_RNEAFD && lc - nd.nw >= O.nv);  // FD: dv_{i+1} enters the RNEA
       } else if (lc < O.ndx) {
         cheap = O.dyn == PL_DYN_CV && lc < 6;  // (without the base, h enters v_b: not cheap)
+        // rnea / acc: the base position enters the integration rows only (rows.h seed_pos)
+        if ((PL_IS_RNEA(O.dyn) || O.dyn == PL_DYN_ACC) && lc < 3) cheap = true;
       } else {
         const int k = lc - O.ndx;
         cheap = PL_IS_RNEA(O.dyn) && k >= O.na + O.nf;

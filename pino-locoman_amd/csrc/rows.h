@@ -233,7 +233,11 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
     // (without the base, h enters the kinematics through v_b; its centroidal pass ran above)
     const bool seed_h = DYN == PL_DYN_CV && seeded(dx, 0, 6);
     const bool seed_f = CV && seeded(u, f_off, f_off + O.nf);
-    tree = !(seed_dxn || seed_tau || seed_h || seed_f) && !lin_base;
+    // whole_body_rnea / _acc: the RNEA, the foot and arm velocities do not read the base
+    // position (translation invariance), so a dq_0..2 column skips the pass (its exact
+    // tangents there are 0; the dual pass left round-off)
+    const bool seed_pos = (PL_IS_RNEA(DYN) || DYN == PL_DYN_ACC) && seeded(dx, 0, 3);
+    tree = !(seed_dxn || seed_tau || seed_h || seed_f || seed_pos) && !lin_base;
     cen = DYN == PL_DYN_CV && !(seed_dxn || seed_h);
   } else {
     (void)lin_base;
