@@ -361,7 +361,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= dalloc(o, &D.t0, B);
   rc |= dalloc(o, &D.xstate, B * (size_t)h.nx);
   D.dbg = nullptr;
-  if (getenv("PL_ADMM_TIMING") && atoi(getenv("PL_ADMM_TIMING")) > 0) rc |= dalloc(o, &D.dbg, B * 32);
+  if (getenv("PL_ADMM_TIMING") && atoi(getenv("PL_ADMM_TIMING")) > 0) rc |= dalloc(o, &D.dbg, B * 40);
   if (rc) { pl_ocp_destroy(o); return -2; }
   {
     int kind = PL_ADMM_AUTO;
@@ -1253,7 +1253,7 @@ static int debug_rw(pl_ocp* o, const char* name, double* out, const double* in, 
       {"As", h->d.As, B * h->nnz}, {"Araw", h->d.Araw, B * h->nnz}, {"qs", h->d.qs, B * h->n},
       {"ls", h->d.ls, B * h->m},   {"us", h->d.us, B * h->m},       {"rho", h->d.rho, B * h->m},
       {"D", h->d.D, B * h->n},     {"E", h->d.E, B * h->m},         {"cs", h->d.cs, B},
-      {"admm_t", h->d.dbg, h->d.dbg ? B * 32 : 0}, {"Ps", h->d.Ps, B * h->n},   {"P", h->d.P, B * h->n},         {"xa", h->d.xa, B * h->n},
+      {"admm_t", h->d.dbg, h->d.dbg ? B * 40 : 0}, {"Ps", h->d.Ps, B * h->n},   {"P", h->d.P, B * h->n},         {"xa", h->d.xa, B * h->n},
       {"za", h->d.za, B * h->m},   {"ya", h->d.ya, B * h->m},       {"S", h->d.S, B * (size_t)h->S_stride},
       {"rhs", h->d.rhs, B * h->n}, {"step", h->d.step, B * h->n},   {"grad", h->d.grad, B * h->n},
       {"g", h->d.g, B * h->m},     {"xstate", h->d.xstate, B * h->nx},

@@ -218,6 +218,18 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
   double* pb = K + nK;     // pivot block rows [2][512] during the sweep
   double* Gs = K + nK;     // after the sweep: G (U x X), row-major
 
+  // optional phase timing (PL_ADMM_TIMING=1): thread 0's s_memtime per phase, added into
+  // d.dbg[32 B + 8 b + k] (k: 0 staging, 1 assembly, 2 diagonal / H, 3 u sweep, 4 C / G
+  // store, 5 A' MFMA) by global f64 atomics
+  const bool TIMING = d.dbg != nullptr;
+  unsigned long long tl = TIMING ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto T = [&](int slot) {
+    if (TIMING && tid == 0) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      atomicAdd(d.dbg + (size_t)32 * gridDim.x / ni + (size_t)8 * b + slot, (double)(now - tl));
+      tl = now;
+    }
+  };
   const double* __restrict__ As = d.As + (size_t)b * nnz + fn->ent_off;
   const double* __restrict__ rho = d.rho + (size_t)b * m + fn->row_off;
   const int* __restrict__ rid = d.rowidx + fn->ent_off;
@@ -228,24 +240,48 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
   }
   for (int k = tid; k < nK; k += NT) K[k] = 0.0;
   __syncthreads();
+  T(0);
   // ---- assembly: each thread owns a set of slots; its stream walks their triples
   {
+    // the stream words are prefetched PF steps ahead (double-buffered registers) and the
+    // slot indices two flags ahead: the one-word-per-step loop waited a full L2 round trip
+    // per product (40 k of a B2G node's 70 k cycles, r04); same FMA order
     const uint32_t* __restrict__ st = d.kasm + fn->asm_off;
     const uint16_t* __restrict__ fl = d.kfl + fn->fl_off;
-    const int L = fn->asm_len;
+    const int L = fn->asm_len, FL = fn->fl_len;
+    constexpr int PF = 8;
     double acc = 0.0;
     int f = 0;
-    for (int t = 0; t < L; ++t) {
-      const uint32_t q = st[(size_t)t * NT + tid];
-      acc = fma(Ar[q & 0x7fff], Av[q >> 16], acc);
-      if (q & 0x8000u) {
-        K[fl[f * NT + tid]] = acc;
-        acc = 0.0;
-        ++f;
+    if (L > 0) {
+      int fcur = fl[tid], fnext = fl[(size_t)min(1, FL - 1) * NT + tid];
+      uint32_t qa[PF];
+#pragma unroll
+      for (int u = 0; u < PF; ++u) qa[u] = st[(size_t)min(u, L - 1) * NT + tid];
+      for (int t0 = 0; t0 < L; t0 += PF) {
+        uint32_t qn[PF];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) qn[u] = st[(size_t)min(t0 + PF + u, L - 1) * NT + tid];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+          const uint32_t q = qa[u];
+          if (t0 + u < L) {
+            acc = fma(Ar[q & 0x7fff], Av[q >> 16], acc);
+            if (q & 0x8000u) {
+              K[fcur] = acc;
+              acc = 0.0;
+              ++f;
+              fcur = fnext;
+              fnext = fl[(size_t)min(f + 1, FL - 1) * NT + tid];
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < PF; ++u) qa[u] = qn[u];
       }
     }
   }
   __syncthreads();
+  T(1);
   {
     const double* __restrict__ Ps = d.Ps + (size_t)b * n + fn->x_off;
     for (int c = tid; c < nw; c += NT) K[lidx(c, c)] += Ps[c] + sigma;
@@ -256,6 +292,7 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
     for (int k = tid; k < nw * (nw + 1) / 2; k += NT) K[k] += Hb[k];
   }
   __syncthreads();
+  T(2);
   double* FS = d.FS + (size_t)b * fs_stride + fn->fs_off;
   double* Ag = FS;
   double* Gg = Ag + X * X;
@@ -288,6 +325,7 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
       if (w == 0 && l == 0 && !(pmin > 0.0)) d.ip_iflag[4 * b] = 1;
     }
     __syncthreads();  // every wave is done with the pivot buffers (they share Gs' region)
+    T(3);
 #pragma unroll
     for (int j = 0; j < NBU; ++j)
 #pragma unroll
@@ -302,6 +340,7 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
         }
       }
     __syncthreads();
+    T(4);
   }
   // ---- A' = A - B G (X x X) on the f64 MFMA: lower 16 x 16 tiles (mt >= nt), K = U in
   // steps of 4; written to both triangles
@@ -334,6 +373,10 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
         }
       }
     }
+  }
+  if (TIMING) {
+    __syncthreads();
+    T(5);
   }
 }
 

@@ -27,7 +27,7 @@ bo.init_solver()
 t = time.time()
 st = bo.solve(timed=True)
 print("solve s", time.time() - t, "phase_ms", st["phase_ms"], "iters", np.bincount(st["admm_iters"]).nonzero())
-ALL = bo.debug("admm_t", B * 32)
+ALL = bo.debug("admm_t", B * 40)[:B * 32]
 T = ALL[:B * 16].reshape(B, 16)
 it = st["admm_iters"].astype(float)
 steps = it * (2 * N)  # one factor block per step

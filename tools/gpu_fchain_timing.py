@@ -1,4 +1,4 @@
-"""Phase timing of the factor chain (k_fchain, s_memtime on thread 0, the last launch of a
+"""Phase timing of the factor (k_fchain and k_fnode, s_memtime on thread 0, the last launch of a
 solve).  Run on the GPU box:  python tools/gpu_fchain_timing.py robot dynamics N B
 Slots (k_factor.hip T(k)): 7 staging, 0 X x X sweep, 1 S_ux, 2 S_uu, 3 Y / Z, 4 E, 6 final store."""
 import os
@@ -21,10 +21,19 @@ bo = BatchedOCP(R, dyn, N, batch=B, device=0)
 bo.set_params(P)
 bo.set_x(X)
 bo.init_solver()
-bo.solve()
-T = bo.debug("admm_t", B * 32)[16 * B:].reshape(B, 16)[:, :8] / (N + 1)
+bo.debug_set("admm_t", np.zeros(B * 40))
+st = bo.solve()
+ALL = bo.debug("admm_t", B * 40)
+T = ALL[16 * B:32 * B].reshape(B, 16)[:, :8] / (N + 1)
+nfac = 2  # factorisations per SQP solve (setup + the rho update; k_fnode launches per group / 2)
+F = ALL[32 * B:].reshape(B, 8)[:, :6] / (N + 1) / nfac
 names = {7: "staging", 0: "X sweep", 1: "S_ux", 2: "S_uu", 3: "Y / Z", 4: "E", 6: "store"}
 print(f"{rob} {dyn} N={N} B={B} kernel={bo.admm_kernel()}: k_fchain cycles per node (thread 0)")
 for k, nm in names.items():
     print(f"  {nm:10s} {T[:, k].mean():10.1f}")
 print(f"  total      {T.sum(1).mean():10.1f}")
+fn = {0: "staging", 1: "assembly", 2: "diag / H", 3: "u sweep", 4: "C / G store", 5: "A' MFMA"}
+print("k_fnode cycles per node (thread 0, one factorisation)")
+for k, nm in fn.items():
+    print(f"  {nm:12s} {F[:, k].mean():10.1f}")
+print(f"  total        {F.sum(1).mean():10.1f}")

@@ -24,7 +24,7 @@ bo.set_params(P)
 bo.set_x(X)
 bo.init_solver()
 st = bo.solve(timed=True)
-T = bo.debug("admm_t", B * 32)[:B * 16].reshape(B, 16)
+T = bo.debug("admm_t", B * 40)[:B * 16].reshape(B, 16)
 it = T[:, 6]
 names = ["P (first)", "C1 chain", "P2", "C2 chain", "P3 + P", "barrier waits"]
 per = T[:, :6] / it[:, None]
