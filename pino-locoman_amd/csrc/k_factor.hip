@@ -243,9 +243,10 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
   T(0);
   // ---- assembly: each thread owns a set of slots; its stream walks their triples
   {
-    // the stream words are prefetched PF steps ahead (double-buffered registers) and the
-    // slot indices two flags ahead: the one-word-per-step loop waited a full L2 round trip
-    // per product (40 k of a B2G node's 70 k cycles, r04); same FMA order
+    // the stream words are prefetched PF steps ahead (double-buffered registers), the slot
+    // indices two flags ahead, and a chunk's LDS operands are read before its slot stores: the
+    // one-word-per-step loop waited an L2 round trip per product (40 k of a B2G node's 70 k
+    // cycles, r04); same FMA order
     const uint32_t* __restrict__ st = d.kasm + fn->asm_off;
     const uint16_t* __restrict__ fl = d.kfl + fn->fl_off;
     const int L = fn->asm_len, FL = fn->fl_len;
@@ -261,11 +262,19 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
         uint32_t qn[PF];
 #pragma unroll
         for (int u = 0; u < PF; ++u) qn[u] = st[(size_t)min(t0 + PF + u, L - 1) * NT + tid];
+        // the chunk's operands first: the slot stores below may alias Ar / Av for the compiler,
+        // which would otherwise issue each load after the previous iteration's store
+        double ar[PF], av[PF];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+          ar[u] = Ar[qa[u] & 0x7fff];
+          av[u] = Av[qa[u] >> 16];
+        }
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
           const uint32_t q = qa[u];
           if (t0 + u < L) {
-            acc = fma(Ar[q & 0x7fff], Av[q >> 16], acc);
+            acc = fma(ar[u], av[u], acc);
             if (q & 0x8000u) {
               K[fcur] = acc;
               acc = 0.0;
