@@ -1,0 +1,20 @@
+#!/bin/bash
+# k_fnode assembly on the f64 MFMA (PL_FNODE_MFA): parity across the factor's users, factor
+# phase timing, headline and configs 1 / 3 A/B.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+T=${1:-r04mf}
+O=gpurun_out/$T
+cd "$R" && mkdir -p "$O"
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu.py tests/test_qp_kernels.py tests/test_ip.py tests/test_admm_kernels.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+for a in "b2g whole_body_rnea 50 1024" "b2 whole_body_aba 40 256"; do
+  n=$(echo $a | tr ' ' '_')
+  timeout -k 10 200 python tools/gpu_fchain_timing.py $a > $O/fac_$n.txt 2>&1 || { tail -5 $O/fac_$n.txt; exit 1; }
+  tail -8 $O/fac_$n.txt
+done
+for v in 1 0; do
+  PL_FNODE_MFA=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/head_mfa$v" -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --host-io-steps 0 > $O/head_mfa$v.log 2>&1 || { tail -5 $O/head_mfa$v.log; exit 1; }
+  echo "mfa=$v $(grep '^{' $O/head_mfa$v.log | tail -1 | grep -o '"ms_per_step": [0-9.]*')"; grep -E "fnode" $O/head_mfa$v/run_kernel_stats.csv | cut -d, -f1-4
+done
