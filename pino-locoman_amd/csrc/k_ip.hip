@@ -24,6 +24,8 @@
 
 using pl::VecIn;
 
+void launch_admm_init_zero(PlOcpHandle* h);  // k_qp.hip: k_admm_init with z = y = 0
+
 #define PL_IP_INF 1e30  // bound on the unbounded rows of the Newton solve (OSQP's infinity)
 
 namespace {
@@ -43,6 +45,28 @@ __device__ __forceinline__ RowKind row_kind(double l, double u) {
   k.hl = !k.eq && isfinite(l);
   k.hu = !k.eq && isfinite(u);
   return k;
+}
+
+// acc + sum over column j's entries of A_e y_row(e) in entry order (the global CSC of
+// d.gc_ptr / d.gc_er), the entry words and the operands of 8 entries loaded together (one
+// dependent round trip per 8 entries instead of per entry); same operations in the same order
+__device__ __forceinline__ double gc_dot(const PlDev& d, int j, const double* A, const double* y, double acc) {
+  const int q0 = d.gc_ptr[j], q1 = d.gc_ptr[j + 1];
+  for (int qb = q0; qb < q1; qb += 8) {
+    int2 er[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) er[u] = d.gc_er[min(qb + u, q1 - 1)];
+    double a[8], t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a[u] = A[er[u].x];
+      t[u] = y[er[u].y];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (qb + u < q1) acc += a[u] * t[u];
+  }
+  return acc;
 }
 
 // red: 256 x K doubles
@@ -203,11 +227,7 @@ __global__ __launch_bounds__(256) void k_ip_kkt(PlDev d, int N, int n, int m, in
   const bool is_max[12] = {true, true, true, false, false, false, true, true, true, true, true, true};
   bool bad = false;
   for (int j = threadIdx.x; j < n; j += 256) {
-    double acc = grad[j];
-    for (int q = d.gc_ptr[j]; q < d.gc_ptr[j + 1]; ++q) {
-      const int2 er = d.gc_er[q];
-      acc += A[er.x] * lam[er.y];
-    }
+    const double acc = gc_dot(d, j, A, lam, grad[j]);
     v[0] = fmax(v[0], fabs(acc));
     bad |= !isfinite(acc);
   }
@@ -332,12 +352,7 @@ __global__ __launch_bounds__(256) void k_ip_kkt(PlDev d, int N, int n, int m, in
   double* xa = d.xa + (size_t)b * n;
   const double* P = d.P + (size_t)b * n;
   for (int j = threadIdx.x; j < n; j += 256) {
-    double acc = grad[j];
-    for (int q = d.gc_ptr[j]; q < d.gc_ptr[j + 1]; ++q) {
-      const int2 er = d.gc_er[q];
-      acc += A[er.x] * lam[er.y];
-    }
-    qs[j] = acc;
+    qs[j] = gc_dot(d, j, A, lam, grad[j]);
     Ps[j] = P[j];
     xa[j] = 0.0;
     d.ip_dx[(size_t)b * n + j] = 0.0;
@@ -443,11 +458,7 @@ __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int N, int n, int m,
     const double dj = dx[j];
     double acc = grad[j] + (Ps[j] + delta_w) * dj;
     if (Hb) acc += qs[j];
-    for (int q = d.gc_ptr[j]; q < d.gc_ptr[j + 1]; ++q) {
-      const int2 er = d.gc_er[q];
-      acc += A[er.x] * t[er.y];
-    }
-    qs[j] = acc;  // rhs = -qs = r
+    qs[j] = gc_dot(d, j, A, t, acc);  // rhs = -qs = r
   }
   __syncthreads();
   for (int j = threadIdx.x; j < n; j += 256) xa[j] = 0.0;
@@ -786,7 +797,7 @@ void enqueue_ip(PlOcpHandle* h) {
     launch_admm(h, 1, 0, 0);
     for (int r = 0; r < st.n_refine; ++r) {
       ip_refine(h, st);
-      launch_admm_init(h);
+      launch_admm_init_zero(h);  // k_ip_refine zeroed x, z, y
       launch_admm(h, 1, 0, 0);
     }
     PL_DISPATCH_DYN(h->oc.dyn, k_ip_step, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->np, st,
@@ -815,7 +826,7 @@ void enqueue_ip_direction(PlOcpHandle* h) {
   launch_admm(h, 1, 0, 0);
   for (int r = 0; r < st.n_refine; ++r) {
     ip_refine(h, st);
-    launch_admm_init(h);
+    launch_admm_init_zero(h);
     launch_admm(h, 1, 0, 0);
   }
   PL_DISPATCH_DYN(h->oc.dyn, k_ip_step, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->np, st, 1);

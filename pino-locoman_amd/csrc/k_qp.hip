@@ -461,7 +461,9 @@ void launch_qp_setup(PlOcpHandle* h) {
 }
 
 // rhs = sigma x - q + A^T (rho z - y)   (before the first iteration of a solve)
-__global__ __launch_bounds__(256) void k_admm_init(PlDev d, int N, int n, int m, int nnz, double sigma) {
+// zero (the interior point's refinement sweeps): z = y = 0, so A^T (rho z - y) adds nothing
+// and the gathers are skipped (rhs = sigma x - q, the same value up to the sign of a zero)
+__global__ __launch_bounds__(256) void k_admm_init(PlDev d, int N, int n, int m, int nnz, double sigma, int zero) {
   const int b = blockIdx.x;
   if (d.info[b].done) return;
   const double* As = d.As + (size_t)b * nnz;
@@ -476,6 +478,10 @@ __global__ __launch_bounds__(256) void k_admm_init(PlDev d, int N, int n, int m,
   constexpr int CK = 8;
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
     double acc = sigma * xa[j] - qs[j];
+    if (zero) {
+      rhs[j] = acc;
+      continue;
+    }
     const int q0 = d.gc_ptr[j], q1 = d.gc_ptr[j + 1];
     for (int q = q0; q < q1; q += CK) {
       int2 er[CK];
@@ -499,7 +505,12 @@ __global__ __launch_bounds__(256) void k_admm_init(PlDev d, int N, int n, int m,
 
 void launch_admm_init(PlOcpHandle* h) {
   hipLaunchKernelGGL(k_admm_init, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz,
-                     h->set.sigma);
+                     h->set.sigma, 0);
+}
+// (k_ip.hip) the refinement sweeps: x = z = y = 0
+void launch_admm_init_zero(PlOcpHandle* h) {
+  hipLaunchKernelGGL(k_admm_init, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz,
+                     h->set.sigma, 1);
 }
 
 // ---------------------------------------------------------------------------
