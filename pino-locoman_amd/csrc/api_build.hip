@@ -825,7 +825,7 @@ int build_factor_prog(pl_ocp* o) {
   const bool mf = !h.fac_gc && !is_short && !(getenv("PL_FCHAIN_MF") && atoi(getenv("PL_FCHAIN_MF")) == 0);
   if (mf) ny = std::max(ny, (2 * X16 * NWS + 1) & ~1);
   h.fchain_ny = ny;
-  h.fchain_short = is_short ? 1 : (mf ? 2 : 0);
+  h.fchain_short = is_short ? (cwlen_max <= 2 ? 3 : 1) : (mf ? 2 : 0);
   h.fchain_ncw = ((is_short ? std::max(ncw_max, 6 * X) : ncw_max) + 1) & ~1;
   h.fchain_nc = h.fac_gc ? nc_max : 0;
   h.fchain_nxc = h.fac_gc ? (nxc_max + 1) & ~1 : 0;

@@ -495,7 +495,7 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
       for (int q = tid; q < nc; q += NT) rcl[q] = rhob[crow[q]];
     } else if (i < N) {
       const int ncwi = (int)cwptr[X];
-      if (short_cw == 1) {
+      if (short_cw == 1 || short_cw == 3) {
         // per row: 4 values (0 past the list) | 4 w columns, so the E loop reads LDS only
         // (the global list words in its inner loop were a chain of dependent loads)
         for (int a = tid; a < X; a += NT) {
@@ -697,31 +697,38 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
       continue;
     }
     // ---- E_{i+1} = D - Kc S Kc^T, Kc row a = rho_a A_{e_a} w_{s_a}^T (one coupling row per column)
-    if (short_cw == 1) {
+    if (short_cw == 1 || short_cw == 3) {
       // short lists: E[a][b] = d_ab - c_a c_b sum_{q in a} A_q sum_{q' in b} A_q' S[c_q][c_q'] straight
-      // from S, in the FMA order of the Y route below (the zero-padded list slots add exact 0s)
-      for (int o = tid; o < X * X; o += NT) {
-        const int a = o / X, bb = o - a * X;
-        if (bb > a) continue;
-        double vb[4];
-        int kb[4];
+      // from S, in the FMA order of the Y route below (the zero-padded list slots add exact 0s;
+      // short_cw 3: lists of at most 2 entries, e.g. the integration rows of rnea / acc, so
+      // only 2 x 2 products per entry)
+      auto eshort = [&](auto lmc) __attribute__((always_inline)) {
+        constexpr int LM = decltype(lmc)::value;
+        for (int o = tid; o < X * X; o += NT) {
+          const int a = o / X, bb = o - a * X;
+          if (bb > a) continue;
+          double vb[LM];
+          int kb[LM];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          vb[k] = sv[4 * bb + k];
-          kb[k] = sk[4 * bb + k];
+          for (int k = 0; k < LM; ++k) {
+            vb[k] = sv[4 * bb + k];
+            kb[k] = sk[4 * bb + k];
+          }
+          double acc = 0.0;
+#pragma unroll
+          for (int j = 0; j < LM; ++j) {
+            const int p = sk[4 * a + j];
+            double y = 0.0;
+#pragma unroll
+            for (int k = 0; k < LM; ++k) y = fma(vb[k], Sl[sidx(p, kb[k])], y);
+            acc = fma(sv[4 * a + j], y, acc);
+          }
+          const double ca = cv[a];
+          Eb[lidx(a, bb)] = (a == bb ? ca * ev[a] : 0.0) - ca * cv[bb] * acc;
         }
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int p = sk[4 * a + j];
-          double y = 0.0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) y = fma(vb[k], Sl[sidx(p, kb[k])], y);
-          acc = fma(sv[4 * a + j], y, acc);
-        }
-        const double ca = cv[a];
-        Eb[lidx(a, bb)] = (a == bb ? ca * ev[a] : 0.0) - ca * cv[bb] * acc;
-      }
+      };
+      if (short_cw == 3) eshort(std::integral_constant<int, 2>{});
+      else eshort(std::integral_constant<int, 4>{});
       T(4);
       continue;
     }

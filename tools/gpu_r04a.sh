@@ -7,7 +7,7 @@ T=${1:-r04a}
 O=gpurun_out/$T
 cd "$R" && mkdir -p "$O"
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu.py tests/test_qp_kernels.py -k "sqp_step or qp or loop" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu.py tests/test_qp_kernels.py tests/test_ip.py -k "sqp_step or qp or loop or ip" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 for a in "b2g whole_body_rnea 50 1024" "b2 whole_body_aba 40 256"; do
   n=$(echo $a | tr ' ' '_')
