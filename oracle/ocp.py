@@ -61,7 +61,7 @@ class OracleOCP:
     """One OCP instance (= one problem) with the reference's semantics."""
 
     def __init__(self, robot, dynamics, nodes, tau_nodes=3, include_acc=True, include_base=True, mu=0.7,
-                 osqp_settings=None):
+                 osqp_settings=None, kkt="quasi_definite"):
         self.robot = robot
         self.dynamics = dynamics
         self.N = nodes
@@ -108,6 +108,7 @@ class OracleOCP:
         self.n = off + self.ndx
         self._pinfo = self._param_layout()
         self.osqp_settings = dict(REFERENCE_SETTINGS if osqp_settings is None else osqp_settings)
+        self.kkt = kkt  # "reduced_block": the GPU's linear algebra (osqp_ref.BlockReduced), a diagnostic
         self.pattern = None
         self.osqp = None
         self.hess_diag = None
@@ -516,7 +517,9 @@ class OracleOCP:
         """ocp.py:265-313 (OSQP branch): constant Hessian diagonal + A pattern."""
         self.hess_diag = self.compute_hess_diag(p)
         self.pattern = self.structural_pattern(p)
-        self.osqp = OSQPRef(self.hess_diag, self.pattern, self.osqp_settings)
+        blocks = [(self.x_off[i], (self.x_off[i + 1] if i < self.N else self.n) - self.x_off[i], self.ndx)
+                  for i in range(self.N + 1)]
+        self.osqp = OSQPRef(self.hess_diag, self.pattern, self.osqp_settings, kkt=self.kkt, blocks=blocks)
 
     def jacobian_values(self, x, p):
         J = self.eval_J(x, p)

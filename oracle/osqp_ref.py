@@ -24,6 +24,18 @@ PARITY UNPINNED (no OSQP binary or test vectors exist in the reference).  The
 KKT system is solved exactly as OSQP's direct path does (full quasi-definite
 KKT, z~ = z_prev + rho^-1 (nu - y)); the factorisation is SuperLU here instead of
 QDLDL+AMD, which changes only round-off.
+
+``kkt="reduced_block"`` (a diagnostic mode, not OSQP's algebra) solves the same ADMM step
+the way the GPU does (csrc/k_factor.hip, csrc/k_admm.hip): the
+reduced SPD system (P + sigma I + A^T R A) x~ = sigma x - q + A^T (rho z - y), z~ = A x~,
+block-tridiagonal over the node blocks w_i = [dx_i, u_i], factored into explicit
+symmetrised block inverses in the GPU's elimination order (per node: C^-1 of the u block,
+G = C^-1 B^T, A' = A - B G, S_xx = (A' + E_i)^-1, S_ux = -G S_xx, S_uu = C^-1 + G S_xx G^T;
+E_{i+1} = -K_{i+1,i} S_i K_{i+1,i}^T) and applied by a forward / backward block sweep.
+Exact arithmetic gives the same iterates; in floating point the explicit inverses of the
+ill-conditioned reduced blocks (sigma = 1e-6 against rho_eq = 20) lose digits the
+quasi-definite LU does not, so this mode separates that formulation error from kernel
+error in the GPU parity tests (tests/test_reduced_oracle.py).
 """
 from __future__ import annotations
 
@@ -64,8 +76,75 @@ def _inf_norm(v):
     return float(np.max(np.abs(v))) if v.size else 0.0
 
 
+def _sym(S):
+    return 0.5 * (S + S.T)
+
+
+class BlockReduced:
+    """The GPU's linear algebra for one ADMM update (see the module docstring):
+    explicit symmetrised inverses S_i of the block-tridiagonal reduced matrix and the
+    forward / backward sweeps.  ``blocks``: (offset, width, ndx) of every node block."""
+
+    def __init__(self, K: sp.csr_matrix, blocks, S_override=None):
+        self.blocks = blocks
+        K = K.tocsr()
+        self.S, self.C = [], []
+        prev = None
+        for i, (o, w, X) in enumerate(blocks):
+            Kii = K[o:o + w, o:o + w].toarray()
+            if i > 0:
+                po, pw, _ = blocks[i - 1]
+                Ci = K[o:o + w, po:po + pw].toarray()
+                if i > 1:  # block tridiagonal: nothing beyond the neighbour
+                    qo, qw, _ = blocks[i - 2]
+                    assert K[o:o + w, qo:qo + qw].nnz == 0
+                Ei = -Ci @ prev @ Ci.T
+            else:
+                Ci, Ei = None, np.zeros((w, w))
+            self.C.append(Ci)
+            Xe = w if np.any(Ei[X:, :]) or np.any(Ei[:, X:]) else X  # E_i on the dx part only (else one stage)
+            if Xe == w:
+                S = _sym(np.linalg.inv(Kii + Ei))
+            else:
+                Am, Bm, Cm = Kii[:X, :X], Kii[:X, X:], Kii[X:, X:]
+                Cinv = _sym(np.linalg.inv(Cm)) if w > X else np.zeros((0, 0))
+                G = Cinv @ Bm.T
+                Ap = Am - Bm @ G
+                Sxx = _sym(np.linalg.inv(Ap + Ei[:X, :X]))
+                Sux = -G @ Sxx
+                Suu = _sym(Cinv + G @ Sxx @ G.T)
+                S = np.block([[Sxx, Sux.T], [Sux, Suu]])
+            if S_override is not None:  # diagnostics: another factor's blocks (e.g. the GPU's)
+                S = S_override[i]
+            self.S.append(S)
+            prev = S
+
+    def solve(self, r):
+        bl, S, C = self.blocks, self.S, self.C
+        bt, wv = [], []
+        for i, (o, w, _) in enumerate(bl):
+            b = r[o:o + w] - (C[i] @ wv[-1] if i > 0 else 0.0)
+            bt.append(b)
+            wv.append(S[i] @ b)
+        x = np.zeros_like(r)
+        xn = None
+        for i in range(len(bl) - 1, -1, -1):
+            o, w, _ = bl[i]
+            xi = wv[i] if xn is None else S[i] @ (bt[i] - C[i + 1].T @ xn)
+            x[o:o + w] = xi
+            xn = xi
+        return x
+
+
 class OSQPRef:
-    def __init__(self, P_diag, A_pattern: sp.csc_matrix, settings=None):
+    def __init__(self, P_diag, A_pattern: sp.csc_matrix, settings=None, kkt="quasi_definite", blocks=None):
+        if kkt not in ("quasi_definite", "reduced_block"):
+            raise ValueError(f"kkt mode {kkt}")
+        if kkt == "reduced_block" and blocks is None:
+            raise ValueError("reduced_block needs the node blocks")
+        self.kkt = kkt
+        self.blocks = blocks
+        self.S_override = None
         self.s = dict(REFERENCE_SETTINGS if settings is None else settings)
         self.n = P_diag.size
         self.m = A_pattern.shape[0]
@@ -126,8 +205,11 @@ class OSQPRef:
         rho[eq] = RHO_EQ_OVER_RHO_INEQ * s["rho"]
         rho_inv = 1.0 / rho
         sigma, alpha = s["sigma"], s["alpha"]
-        KKT = sp.bmat([[sp.diags(P + sigma), A.T], [A, sp.diags(-rho_inv)]], format="csc")
-        lu = spla.splu(KKT, permc_spec="COLAMD")
+        if self.kkt == "quasi_definite":
+            KKT = sp.bmat([[sp.diags(P + sigma), A.T], [A, sp.diags(-rho_inv)]], format="csc")
+            lu = spla.splu(KKT, permc_spec="COLAMD")
+        else:
+            red = BlockReduced(sp.diags(P + sigma) + A.T @ sp.diags(rho) @ A, self.blocks, self.S_override)
         x, z, y = self.x.copy(), self.z.copy(), self.y.copy()
         if not s["warm_start"]:
             x[:], z[:], y[:] = 0, 0, 0
@@ -139,10 +221,14 @@ class OSQPRef:
         can_check = False
         for it in range(1, s["max_iter"] + 1):
             x_prev, z_prev = x, z
-            rhs = np.concatenate([sigma * x_prev - qs, z_prev - rho_inv * y])
-            sol = lu.solve(rhs)
-            xt = sol[:n]
-            zt = (z_prev - rho_inv * y) + rho_inv * sol[n:]
+            if self.kkt == "quasi_definite":
+                rhs = np.concatenate([sigma * x_prev - qs, z_prev - rho_inv * y])
+                sol = lu.solve(rhs)
+                xt = sol[:n]
+                zt = (z_prev - rho_inv * y) + rho_inv * sol[n:]
+            else:  # (P + sigma I + A^T R A) x~ = sigma x - q + A^T (rho z - y), z~ = A x~
+                xt = red.solve(sigma * x_prev - qs + A.T @ (rho * z_prev - y))
+                zt = A @ xt
             x = alpha * xt + (1 - alpha) * x_prev
             delta_x = x - x_prev
             z = np.clip(alpha * zt + (1 - alpha) * z_prev + rho_inv * y, ls, us)

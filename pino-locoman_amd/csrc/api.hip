@@ -1255,6 +1255,7 @@ static int debug_rw(pl_ocp* o, const char* name, double* out, const double* in, 
       {"D", h->d.D, B * h->n},     {"E", h->d.E, B * h->m},         {"cs", h->d.cs, B},
       {"admm_t", h->d.dbg, h->d.dbg ? B * 40 : 0}, {"Ps", h->d.Ps, B * h->n},   {"P", h->d.P, B * h->n},         {"xa", h->d.xa, B * h->n},
       {"za", h->d.za, B * h->m},   {"ya", h->d.ya, B * h->m},       {"S", h->d.S, B * (size_t)h->S_stride},
+      {"FS", h->d.FS, h->d.FS ? B * (size_t)h->fs_stride : 0},
       {"rhs", h->d.rhs, B * h->n}, {"step", h->d.step, B * h->n},   {"grad", h->d.grad, B * h->n},
       {"g", h->d.g, B * h->m},     {"xstate", h->d.xstate, B * h->nx},
       {"ip_s", h->d.ip_s, h->d.ip_s ? B * h->m : 0},     {"ip_lam", h->d.ip_lam, h->d.ip_lam ? B * h->m : 0},

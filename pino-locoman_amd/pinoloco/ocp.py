@@ -456,6 +456,120 @@ class ModelCache:
         return cls._cache[key][1]
 
 
+class ParamSym:
+    """An Opti parameter (or decision) symbol of the reference (``opti.parameter`` /
+    ``opti.x``, ocp.py:54-69): a name that :meth:`Opti.value` reads back and that
+    :class:`CompiledSolver` accepts as an argument slot."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __repr__(self):
+        return f"ParamSym({self.name!r})"
+
+
+# Parameters the drivers read through ocp.opti.value (run_mpc.py:64-77) or pass to the
+# compiled solver (ocp.py:326-335, ocp_whole_body_rnea.py:239-250)
+OPTI_PARAMS = ("x_init", "dt_min", "dt_max", "contact_schedule", "swing_schedule", "n_contacts", "swing_period",
+               "swing_height", "swing_vel_limits", "Q_diag", "R_diag", "base_vel_des", "ext_force_des", "arm_vel_des",
+               "tau_prev", "W_diag")
+
+
+class Opti:
+    """The part of the reference's ``ca.Opti`` its drivers read (run_mpc.py:56-77, 176):
+    ``value(parameter)``, ``value(opti.x, opti.initial())`` (the warm-start point),
+    ``value(opti.x)`` / ``value(opti.lam_g)`` after a solve, and plain numbers (the
+    geometric ``dts``) returned unchanged."""
+
+    x = ParamSym("x")
+    lam_g = ParamSym("lam_g")
+
+    def __init__(self, ocp):
+        self._ocp = ocp
+
+    @staticmethod
+    def initial():
+        return "initial"
+
+    def value(self, sym, initial=None):
+        o = self._ocp
+        if not isinstance(sym, ParamSym):
+            return np.asarray(sym, float) if np.ndim(sym) else float(sym)
+        if sym.name == "x":
+            if initial is not None:
+                return o._x_initial.copy()
+            if o._x_sol is None:
+                raise RuntimeError("opti.value(opti.x): no solution yet (solve first)")
+            return o._x_sol.copy()
+        if sym.name == "lam_g":
+            if o.lam_g is None:
+                raise RuntimeError("opti.value(opti.lam_g): no solution yet (solve first)")
+            return o.lam_g.copy()
+        if sym.name not in o.p:
+            raise RuntimeError(f"opti.value({sym.name}): parameter not set")
+        v = o.p[sym.name]
+        return np.array(v, float) if np.ndim(v) else float(v)
+
+
+class CompiledSolver:
+    """The Fatrop branch's compiled solver (``opti.to_function("compiled_solver", params,
+    [opti.x])``, ocp.py:324-342 and ocp_whole_body_rnea.py:237-258; called as
+    ``sol_x = solver_function(*params)`` at run_mpc.py:100 with the parameter list of
+    run_mpc.py:84-96).  One call is one interior-point solve of this OCP on the GPU from
+    the given parameters and primal warm start (``x_warm_start`` when compiled with
+    ``warm_start``, else the initial guess at compile time).  The function has no lam_g
+    input, so the multipliers start cold, as the reference's generated function does
+    (its lam_g initial is the one baked in at ``to_function`` time, before any solve).
+    A solve that stops at the iteration cap or on a failed line search returns its last
+    iterate (the reference's function returns the solver's output; ``opti.debug``,
+    ocp.py:362-365, in the uncompiled branch).  Returns x as a flat float64 vector."""
+
+    def __init__(self, ocp, names):
+        self._ocp = ocp
+        self.names = list(names)
+        self._x0 = None if "x" in self.names else ocp._x_initial.copy()
+
+    def n_in(self):
+        return len(self.names)
+
+    def name_in(self, i):
+        return self.names[i]
+
+    def _pack(self, args):
+        """(p, x0) of one call: the OCP's current parameters overridden by the arguments."""
+        if len(args) != len(self.names):
+            raise TypeError(f"compiled_solver takes {len(self.names)} arguments ({', '.join(self.names)}), "
+                            f"got {len(args)}")
+        o = self._ocp
+        vals = dict(o.p)
+        x0 = self._x0
+        for name, a in zip(self.names, args):
+            if name == "x":
+                x0 = np.asarray(a, float).ravel()
+                if x0.size != o.layout.n:
+                    raise ValueError(f"x_warm_start has {x0.size} entries, the OCP {o.layout.n}")
+            else:
+                vals[name] = a
+        return o.layout.pack(vals), np.array(x0, float)
+
+    def __call__(self, *args):
+        o = self._ocp
+        p, x0 = self._pack(args)
+        be = o._backend
+        be.set_params(p)
+        be.init_solver()  # the objective's Hessian diagonal from these parameters (ocp.py:293-296)
+        be.set_x(x0)
+        be.set_lam(None)
+        start = time.time()
+        st = be.solve()
+        o.solve_time = time.time() - start
+        o.stats = {k: v[0] for k, v in st.items()}
+        o.stats.update({"ip_" + k: v[0] for k, v in be.ip_stats().items()})
+        x = be.get_x()[0]
+        o._x_sol = x.copy()
+        return x
+
+
 class OCP:
     """Single-problem OCP with the reference's method surface (ocp.py:11-480)."""
 
@@ -492,11 +606,17 @@ class OCP:
         self.lam_g = None
         self.solve_time = None
         self.stats = None
+        self.solver_function = None
+        self._x_sol = None
+        # the Opti view and its parameter symbols (ocp.opti.value(ocp.Q_diag), run_mpc.py:64-77)
+        self.opti = Opti(self)
+        for name in OPTI_PARAMS:
+            setattr(self, name, ParamSym(name))
         self._backend = BatchedOCP(robot, dynamics, nodes, batch=1, device=device, tau_nodes=tau_nodes,
                                    include_acc=include_acc, include_base=include_base,
                                    gait_type=self.gait_sequence.gait_type if self.gait_sequence else "trot",
                                    gait_period=self.gait_sequence.gait_period if self.gait_sequence else 0.8)
-        if solver == "fatrop":
+        if solver == "fatrop" and device >= 0:  # a host-only handle (device < 0) never solves
             self._backend.set_solver("fatrop")
             self._backend.set_ip_settings()
         self.p = {"tau_prev": np.zeros(self.nj), "W_diag": np.zeros(self.nj), "ext_force_des": np.zeros(3),
@@ -599,6 +719,29 @@ class OCP:
         self._backend.set_params(self.param_vector())
         self._backend.init_solver()
 
+    def compile_solver(self, warm_start):
+        """ocp.py:324-353 / ocp_whole_body_rnea.py:237-258.  Fatrop: ``self.solver_function``
+        takes the reference's parameter list -- x_init, dt_min, dt_max, contact_schedule,
+        swing_schedule, n_contacts, swing_period, swing_height, swing_vel_limits, Q_diag,
+        R_diag, base_vel_des, [ext_force_des], [arm_vel_des], [x_warm_start],
+        [tau_prev, W_diag (whole_body_rnea)] -- and returns the solution x (CompiledSolver).
+        OSQP: the reference generates C for sqp_data / f_data / g_data; the library's
+        evaluation is native already (and exported in CasADi's external ABI by
+        casadi_ext), so there is nothing to generate."""
+        if self.solver != "fatrop":
+            return
+        names = ["x_init", "dt_min", "dt_max", "contact_schedule", "swing_schedule", "n_contacts", "swing_period",
+                 "swing_height", "swing_vel_limits", "Q_diag", "R_diag", "base_vel_des"]
+        if self.ext_force_frame:
+            names.append("ext_force_des")
+        if self.arm_ee_frame:
+            names.append("arm_vel_des")
+        if warm_start:
+            names.append("x")
+        if self.dynamics == "whole_body_rnea":
+            names += ["tau_prev", "W_diag"]
+        self.solver_function = CompiledSolver(self, names)
+
     def solve(self, retract_all=True, sqp_iters=1):
         """ocp.py:375-422 (OSQP branch) on the GPU: `sqp_iters` SQP iterations (the
         reference runs one, `for _ in range(1)`, ocp.py:382-383).  With solver
@@ -616,6 +759,7 @@ class OCP:
             self.stats.update({"ip_" + k: v[0] for k, v in self._backend.ip_stats().items()})
             self.lam_g = self._backend.get_lam()[0]
         x = self._backend.get_x()[0]
+        self._x_sol = x.copy()
         self.retract_stacked_sol(x, retract_all)
         return x
 

@@ -229,20 +229,45 @@ def test_ip_gpu_lam_warm_start_matches_oracle():
     bo.close()
 
 
+def _stand_ocp(device):
+    """make_ocp(..., solver="fatrop") for the standing fixture, parameters through the
+    reference's setters (run_mpc.py:166-176, 127-135)."""
+    from pinoloco.ocp import OCP, OCP_ARGS, make_ocp
+    R = make_robot("go2", "stand")
+    if device >= 0:
+        ocp = make_ocp("whole_body_rnea", OCP_ARGS["whole_body_rnea"], robot=R, solver="fatrop", nodes=20)
+    else:
+        ocp = OCP(R, "fatrop", 20, "whole_body_rnea", device=-1)
+        ocp.set_weights()
+    ocp.set_time_params(0.01, 0.08)
+    ocp.set_swing_params(0.07, [0.1, -0.2])
+    ocp.set_tracking_targets(np.zeros(6), np.zeros(3), np.zeros(3))
+    ocp.update_initial_state(np.concatenate([R.q0, np.zeros(R.nv)]))
+    ocp.update_gait_sequence(0.0)
+    ocp.update_previous_torques(np.zeros(R.nj))
+    return ocp
+
+
+def test_make_ocp_setters_reproduce_fixture_params():
+    """The setters give the standing fixture's parameter vector bit for bit (host-only)."""
+    G = golden("ip_go2_rnea_n20_stand.npz")
+    assert np.array_equal(_stand_ocp(-1).param_vector(), G["P"][0])
+
+
 @pytest.mark.gpu
 def test_make_ocp_fatrop_surface():
-    """make_ocp(..., solver="fatrop") -> solve() -> retract / lam_g (ocp.py:360-373)."""
-    from pinoloco.ocp import OCP_ARGS, make_ocp
+    """make_ocp(..., solver="fatrop") -> setters -> init_solver -> solve() -> retract / lam_g
+    (ocp.py:360-373), at the interior point's trajectory bar (1e-7)."""
     G = golden("ip_go2_rnea_n20_stand.npz")
-    R = make_robot("go2", "stand")
-    ocp = make_ocp("whole_body_rnea", OCP_ARGS["whole_body_rnea"], robot=R, solver="fatrop", nodes=20)
-    ocp.param_vector = lambda: G["P"][0]  # the fixture's parameters in place of the setters
-    ocp._x_initial = G["X"][0].copy()
+    ocp = _stand_ocp(0)
+    assert np.array_equal(ocp.param_vector(), G["P"][0])
+    ocp._x_initial = G["X"][0].copy()  # opti.set_initial: the fixture's standing-equilibrium guess
     ocp.init_solver()
     x = ocp.solve()
-    assert ocp.stats["ip_status"] == int(G["status"][0])
-    assert _rel(x, G["x_out"][0]) <= 1e-5
-    assert ocp.lam_g.shape == (G["lam"].shape[1],)
+    assert ocp.stats["ip_status"] == int(G["status"][0]) and ocp.stats["ip_iter"] == int(G["iter"][0])
+    assert _rel(x, G["x_out"][0]) <= TRAJ_TOL
+    assert _rel(ocp.lam_g, G["lam"][0]) <= TRAJ_TOL
+    assert _rel(ocp.opti.value(ocp.opti.x), G["x_out"][0]) <= TRAJ_TOL
     assert len(ocp.q_sol) == 21
 
 
@@ -333,3 +358,116 @@ def test_ip_gpu_gauss_newton_option():
     assert int(st["status"][0]) == so["status"] and int(st["iter"][0]) == so["iter"]
     assert _rel(bo.get_x()[0], x) <= 1e-5 and _rel(bo.get_lam()[0], lam) <= 1e-5
     bo.close()
+
+
+def _run_mpc_setup(device):
+    """run_mpc.py:13-37 and main() (:147-176): B2G standing_with_arm_up, whole_body_rnea,
+    nodes 14, trot 0.8, dt 0.01 / 0.08, the tracking targets and swing parameters."""
+    from pinoloco.ocp import OCP, OCP_ARGS, make_ocp
+    from pinoloco.robots import B2G
+    robot = B2G(reference_pose="standing_with_arm_up", ignore_arm=False)
+    robot.set_gait_sequence("trot", 0.8)
+    if device >= 0:
+        ocp = make_ocp(dynamics="whole_body_rnea", default_args=OCP_ARGS["whole_body_rnea"], robot=robot, nodes=14,
+                       solver="fatrop")
+    else:  # host-only handle (no GPU): the same OCP class surface
+        ocp = OCP(robot, "fatrop", 14, "whole_body_rnea", device=-1)
+        ocp.set_weights()
+    ocp.set_time_params(0.01, 0.08)
+    ocp.set_swing_params(0.07, [0.1, -0.2])
+    ocp.set_tracking_targets(np.array([0.2, 0, 0, 0, 0, 0]), np.array([0, 0, 0]), np.array([0, 0, 0]))
+    return robot, ocp
+
+
+def _compiled_params(ocp, robot, x_init, k, Q_diag, R_diag, W_diag, tau_prev, warm_start=True):
+    """One iteration's parameter list, as run_mpc.py:70-96 builds it."""
+    dt_min, dt_max = 0.01, 0.08
+    t_current = k * dt_min
+    ocp.update_initial_state(x_init)
+    ocp.update_gait_sequence(t_current)
+    contact_schedule = ocp.opti.value(ocp.contact_schedule)
+    swing_schedule = ocp.opti.value(ocp.swing_schedule)
+    n_contacts = ocp.opti.value(ocp.n_contacts)
+    swing_period = ocp.opti.value(ocp.swing_period)
+    params = [x_init, dt_min, dt_max, contact_schedule, swing_schedule, n_contacts,
+              swing_period, 0.07, [0.1, -0.2], Q_diag, R_diag, np.array([0.2, 0, 0, 0, 0, 0])]
+    if ocp.ext_force_frame:
+        params += [np.array([0, 0, 0])]
+    if ocp.arm_ee_frame:
+        params += [np.array([0, 0, 0])]
+    if warm_start:
+        ocp.warm_start()
+        x_warm_start = ocp.opti.value(ocp.opti.x, ocp.opti.initial())
+        params += [x_warm_start]
+    params += [tau_prev, W_diag]
+    return params
+
+
+def test_compiled_solver_surface():
+    """compile_solver / solver_function / opti.value (ocp.py:324-342, ocp_whole_body_rnea.py:
+    237-258, run_mpc.py:56-100) on a host-only handle: the argument list of the reference's
+    generated function, its packing into the parameter vector (bit-equal to the setters'
+    and to the oracle loop's first step, tests/golden/ip_b2g_rnea_n14_compiled.npz), and
+    the arity check."""
+    from pinoloco.ocp import OCP
+    robot, ocp = _run_mpc_setup(-1)
+    ocp.update_initial_state(ocp.x_nom)
+    ocp.update_gait_sequence(0.0)
+    ocp.compile_solver(True)
+    f = ocp.solver_function
+    assert f.n_in() == 17 and f.names[12:] == ["ext_force_des", "arm_vel_des", "x", "tau_prev", "W_diag"]
+    Q, R, W = ocp.opti.value(ocp.Q_diag), ocp.opti.value(ocp.R_diag), ocp.opti.value(ocp.W_diag)
+    params = _compiled_params(ocp, robot, ocp.x_nom, 0, Q, R, W, np.zeros(robot.nj))
+    p, x0 = f._pack(params)
+    assert np.array_equal(p, ocp.param_vector())
+    G = golden("ip_b2g_rnea_n14_compiled.npz")
+    assert np.array_equal(p, G["P"][0]) and np.array_equal(x0, G["X0"][0])
+    with pytest.raises(TypeError):
+        f(*params[:-1])
+    ocp.compile_solver(False)  # without the warm start the initial guess is baked in
+    assert ocp.solver_function.n_in() == 16 and "x" not in ocp.solver_function.names
+    go2 = OCP(make_robot("go2"), "fatrop", 20, "whole_body_rnea", device=-1)
+    go2.compile_solver(True)
+    assert go2.solver_function.n_in() == 15  # no ext force / arm targets
+    osqp = OCP(make_robot("go2"), "osqp", 20, "whole_body_rnea", device=-1)
+    osqp.compile_solver(True)
+    assert osqp.solver_function is None
+    assert ocp.opti.value(0.25) == 0.25  # plain numbers (the dts) pass through
+
+
+@pytest.mark.gpu
+def test_run_mpc_compiled_fatrop_branch():
+    """The reference's default driver configuration -- solver "fatrop", compile_solver = True,
+    warm_start = True (run_mpc.py:34-37) -- through mpc_loop's compiled branch (run_mpc.py:
+    50-113) verbatim for 3 steps, against the oracle's loop (make_golden.py
+    ip_compiled_fixture): per step the interior point's status and iteration count exact, sol_x <= 1e-7 and the next x_init
+    <= 1e-7 relative (the first step's parameters and warm start bit-equal, later ones <= 1e-7:
+    they carry the previous solves' round-off)."""
+    robot, ocp = _run_mpc_setup(0)
+    G = golden("ip_b2g_rnea_n14_compiled.npz")
+    warm_start = True
+    x_init = ocp.x_nom
+    tau_prev = np.zeros(robot.nj)
+    ocp.init_solver()
+    ocp.compile_solver(warm_start)
+    solver_function = ocp.solver_function
+    Q_diag = ocp.opti.value(ocp.Q_diag)
+    R_diag = ocp.opti.value(ocp.R_diag)
+    W_diag = ocp.opti.value(ocp.W_diag)
+    errs = []
+    for k in range(G["P"].shape[0]):
+        params = _compiled_params(ocp, robot, x_init, k, Q_diag, R_diag, W_diag, tau_prev, warm_start)
+        p, x0 = solver_function._pack(params)
+        if k == 0:  # from x_nom: the same parameters bit for bit
+            assert np.array_equal(p, G["P"][k]) and np.array_equal(x0, G["X0"][k])
+        else:  # x_init, tau_prev and the warm start carry the previous solves' round-off
+            assert _rel(p, G["P"][k]) <= 1e-7 and _rel(x0, G["X0"][k]) <= 1e-7, k
+        sol_x = solver_function(*params)
+        st = ocp.stats
+        assert (int(st["ip_status"]), int(st["ip_iter"])) == (int(G["status"][k]), int(G["iter"][k])), (k, st)
+        ocp.retract_stacked_sol(sol_x, retract_all=False)
+        x_init = ocp.dyn.state_integrate()(x_init, ocp.DX_prev[1])
+        tau_prev = ocp.get_tau_sol(i=1)
+        errs.append((_rel(sol_x, G["x_out"][k]), _rel(x_init, G["x_init_next"][k])))
+        assert errs[-1][0] <= 1e-7 and errs[-1][1] <= 1e-7, (k, errs)
+    ocp._backend.close()
