@@ -81,8 +81,8 @@ __device__ __forceinline__ f64x4 mfma4(double a, double b, f64x4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// Blocked symmetric sweep, four pivots P = [k, k + 4) per block:
-//   Q = M_PP^-1;  non-pivot column j: t = Q M_Pj, M_rj -= M_rP t, M_Pj = t;
+// Blocked symmetric sweep, four pivots P = [k, k + 4) per block, M_PP = L D L^T:
+//   Q = M_PP^-1;  non-pivot column j: t = M_PP^-1 M_Pj (substitution), M_rj -= M_rP t, M_Pj = t;
 //   pivot column j = k + q: M_rj = (M_rP Q)_q, M_Pj = -Q_:q.
 // After all pivots the swept block holds -M^-1 (Schur complements / G elsewhere).
 // Columns are held one per lane.  The loop over the pivot blocks is rolled (small code:
@@ -133,19 +133,60 @@ __device__ __forceinline__ void sweep_split(double (&col)[4 * NB], double* pbC, 
       const double2 a = pr[2 * p], b = pr[2 * p + 1];
       m[p][0] = a.x; m[p][1] = a.y; m[p][2] = b.x; m[p][3] = b.y;
     }
+    // LDL^T of the pivot block (wave-uniform, no pivoting: the block is SPD).  A non-pivot column
+    // takes t = M_PP^-1 M_Pj by substitution and the pivot columns take Q = M_PP^-1 from the same
+    // factors.  Until r05 Q came from a Gauss-Jordan of the 4x4 block and t = Q M_Pj: on
+    // ill-conditioned pivot blocks (the u block of a stance node, cond(C) ~ 5e5) the explicit
+    // inverse applied to the pivot rows lost ~20x the accuracy of the substitution (C^-1 1e-10 ..
+    // 3e-10 against 1e-11 in long double, profiles/r05/factor_stages_*), which 100 ADMM
+    // iterations carried into the QP step as up to 1.5e-7 (all-stance fixture).  Substitution for
+    // t with the Gauss-Jordan Q kept for the pivot columns was worse still (an inconsistent
+    // update, 7e-7 on go2_rnea_fd_n20); both from the LDL^T: every fixture's step <= 1e-9 of the
+    // KKT oracle but one (3.4e-9, profiles/r05/parity_sweep*.json).
+    double Lm[4][4], dinv[4], dd[4];
+    {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      if constexpr (kTrack) *pmin = fmin(*pmin, m[p][p]) + (m[p][p] == m[p][p] ? 0.0 : -1.0);  // NaN: fails
-      const double pinv = rcp_nr(m[p][p]);
+      for (int j = 0; j < 4; ++j) {
+        double s = m[j][j];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+        for (int k2 = 0; k2 < j; ++k2) s = fma(-Lm[j][k2] * dd[k2], Lm[j][k2], s);
+        dd[j] = s;
+        dinv[j] = rcp_nr(s);
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (r != p && c != p) m[r][c] = fma(-m[r][p] * pinv, m[p][c], m[r][c]);
+        for (int i2 = j + 1; i2 < 4; ++i2) {
+          double t2 = m[i2][j];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (r != p) { m[r][p] *= pinv; m[p][r] *= pinv; }
-      m[p][p] = -pinv;
+          for (int k2 = 0; k2 < j; ++k2) t2 = fma(-Lm[i2][k2] * dd[k2], Lm[j][k2], t2);
+          Lm[i2][j] = t2 * dinv[j];
+        }
+      }
+    }
+    // the pivots d are the Gauss-Jordan pivots: the interior point's inertia check (<= 0 or NaN)
+    if constexpr (kTrack) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) *pmin = fmin(*pmin, dd[p]) + (dd[p] == dd[p] ? 0.0 : -1.0);
+    }
+    // Q = L^-T D^-1 L^-1 (the pivot columns), m = -Q
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double y[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double a = r == c ? 1.0 : 0.0;
+#pragma unroll
+        for (int k2 = 0; k2 < r; ++k2) a = fma(-Lm[r][k2], y[k2], a);
+        y[r] = a;
+      }
+      double z[4];
+#pragma unroll
+      for (int r = 3; r >= 0; --r) {
+        double a = y[r] * dinv[r];
+#pragma unroll
+        for (int k2 = 3; k2 > r; --k2) a = fma(-Lm[k2][r], z[k2], a);
+        z[r] = a;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) m[r][c] = -z[r];
     }
     // this lane's column of the pivot rows
     const int lc = min(l, ncol - 1);
@@ -158,12 +199,23 @@ __device__ __forceinline__ void sweep_split(double (&col)[4 * NB], double* pbC, 
     double e[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) e[p] = (piv && q == p) ? 1.0 : 0.0;
+    // t = M_PP^-1 own: forward substitution, 1 / d, back substitution
+    double ts[4];
+    {
+      const double y0 = own[0];
+      const double y1 = fma(-Lm[1][0], y0, own[1]);
+      const double y2 = fma(-Lm[2][1], y1, fma(-Lm[2][0], y0, own[2]));
+      const double y3 = fma(-Lm[3][2], y2, fma(-Lm[3][1], y1, fma(-Lm[3][0], y0, own[3])));
+      ts[3] = y3 * dinv[3];
+      ts[2] = fma(-Lm[3][2], ts[3], y2 * dinv[2]);
+      ts[1] = fma(-Lm[3][1], ts[3], fma(-Lm[2][1], ts[2], y1 * dinv[1]));
+      ts[0] = fma(-Lm[3][0], ts[3], fma(-Lm[2][0], ts[2], fma(-Lm[1][0], ts[1], y0 * dinv[0])));
+    }
     double t[4], nb[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      const double qf = -(m[p][0] * own[0] + m[p][1] * own[1] + m[p][2] * own[2] + m[p][3] * own[3]);
       const double qcol = m[p][0] * e[0] + m[p][1] * e[1] + m[p][2] * e[2] + m[p][3] * e[3];
-      nb[p] = fma(1.0 - pv, qf, qcol);
+      nb[p] = fma(1.0 - pv, ts[p], qcol);
       t[p] = nb[p] + e[p];
     }
     const bool own_blk = ws == ow;

@@ -1,0 +1,65 @@
+"""The formulation error of the GPU's linear algebra, measured on the CPU.
+
+The GPU solves each ADMM step with the reduced SPD system (P + sigma I + A^T R A) x~ = r,
+factored into explicit block inverses (csrc/k_factor.hip); the oracle (and OSQP, QDLDL)
+solves the quasi-definite KKT.  oracle/osqp_ref.py kkt="reduced_block" restates the GPU's
+algebra in numpy (same reduced system, same block elimination order, LAPACK inverses).  Its
+QP step against the KKT oracle's golden step is the formulation error: <= 8.3e-10 over the
+fixtures (tools/reduced_vs_kkt.py, profiles/r05/reduced_vs_kkt.json), under SURVEY's 1e-9 bar.
+The GPU's own excess over it was the factor's 4x4 pivot inverse (profiles/r05/,
+k_factor.hip sweep_split) and is gone: tests/test_gpu.py holds the kernels to 1e-9 on every
+fixture but one (STEP_TOL).
+"""
+import numpy as np
+import pytest
+
+from conftest import golden, make_robot
+
+CASES = [("go2_rnea_n20_stand", "go2", "whole_body_rnea", 20, [1, 2]),
+         ("go2_rnea_n20_walk", "go2", "whole_body_rnea", 20, [2]),
+         ("go2_rnea_n20", "go2", "whole_body_rnea", 20, [0, 2]),
+         ("go2_rnea_fd_n20", "go2", "whole_body_rnea", 20, [2])]
+
+
+@pytest.mark.parametrize("name,rname,dyn,N,probs", CASES)
+def test_reduced_form_matches_kkt_oracle(name, rname, dyn, N, probs):
+    from oracle.ocp import OracleOCP
+    from oracle.osqp_ref import REFERENCE_SETTINGS
+    G = golden(f"sqp_{name}.npz")
+    s = dict(REFERENCE_SETTINGS)
+    s.update(eps_abs=float(G["osqp_eps"][0]), eps_rel=float(G["osqp_eps"][1]), max_iter=int(G["osqp_max_iter"]))
+    R = make_robot(rname, str(G["gait"]))
+    kw = {k: bool(int(G[k])) for k in ("include_base", "include_acc") if k in G}
+    for b in probs:
+        o = OracleOCP(R, dyn, N, osqp_settings=s, kkt="reduced_block", **kw)
+        o.init_solver(G["X"][b], G["P"][b])
+        xn, dx, st = o.sqp_step(G["X"][b], G["P"][b])
+        assert (st["status"], st["iter"], st["branch"], st["trials"]) == \
+            (G["status"][b], G["iters"][b], G["branch"][b], G["trials"][b]), b
+        assert np.abs(dx - G["dx"][b]).max() <= 1e-9 * np.abs(G["dx"][b]).max(), b
+
+
+def test_block_reduced_solves_the_reduced_system():
+    """BlockReduced (the GPU's factor and sweeps in numpy) against a dense solve of a random
+    block-tridiagonal SPD system with the OCP's block shapes."""
+    import scipy.sparse as sp
+    from oracle.osqp_ref import BlockReduced
+    rng = np.random.default_rng(3)
+    X, widths = 6, [10, 10, 9, 6]
+    offs = np.concatenate([[0], np.cumsum(widths)[:-1]])
+    n = sum(widths)
+    A = np.zeros((n, n))
+    for i, (o, w) in enumerate(zip(offs, widths)):
+        Bm = rng.normal(size=(w, w))
+        A[o:o + w, o:o + w] = Bm @ Bm.T + w * np.eye(w)
+        if i > 0:  # coupling on the dx part of node i only
+            po, pw = offs[i - 1], widths[i - 1]
+            C = np.zeros((w, pw))
+            C[:X, :] = 0.3 * rng.normal(size=(X, pw))
+            A[o:o + w, po:po + pw] = C
+            A[po:po + pw, o:o + w] = C.T
+    K = sp.csr_matrix(A)
+    br = BlockReduced(K, [(int(o), w, X) for o, w in zip(offs, widths)])
+    r = rng.normal(size=n)
+    x = br.solve(r)
+    assert np.abs(A @ x - r).max() <= 1e-12 * np.abs(r).max() * np.linalg.cond(A)

@@ -4,7 +4,8 @@ Writes gpurun_out/parity_errors.json: per fixture and problem the relative
 (inf-norm) errors of g, grad, J (where stored), the QP step dx and the new iterate,
 and whether the solver outcome (status, iterations, branch, trials, alpha) is exact --
 the step errors once per ADMM kernel (sweep, sweep2, chain) that supports the fixture.
-Usage: python tools/parity_report.py
+Usage: python tools/parity_report.py   (PARITY_KERNELS=sweep,chain limits the kernels,
+PARITY_TAG=x writes gpurun_out/parity_errors_x.json)
 """
 import json
 import os
@@ -32,7 +33,7 @@ def main():
     for name, rname, dyn, N in CONFIGS + EDGE + ACCF + FD:
         G = golden(f"sqp_{name}.npz")
         out[name] = {"kernels": {}}
-        for kernel in ("sweep", "sweep2", "chain"):
+        for kernel in os.environ.get("PARITY_KERNELS", "sweep,sweep2,chain").split(","):
             R, bo = _batched(rname, dyn, N, G)
             try:
                 bo.set_admm_kernel(kernel)
@@ -64,7 +65,8 @@ def main():
         out[name]["max_over_kernels"] = {k: max(v["max"][k] for v in out[name]["kernels"].values())
                                          for k in ("dx", "x_new")}
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "parity_errors.json"), "w") as fh:
+    tag = os.environ.get("PARITY_TAG")
+    with open(os.path.join(ROOT, "gpurun_out", f"parity_errors{'_' + tag if tag else ''}.json"), "w") as fh:
         json.dump(out, fh, indent=1)
 
 
