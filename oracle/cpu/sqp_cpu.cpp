@@ -19,6 +19,8 @@
 #include <math.h>
 #include <omp.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -102,6 +104,8 @@ struct Problem {
   // interior point (built by cpu_ip_prepare): Lagrangian Hessian pairs per node type and the
   // KKT [H + H_L + d I, J^T; J, -W^-1] with the w_i blocks of H_L in its pattern
   bool ip_ready = false;
+  // its own KKT ordering: per node the node's rows, then its variables (ip_prepare)
+  std::vector<int> iperm_x, iperm_z;
   std::vector<std::pair<int, int>> hpairs[3];  // (j, k), j <= k, structurally non-zero (probe)
   Kkt ipk;
   std::vector<int> ik_diag_x, ik_diag_z, ik_A;
@@ -810,15 +814,35 @@ void ip_prepare(Problem& pr) {
     const int t = pl::node_type(pr.O, i);
     if (pr.hpairs[t].empty()) probe_pairs<DYN>(pr, i, pr.hpairs[t]);
   }
-  // KKT pattern: the OSQP branch's (diagonal + A) plus the H_L pairs, same ordering
+  // KKT pattern: diagonal + A plus the H_L pairs, in a rows-first order: per node its rows
+  // (pivots -1 / W_r), then its variables.  Eliminating the rows first adds W_r J_r^T J_r to the
+  // variables, so their pivots are those of the reduced SPD matrix H + H_L + J^T W J the oracle
+  // factors (oracle/ip_ref.py).  The OSQP branch's variables-first order put the objective's
+  // diagonal (down to delta_w = 1e-8 on the unweighted base coordinates) first: its pivots
+  // lost the directions' accuracy (1e-3 at B2G's first iteration) and the inertia count
+  // (shifts of 1e6 where the reduced matrix is positive definite), so the restatement failed
+  // line searches the oracle and the GPU pass (17 of 64 headline problems, r05).
+  pr.iperm_x.assign(n, 0);
+  pr.iperm_z.assign(m, 0);
+  {
+    int idx = 0;
+    for (int i = 0; i <= N; ++i) {
+      const int nri = pr.nrow[i];
+      for (int r = 0; r < nri; ++r) pr.iperm_z[pr.row_off[i] + r] = idx++;
+      if (i == 0) {  // the initial rows DX_0 = 0 (before node 0's own rows in g)
+        for (int r = 0; r < pr.row_off[0]; ++r) pr.iperm_z[r] = idx++;
+      }
+      for (int c = 0; c < pr.nw[i]; ++c) pr.iperm_x[pr.x_off[i] + c] = idx++;
+    }
+  }
   Kkt& kk = pr.ipk;
   kk.K = n + m;
   std::vector<std::vector<std::pair<int, int>>> cols(kk.K);  // (row, tag)
-  for (int j = 0; j < n; ++j) cols[pr.perm_x[j]].push_back({pr.perm_x[j], -1 - j});
-  for (int r = 0; r < m; ++r) cols[pr.perm_z[r]].push_back({pr.perm_z[r], -1 - n - r});
+  for (int j = 0; j < n; ++j) cols[pr.iperm_x[j]].push_back({pr.iperm_x[j], -1 - j});
+  for (int r = 0; r < m; ++r) cols[pr.iperm_z[r]].push_back({pr.iperm_z[r], -1 - n - r});
   for (int j = 0; j < n; ++j)
     for (int k = pr.Ap[j]; k < pr.Ap[j + 1]; ++k) {
-      const int a = pr.perm_x[j], b = pr.perm_z[pr.Ai[k]];
+      const int a = pr.iperm_x[j], b = pr.iperm_z[pr.Ai[k]];
       cols[std::max(a, b)].push_back({std::min(a, b), k});
     }
   const int tagH = 1 << 30;  // pair tags: tagH + running pair index
@@ -827,7 +851,7 @@ void ip_prepare(Problem& pr) {
   for (int i = 0; i < N; ++i) {
     pr.ik_H_off[i] = npair;
     for (auto& jk : pr.hpairs[pl::node_type(pr.O, i)]) {
-      const int a = pr.perm_x[pr.x_off[i] + jk.first], b = pr.perm_x[pr.x_off[i] + jk.second];
+      const int a = pr.iperm_x[pr.x_off[i] + jk.first], b = pr.iperm_x[pr.x_off[i] + jk.second];
       cols[std::max(a, b)].push_back({std::min(a, b), tagH + npair});
       ++npair;
     }
@@ -971,6 +995,7 @@ IpStats ip_solve(const Problem& pr, Work& w, IpWork& iw, const IpSettings& S, co
     return f - mu * (a + b);
   };
   std::vector<std::pair<double, double>> filt;
+  static const bool ip_debug = getenv("CPU_IP_DEBUG") != nullptr;  // per-trial trace (debugging aid)
   IpStats out{IP_MAX_ITER, 0, 0, INFINITY, NAN};
   double f = NAN, err = INFINITY;
   for (int k = 0; k <= S.max_iter; ++k) {
@@ -1044,11 +1069,12 @@ IpStats ip_solve(const Problem& pr, Work& w, IpWork& iw, const IpSettings& S, co
       ++tries;
       assemble(dwi);
     }
+    if (ip_debug) fprintf(stderr, " it %d: inertia shift %.3e after %d tries (dw_last %.3e) mu %.3e\n", k, dwi, tries, dw_last, mu);
     auto kkt_solve = [&](const double* r_x, double* out_x) {
-      for (int j = 0; j < n; ++j) iw.sol[pr.perm_x[j]] = r_x[j];
-      for (int r = 0; r < m; ++r) iw.sol[pr.perm_z[r]] = 0.0;
+      for (int j = 0; j < n; ++j) iw.sol[pr.iperm_x[j]] = r_x[j];
+      for (int r = 0; r < m; ++r) iw.sol[pr.iperm_z[r]] = 0.0;
       ldl_solve(pr.ipk, iw.ldl, iw.sol.data());
-      for (int j = 0; j < n; ++j) out_x[j] = iw.sol[pr.perm_x[j]];
+      for (int j = 0; j < n; ++j) out_x[j] = iw.sol[pr.iperm_x[j]];
     };
     for (int r = 0; r < m; ++r) iw.st[r] = iw.W[r] * iw.rhat[r];
     jt_mul(pr, iw.J.data(), iw.st.data(), iw.rhs.data());
@@ -1121,6 +1147,12 @@ IpStats ip_solve(const Problem& pr, Work& w, IpWork& iw, const IpSettings& S, co
         th_t += fabs(cval(iw.gt.data(), iw.st.data(), r));
       }
       const double ph_t = phi_of(ft, slt.data(), sut.data());
+      if (ip_debug) {
+        double dxm = 0.0;
+        for (int j = 0; j < n; ++j) dxm = fmax(dxm, fabs(iw.dx[j]));
+        fprintf(stderr, "  it %d trial %d a %.3e theta %.4e -> %.4e  phi %.6e -> %.6e  dphi %.3e amax %.3e az %.3e |dx| %.3e\n",
+                k, t, a, theta, th_t, phi, ph_t, dphi, amax, az, dxm);
+      }
       if (!(std::isfinite(th_t) && std::isfinite(ph_t)) || th_t > theta_max) continue;
       bool dominated = false;
       for (auto& fp : filt) dominated |= th_t >= fp.first && ph_t >= fp.second;
@@ -1383,6 +1415,25 @@ extern "C" long long cpu_ip_prepare(void* h) {
   if (pr.O.dyn == PL_DYN_RNEAFD) return -1;  // the Fatrop branch keeps a in u (ocp_whole_body_rnea.py:21)
   if (!pr.ip_ready) PL_CPU_DISPATCH(pr.O.dyn, ip_prepare<D_>(pr));
   return pr.ik_H_off.back();
+}
+
+// The Lagrangian Hessian blocks sum_r lam_r d^2 g_r / dw_i^2 at (p, x, lam), as the interior
+// point forms them, into H [n][n] (dense, both triangles; tests / debugging).
+extern "C" int cpu_ip_lag_hess(void* h, const double* p, const double* x, const double* lam, double* H) {
+  Problem& pr = *(Problem*)h;
+  if (cpu_ip_prepare(h) < 0) return -1;
+  std::vector<double> hv(pr.ik_H_off.back());
+  PL_CPU_DISPATCH(pr.O.dyn, lag_hess<D_>(pr, p, x, lam, hv.data()));
+  const size_t n = pr.n;
+  for (size_t k = 0; k < n * n; ++k) H[k] = 0.0;
+  for (int i = 0; i < pr.N; ++i) {
+    const auto& pl_ = pr.hpairs[pl::node_type(pr.O, i)];
+    for (size_t q = 0; q < pl_.size(); ++q) {
+      const size_t a = pr.x_off[i] + pl_[q].first, b = pr.x_off[i] + pl_[q].second;
+      H[a * n + b] = H[b * n + a] = hv[pr.ik_H_off[i] + q];
+    }
+  }
+  return 0;
 }
 
 // One interior-point solve of one problem from x (in / out); lam [m] in / out (the warm

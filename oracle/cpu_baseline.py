@@ -66,6 +66,7 @@ def lib():
         L.cpu_ip_prepare.restype = C.c_longlong
         L.cpu_ip_prepare.argtypes = [C.c_void_p]
         L.cpu_ip_solve.argtypes = [C.c_void_p, _dp, _dp, _dp, C.c_int, _dp, _ip, _dp]
+        L.cpu_ip_lag_hess.argtypes = [C.c_void_p, _dp, _dp, _dp, _dp]
         L.cpu_ip_mpc_batch.restype = C.c_double
         L.cpu_ip_mpc_batch.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp, C.c_int, C.c_int, _dp, _dp, _ip]
         _lib = L
@@ -148,6 +149,14 @@ class CpuOCP:
         if n < 0:
             raise ValueError("the interior-point restatement needs include_acc=True")
         return n
+
+    def lag_hess(self, x, p, lam):
+        """The restatement's Lagrangian Hessian blocks at (x, p, lam): dense n x n."""
+        H = np.zeros((self.n, self.n))
+        args = [np.ascontiguousarray(np.asarray(a, dtype=np.float64)) for a in (p, x, lam)]
+        if lib().cpu_ip_lag_hess(self.h, *[_d(a) for a in args], _d(H)) != 0:
+            raise ValueError("the interior-point restatement needs include_acc=True")
+        return H
 
     def ip_solve(self, x, p, lam0=None, settings=None):
         """One interior-point solve (oracle/ip_ref.py IPRef.solve restated in C++):

@@ -73,6 +73,10 @@ def _cpu_ip(name, rname, dyn, N):
     ("ip_go2_rnea_n20", "go2", "whole_body_rnea", 20, [0, 2]),
     ("ip_go2_rnea_n20_stand", "go2", "whole_body_rnea", 20, [0]),
     ("ip_go2_cv_nb_n20", "go2", "centroidal_vel", 20, [1]),
+    # the headline shapes: the rows-first KKT order (r05) -- the variables-first order failed
+    # line searches the oracle passes on 5 of these 8 problems each
+    ("ip_b2g_rnea_n50", "b2g", "whole_body_rnea", 50, [3, 7]),
+    ("ip_b2g_acc_n50", "b2g", "whole_body_acc", 50, [4]),
 ])
 def test_cpu_interior_point_matches_golden(name, rname, dyn, N, probs):
     """The C++ interior point (the CPU baseline of bench.py --solver fatrop) against the

@@ -11,7 +11,7 @@ oracle itself on the same seeded inputs.  Tolerances (fp64 throughout):
   factors the reduced system P + sigma I + A^T R A with block inverses, the oracle
   (and the CPU baseline) the quasi-definite KKT with LU / LDL^T; after up to 100 ADMM
   iterations the two differ by <= 1e-9 (profiles/r05/parity_sweep2.json,
-  tools/parity_report.py), the reduced form itself in numpy by <= 8.3e-10
+  tools/parity_report.py), the reduced form itself in numpy by <= 1.4e-9
   (tests/test_reduced_oracle.py);
 * 4-step closed MPC loop on the device: states <= 1e-7 relative (SURVEY 8c);
 * batch invariance and repeatability: bit-exact.
@@ -49,8 +49,8 @@ FD = [("go2_rnea_fd_n20", "go2", "whole_body_rnea", 20), ("b2g_rnea_fd_n50", "b2
 # blocks were inverted explicitly and applied to the pivot rows, which lost ~20x in accuracy on
 # ill-conditioned u blocks; with the LDL^T substitution (k_factor.hip sweep_split) they measure
 # 4.7e-10 / 7.0e-10 (profiles/r05/parity_sweep2.json).  The reduced-form oracle (oracle/osqp_ref.py
-# kkt="reduced_block") shows the formulation itself costs <= 8.3e-10 against the KKT oracle on
-# every fixture (tests/test_reduced_oracle.py).
+# kkt="reduced_block") shows the formulation itself costs <= 1.4e-9 against the KKT oracle
+# (b2_aba_n40; <= 8.3e-10 elsewhere) (tests/test_reduced_oracle.py).
 STEP_TOL = {"go2_rnea_fd_n20": 1e-8}      # measured 3.4e-9 (problem 2; include_acc=False: the
                                           # dense M / dt coupling blocks enter E_{i+1})
 

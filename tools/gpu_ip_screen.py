@@ -1,0 +1,47 @@
+"""Interior-point outcomes of the benchmark batch per MPC step (GPU): which problems end with
+status -2 (failed filter line search), -1 (iteration cap) or 1, at the cold first solve and
+at the warm-started steps after it (lam_g carried, as bench.py --solver fatrop runs them).
+Usage: python tools/gpu_ip_screen.py dynamics batch steps"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "pino-locoman_amd")]
+
+from pinoloco import robots  # noqa: E402
+from pinoloco.ocp import BatchedOCP  # noqa: E402
+from pinoloco.synthetic import build_batch  # noqa: E402
+
+
+def main():
+    dyn, B, steps = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    R = robots.ROBOTS["b2g"]()
+    R.set_gait_sequence("trot", 0.8)
+    lay, P, X, XS, T0 = build_batch(R, dyn, 50, B, 0)
+    bo = BatchedOCP(R, dyn, 50, batch=B, device=0, gait_type="trot", gait_period=0.8)
+    bo.set_solver("fatrop")
+    bo.set_ip_settings()
+    bo.set_params(P)
+    bo.set_x(X)
+    bo.init_solver()
+    bo.mpc_setup(XS, T0)
+    out = []
+    for k in range(steps):
+        bo.mpc_step(k)
+        st = bo.ip_stats()
+        s, it = st["status"], st["iter"]
+        rec = {"step": k, "counts": {int(v): int((s == v).sum()) for v in np.unique(s)},
+               "fail": [[int(b), int(it[b])] for b in np.flatnonzero(s == -2)[:64]]}
+        out.append(rec)
+        print(json.dumps({"step": k, "counts": rec["counts"], "fail_first": rec["fail"][:16]}), flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", f"ip_screen_{dyn}.json"), "w") as f:
+        json.dump(out, f)
+    bo.close()
+
+
+if __name__ == "__main__":
+    main()
