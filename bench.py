@@ -428,8 +428,7 @@ def main():
             # roofline; the ADMM sweeps' HBM line above moves to admm_roofline
             hp = hprof
             h_avg = hp["hess_ms"] / max(1, hp["launches"])
-            mapping = "pairs" if os.environ.get("PL_HESS_PB", "1") == "0" else "pb"
-            hf = measured_hess_flops(B, args.nodes, workload, mapping)
+            hf = measured_hess_flops(B, args.nodes, workload, "pb")
             ach = hf["flops_per_launch"] / (h_avg * 1e-3) / 1e12 if (hf and h_avg > 0) else None
             out["admm_roofline"] = out["roofline"]
             out["roofline"] = {"bound": "fp64_valu", "kernel": "k_lag_hess (+ k_lag_hess_lin for whole_body_rnea)",

@@ -101,7 +101,21 @@ typedef struct {
   /* gait used by the device-side MPC loop (utils/gait_sequence.py:5-24) */
   int gait_type;               /* 0 trot, 1 walk, 2 stand */
   double gait_period;
+  /* 0 in production.  Bits of PL_PATH_*: the paths earlier builds used, kept as the references
+     the regression tests compare the current kernels with (tests/test_r04_paths.py,
+     tests/test_qp_kernels.py, tests/test_graph_gpu.py), and the phase-timing instrumentation.
+     No environment variable changes a kernel path; pl_ocp_sizes reports this field. */
+  unsigned debug_paths;
 } pl_ocp_desc;
+
+#define PL_PATH_JAC_DUAL_ALL    1u   /* rnea a / f Jacobian columns as dual lanes (not k_eval_jac_lin) */
+#define PL_PATH_JAC_CONST_EVERY 2u   /* the constant Jacobian columns re-evaluated every time */
+#define PL_PATH_HESS_FULL_TREE  4u   /* Lagrangian-Hessian passes over the whole tree (no chain confinement) */
+#define PL_PATH_HESS_DUAL_ALL   8u   /* the (dq, a) / (dq, f) Hessian blocks as hyper-dual pairs */
+#define PL_PATH_FCHAIN_LIST     16u  /* the factor chain's E_{i+1} by list sums (not the f64 MFMA) */
+#define PL_PATH_RUIZ_PER_PASS   32u  /* Ruiz equilibration as per-pass kernels (not k_ruiz_fused) */
+#define PL_PATH_NO_MPC_GRAPH    64u  /* pl_mpc_step launches eagerly (no HIP graph) */
+#define PL_PATH_ADMM_TIMING     128u /* s_memtime phase timing in the sweep / factor kernels (pl_debug_get "admm_t") */
 
 typedef struct {
   int status;                  /* OSQP status code (1 solved, 2 inaccurate, -2 max iter, ...) */
@@ -287,11 +301,11 @@ int pl_ocp_get_admm_kernel(const pl_ocp* o);
 
 /* Timing of the dominant kernel (ADMM sweeps) with HIP events on the handle's
  * stream: pl_ocp_profile(o, 1) clears and starts, pl_ocp_profile_read returns
- * [total_ms, launches, problem_iterations]. pl_ocp_sizes (out[12]): [n, m, nnz,
+ * [total_ms, launches, problem_iterations]. pl_ocp_sizes (out[13]): [n, m, nnz,
  * factor doubles per problem, largest node block, N, ADMM gather program length
  * (u16 words, LDS-resident), problems per ADMM workgroup, ADMM LDS bytes per
  * workgroup, A values per thread, A values per problem staged in LDS by the sweep,
- * largest node's A count]. */
+ * largest node's A count, the descriptor's debug_paths bits]. */
 int pl_ocp_profile(pl_ocp* o, int enable);
 int pl_ocp_profile_read(pl_ocp* o, double* out);
 /* The same for the interior point's Lagrangian-Hessian launches (k_lag_hess): out[0] total ms,

@@ -230,12 +230,14 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   // (oracle/ip_ref.py IP_SETTINGS)
   h.ip = PlIpSettings{1e-3, 1e-4, 1e-7, 1e-2, 1e-8, 1e-4, 10, 12, 8, 0, 1e-7};
   h.ip_hess = PL_IP_HESS_EXACT;  // the Lagrangian Hessian (pl_ip_settings.hessian)
-  // ADMM kernel (admm_select below): PL_ADMM_KERNEL = sweep | sweep2 | chain | auto overrides
-  // the batch-size rule at creation, pl_ocp_set_admm_kernel afterwards.
+  // ADMM kernel (admm_select below): the batch-size rule at creation, pl_ocp_set_admm_kernel
+  // afterwards.  No environment variable changes a kernel path: the reference paths of the
+  // regression tests and the phase timing are pl_ocp_desc.debug_paths bits.
+  h.debug_paths = d->debug_paths;
   h.admm_waves = 1;
   h.admm_rc = 0;
   h.rc_waves = 8;
-  h.ruiz_fused = !(getenv("PL_RUIZ_FUSED") && atoi(getenv("PL_RUIZ_FUSED")) == 0);
+  h.ruiz_fused = !(h.debug_paths & PL_PATH_RUIZ_PER_PASS);
   h.ch_stride = rc_ch_stride(h.N, h.ndx);
   h.chv_stride = rc_chv_stride(h.N, h.ndx);
   h.gait_type = d->gait_type;
@@ -304,8 +306,8 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= upload(o, &D.kcpl, o->kcpl);
   {
     std::vector<int2> jl, jlin;
-    // PL_JAC_LIN=0 keeps the rnea a / f columns as dual tree-pass lanes (A/B)
-    const bool use_lin = !(getenv("PL_JAC_LIN") && atoi(getenv("PL_JAC_LIN")) == 0);
+    // PL_PATH_JAC_DUAL_ALL keeps the rnea a / f columns as dual tree-pass lanes (the r03 path)
+    const bool use_lin = !(h.debug_paths & PL_PATH_JAC_DUAL_ALL);
     if (build_jac_list(o, jl, jlin, use_lin, &h.jl_ex)) {
       pl_ocp_destroy(o);
       return -1;
@@ -361,25 +363,14 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   rc |= dalloc(o, &D.t0, B);
   rc |= dalloc(o, &D.xstate, B * (size_t)h.nx);
   D.dbg = nullptr;
-  if (getenv("PL_ADMM_TIMING") && atoi(getenv("PL_ADMM_TIMING")) > 0) rc |= dalloc(o, &D.dbg, B * 40);
+  if (h.debug_paths & PL_PATH_ADMM_TIMING) rc |= dalloc(o, &D.dbg, B * 40);
   if (rc) { pl_ocp_destroy(o); return -2; }
-  {
-    int kind = PL_ADMM_AUTO;
-    if (const char* k = getenv("PL_ADMM_KERNEL")) {
-      if (!strcmp(k, "sweep")) kind = PL_ADMM_SWEEP;
-      else if (!strcmp(k, "sweep2")) kind = PL_ADMM_SWEEP2;
-      else if (!strcmp(k, "chain")) kind = PL_ADMM_CHAIN;
-    }
-    if (admm_select(o, kind)) { pl_ocp_destroy(o); return -2; }
-  }
-  o->mpc_graph_off = getenv("PL_MPC_GRAPH") && atoi(getenv("PL_MPC_GRAPH")) == 0;
-  o->h.admm_scatter = getenv("PL_ADMM_SCATTER") ? atoi(getenv("PL_ADMM_SCATTER")) : 0;  // A/B of k_admm's gathers
-  o->h.admm_defer = !(getenv("PL_ADMM_DEFER") && atoi(getenv("PL_ADMM_DEFER")) == 0);  // k_admm's store placement (A/B)
+  if (admm_select(o, PL_ADMM_AUTO)) { pl_ocp_destroy(o); return -2; }
+  o->mpc_graph_off = (h.debug_paths & PL_PATH_NO_MPC_GRAPH) != 0;
   // the cheap Jacobian columns (dx_{i+1}, rnea tau_j, centroidal_vel h) have constant entries
-  // (+-1, -m): written by the first evaluation only (PL_JAC_CHEAP=1: every evaluation)
-  o->h.jac_cheap_every = getenv("PL_JAC_CHEAP") && atoi(getenv("PL_JAC_CHEAP")) == 1;
+  // (+-1, -m): written by the first evaluation only (PL_PATH_JAC_CONST_EVERY: every evaluation)
+  o->h.jac_cheap_every = (h.debug_paths & PL_PATH_JAC_CONST_EVERY) != 0;
   o->h.jac_cheap_ok = 0;
-  o->h.hess_pb = !(getenv("PL_HESS_PB") && atoi(getenv("PL_HESS_PB")) == 0);  // Hessian mapping (PL_HESS_PB=0: pairs per lane)
   if (hipMemcpy(D.model, &h.model, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(D.oc, &h.oc, sizeof(PlOcpConst), hipMemcpyHostToDevice) != hipSuccess) {
     pl_set_error("upload of model tables failed");
@@ -757,16 +748,16 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
     // whole_body_rnea / whole_body_acc: the rows are linear in a and in the contact forces, and only the RNEA rows
     // couple them to q, so the (dq, a) and (dq, f_feet) blocks are d/dq of M(q) lambda_tau and
     // of -J_e(q) lambda_tau (k_lag_hess_lin: two dual tree passes per dq column instead of one
-    // hyper-dual pass per pair); PL_HESS_LIN=0 keeps them as pairs
+    // hyper-dual pass per pair); PL_PATH_HESS_DUAL_ALL keeps them as pairs
     const bool lin = (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC) &&
-                     !(getenv("PL_HESS_LIN") && atoi(getenv("PL_HESS_LIN")) == 0);
+                     !(h->debug_paths & PL_PATH_HESS_DUAL_ALL);
     const int lin_lo = O.ndx, lin_hi = O.ndx + O.na + 3 * O.nfeet;
     // rnea family and whole_body_acc: the chain of a w_i coordinate (-1: the base, or none).  The rows are sums of
     // per-chain terms that read the base and their own chain only, so a pair with a coordinate
     // of chain c has a mixed part from chain c's terms alone, and its pass skips the other
-    // chains (tree_pass only_ch, packed as .x = node | (chain + 1) << 16).  PL_HESS_CHAIN=0: off
+    // chains (tree_pass only_ch, packed as .x = node | (chain + 1) << 16).  PL_PATH_HESS_FULL_TREE: off
     const bool chains = (PL_IS_RNEA(O.dyn) || O.dyn == PL_DYN_ACC) &&
-                        !(getenv("PL_HESS_CHAIN") && atoi(getenv("PL_HESS_CHAIN")) == 0);
+                        !(h->debug_paths & PL_PATH_HESS_FULL_TREE);
     const PlModel& Mo = h->model;
     const auto joint_chain = [&](int jt) {
       for (int c = 0; c < Mo.nchains; ++c)
@@ -1239,7 +1230,7 @@ extern "C" int pl_ocp_sizes(const pl_ocp* o, long long* out) {
   if (!o) { pl_set_error("null handle"); return -1; }
   out[0] = o->h.n; out[1] = o->h.m; out[2] = o->h.nnz; out[3] = o->h.S_stride; out[4] = o->h.nw_max; out[5] = o->h.N;
   out[6] = (long long)o->aprog.size(); out[7] = admm_ppw(&o->h); out[8] = admm_lds_bytes(&o->h); out[9] = o->h.admm_asr;
-  out[10] = admm_asb_cap(&o->h); out[11] = o->h.nent_max;
+  out[10] = admm_asb_cap(&o->h); out[11] = o->h.nent_max; out[12] = o->h.debug_paths;
   return 0;
 }
 

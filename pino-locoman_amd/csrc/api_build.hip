@@ -413,7 +413,6 @@ int build_admm_prog(pl_ocp* o) {
     for (int q = 0; q < nq; ++q) P.push_back((uint16_t)re[q]);
     bytes(a.rowc, nq, [&](int q) { return ecol[re[q]]; });
     bytes(a.colr, nd.nent, [&](int e) { return rid[e]; });
-    bytes(a.ecol, nd.nent, [&](int e) { return ecol[e]; });  // the entry-order scatters of k_admm
     // coupling rows split into their w part and their dx_{i+1} part
     std::vector<int> cwp{0}, cxp{0};
     std::vector<std::pair<int, int>> cw, cx;
@@ -822,7 +821,7 @@ int build_factor_prog(pl_ocp* o) {
   // list route)
   const bool is_short = !h.fac_gc && cwlen_max <= 4;
   const int X16 = (X + 15) & ~15, NWS = ((h.nw_max + 15) & ~15) + 1;
-  const bool mf = !h.fac_gc && !is_short && !(getenv("PL_FCHAIN_MF") && atoi(getenv("PL_FCHAIN_MF")) == 0);
+  const bool mf = !h.fac_gc && !is_short && !(h.debug_paths & PL_PATH_FCHAIN_LIST);
   if (mf) ny = std::max(ny, (2 * X16 * NWS + 1) & ~1);
   h.fchain_ny = ny;
   h.fchain_short = is_short ? (cwlen_max <= 2 ? 3 : 1) : (mf ? 2 : 0);

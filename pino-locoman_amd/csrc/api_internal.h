@@ -39,7 +39,7 @@ struct pl_ocp {
   // once into a HIP graph and replayed while the handle's host state is unchanged
   hipGraphExec_t mpc_graph = nullptr;
   std::vector<unsigned char> mpc_key;  // bytes of `h` the graph was captured with (or last seen)
-  int mpc_graph_off = 0;               // 1: capture failed or PL_MPC_GRAPH=0: launch eagerly
+  int mpc_graph_off = 0;               // 1: capture failed or PL_PATH_NO_MPC_GRAPH: launch eagerly
   long long mpc_captures = 0;
   long long mpc_replays = 0;           // graph launches (pl_mpc_graph_info)
   void* dl_host = nullptr;             // pinned staging of pl_mpc_download

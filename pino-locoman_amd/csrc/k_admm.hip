@@ -37,8 +37,8 @@
 // diagonal, 4 column partials; both go straight into a per-wave LDS accumulator with
 // ds_add_f64 (PL_ADMM_ATOMIC, r02e; the segment / column-partial arrays of r01 remain as
 // the #else branch).  The backward step's A x~ and A^T (rho z - y) are chunked CSR / CSC
-// gathers; PL_ADMM_SCATTER=1 / 2 (A/B experiments, r04) scatter the node's entries in
-// storage order into LDS row sums / row and column sums instead.  The lanes of one ds_add instruction and the instructions
+// gathers (entry-order scatters into LDS row / column sums were measured slower in r04 and
+// removed).  The lanes of one ds_add instruction and the instructions
 // of one wave apply in a fixed order, so results are bit-identical for a problem
 // regardless of the batch or workgroup it runs in.
 #include <algorithm>
@@ -78,7 +78,7 @@ struct AdmmLds {
 
 }  // namespace
 
-template <int PPW, int ASR, bool TIMING, int SC, bool DS>
+template <int PPW, int ASR, bool TIMING>
 __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int n, int m, int nnz, int ndx,
                                                       int S_stride, int cpl_stride, AdmmLds lm, int niter, int check,
                                                       int fwd_asb, double sigma, double alpha) {
@@ -350,11 +350,10 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   };
 
   // ---------------- the stores of a step (bt of a forward step; rows z, y (dy) and columns x
-  // (dx), rhs of a backward step).  Issued at the step's end, the next step's vmcnt(0) also
-  // waits for their retirement (stores count in vmcnt, in issue order); with DS (default,
-  // PL_ADMM_DEFER=0 turns it off) they are issued right after that wait, from registers
-  // carried across the boundary, so the wait covers only loads and the stores retire
-  // behind a whole step (profiles/r04o: 24.12 -> 23.46 ms per launch at the headline).
+  // (dx), rhs of a backward step).  They are issued right after the next step's wait, from
+  // registers carried across the boundary, so that wait covers only loads and the stores retire
+  // behind a whole step (stores count in vmcnt; issued at the step's end, as until r04, the
+  // next wait also waited for them: profiles/r04o, 24.12 -> 23.46 ms per launch).
   struct StoreSet {
     double kz[MR], ky[MR], kd[MR], kb[MV];
     double2 pxa, pdx, prh;
@@ -406,8 +405,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   auto step = [&](int q) __attribute__((always_inline)) {
     // No store is issued mid-step: on CDNA4 a store's source VGPRs may be reused only after
     // its vmcnt retires, so a mid-step store followed by register reuse would wait and drain
-    // the factor stream.  The step's results go out after the next step's vmcnt(0) (DS, the
-    // default since r04: 24.1 -> 23.5 ms per launch) or at the step's end (DS off).
+    // the factor stream.  The step's results go out after the next step's vmcnt(0).
     double kz[MR], ky[MR], kd[MR], kb[MV];
 #pragma unroll
     for (int mm = 0; mm < MR; ++mm) kz[mm] = ky[mm] = kd[mm] = 0.0;
@@ -457,9 +455,11 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     E = En;
     LR = LRn;
     LC = LCn;
-    if constexpr (DS) {
-      if (pend.kind >= 0) issue_stores(pend);  // step q-1's stores, behind its wait
-    }
+    // the next step's row / column operands right away: a whole step of cover (r05; issued after
+    // the mat-vec / the row gathers until r04, the x update then waited ~2 k cycles for them)
+    prefetch_LR(kind1, i1, LRn);
+    prefetch_LC(kind1, i1, LCn);
+    if (pend.kind >= 0) issue_stores(pend);  // step q-1's stores, behind its wait
     if (bw) stage(ne, Ai);
     else if (fwd_asb && kind != KF0) stage(an[i - 1].nent, As + an[i - 1].ent_off);
     T(0);
@@ -571,37 +571,10 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     T(3);
     matvec(SR, i, false, kind == KT0 ? i : i1, E.tt);
     T(4);
-    if (!bw) {
-      prefetch_LR(kind1, i1, LRn);
-      prefetch_LC(kind1, i1, LCn);
-    }
     if (bw) {
       with_A(ne, Ai, [&](auto A) __attribute__((always_inline)) {
         // ---- z~ = A x~
-        if constexpr (SC >= 1) {
-          // entry-order scatter: entry e = lane + 64 k (storage order: column-major, so the lanes
-          // of one instruction mostly hit distinct rows) adds A_e x~_c into row r with ds_add_f64;
-          // every load is independent (one LDS round trip deep), and row r sums its entries in
-          // column order (the lanes of an instruction and the instructions of the wave apply in
-          // a fixed order: deterministic)
-          const uint8_t* er8 = reinterpret_cast<const uint8_t*>(P + an[i].colr);
-          const uint8_t* ec8 = reinterpret_cast<const uint8_t*>(P + an[i].ecol);
-          for (int o = lane; o < an[i].nrow; o += 64) part[o] = 0.0;
-          wsync();
-          for (int e0 = 0; e0 < ne; e0 += 256) {
-            double t[4];
-            int r[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int e = min(e0 + 64 * u + lane, ne - 1);
-              r[u] = er8[e];
-              t[u] = A(e) * y[ec8[e]];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              if (e0 + 64 * u + lane < ne) lds_add(part + r[u], t[u]);
-          }
-        } else {
+        {
           const uint16_t* rowe = P + an[i].rowe;
           const uint8_t* rowc = reinterpret_cast<const uint8_t*>(P + an[i].rowc);
           const uint32_t* rch = reinterpret_cast<const uint32_t*>(P + an[i].rch);
@@ -640,9 +613,6 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
         }
         wsync();
         T(5);
-        // row / column operands of step q+1 (behind the factor stream, inside the vmcnt window)
-        prefetch_LR(kind1, i1, LRn);
-        prefetch_LC(kind1, i1, LCn);
         // ---- update_z, update_y (relaxed)
         {
           const int nrow = an[i].nrow, ro = an[i].row_off, rcp = an[i].rchptr;
@@ -672,28 +642,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
         wsync();
         T(6);
         // ---- A^T (rho z - y)
-        if constexpr (SC >= 2) {
-          // entry-order scatter into the columns (w_i, then the dx_{i+1} part a2); a column's
-          // entries are contiguous, so the lanes of one instruction share a few column addresses
-          // (applied in lane order); column c sums its rows in row order
-          const uint8_t* er8 = reinterpret_cast<const uint8_t*>(P + an[i].colr);
-          const uint8_t* ec8 = reinterpret_cast<const uint8_t*>(P + an[i].ecol);
-          for (int o = lane; o < an[i].ncol; o += 64) part[o] = 0.0;
-          wsync();
-          for (int e0 = 0; e0 < ne; e0 += 256) {
-            double t[4];
-            int c[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int e = min(e0 + 64 * u + lane, ne - 1);
-              c[u] = ec8[e];
-              t[u] = A(e) * trow[er8[e]];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              if (e0 + 64 * u + lane < ne) lds_add(part + c[u], t[u]);
-          }
-        } else {
+        {
           const uint8_t* colr = reinterpret_cast<const uint8_t*>(P + an[i].colr);
           const uint32_t* cch = reinterpret_cast<const uint32_t*>(P + an[i].cch);
           const int cchn = an[i].cchn;
@@ -810,8 +759,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
       for (int mm = 0; mm < MV; ++mm) cur.kb[mm] = kb[mm];
       cur.pxa = pxa; cur.pdx = pdx; cur.prh = prh; cur.prn = prn;
       cur.kind = kind; cur.i = i; cur.delta = store_delta;
-      if constexpr (DS) pend = cur;
-      else issue_stores(cur);
+      pend = cur;
     }
     T(9);
   };
@@ -822,7 +770,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   prefetch_LC(KF0, 0, LCn);
   load_S(0, 0, SR);
   for (int q = 0; q < Q; ++q) step(q);
-  if constexpr (DS) issue_stores(pend);
+  issue_stores(pend);
   if (lane == 0) {
     info->iter += niter;
     info->iter_prof += niter;  // only problems still iterating reach here (done ones return above)
@@ -919,28 +867,22 @@ AdmmCfg admm_config(const PlOcpHandle* h) {
   return c;
 }
 
-template <int PPW, int ASR, bool TIMING = false, int SC = 0, bool DS = false>
+template <int PPW, int ASR, bool TIMING = false>
 void launch_admm_t(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)k_admm<PPW, ASR, TIMING, SC, DS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
+    hipFuncSetAttribute((const void*)k_admm<PPW, ASR, TIMING>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   const int grid = (h->B + PPW - 1) / PPW;
-  hipLaunchKernelGGL((k_admm<PPW, ASR, TIMING, SC, DS>), dim3(grid), dim3(64 * PPW), c.lds, h->stream, h->d, h->B, h->N, h->n, h->m,
-                     h->nnz, h->ndx, h->S_stride, std::max(h->ncpl_max, 1), c.lm, niter, check, h->admm_fwd_asb,
+  hipLaunchKernelGGL((k_admm<PPW, ASR, TIMING>), dim3(grid), dim3(64 * PPW), c.lds, h->stream, h->d, h->B, h->N, h->n,
+                     h->m, h->nnz, h->ndx, h->S_stride, std::max(h->ncpl_max, 1), c.lm, niter, check, h->admm_fwd_asb,
                      h->set.sigma, h->set.alpha);
 }
 
 template <int ASR>
 void launch_admm_a(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
-  if (c.ppw == 4 && ASR == 16 && h->d.dbg && h->admm_defer) launch_admm_t<4, 16, true, 0, true>(h, niter, check, c);
-  else if (c.ppw == 4 && ASR == 16 && h->d.dbg) launch_admm_t<4, 16, true>(h, niter, check, c);
-  else if (c.ppw == 4 && ASR == 16 && h->admm_defer && h->admm_scatter == 1) launch_admm_t<4, 16, false, 1, true>(h, niter, check, c);
-  else if (c.ppw == 4 && ASR == 16 && h->admm_defer && h->admm_scatter == 0) launch_admm_t<4, 16, false, 0, true>(h, niter, check, c);
-  else if (c.ppw == 4 && ASR == 16 && h->admm_scatter == 1) launch_admm_t<4, 16, false, 1>(h, niter, check, c);
-  else if (c.ppw == 4 && ASR == 16 && h->admm_scatter == 2) launch_admm_t<4, 16, false, 2>(h, niter, check, c);
+  if (c.ppw == 4 && ASR == 16 && h->d.dbg) launch_admm_t<4, 16, true>(h, niter, check, c);  // phase timing
   else if (c.ppw == 4) launch_admm_t<4, ASR>(h, niter, check, c);
   else if (c.ppw == 2) launch_admm_t<2, ASR>(h, niter, check, c);
   else launch_admm_t<1, ASR>(h, niter, check, c);

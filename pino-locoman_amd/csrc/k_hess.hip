@@ -5,13 +5,11 @@
 //     H_L = diag(objective Hessian) + sum_i H_i,   H_i = sum_{rows r of node i} lam_r d^2 g_r / dw_i^2
 // is block diagonal over the w_i: the same sparsity as the factor's diagonal blocks Kt_ii.
 //
-// k_lag_hess: one lane per (node i, column pair j <= k of w_i) of the work list d.hlist
-// (api.hip build_hess_list; pairs with an rnea tau_j column are structurally zero and not
-// listed).  The lane evaluates node i's rows in hyper-dual numbers seeded on columns j and
-// k (ad.h HDual) and contracts the e1 e2 parts with lam: H_i[k][j] = sum_r lam_r g_r.c,
-// written packed lower (k (k + 1) / 2 + j from the node's offset d.hoff[i]), the layout
-// k_fnode assembles Kt_ii in.  Grid (work-list blocks, B); the lanes' kinematic stores
-// (NodeKin<HDual>) are private arrays.
+// The work list d.hlist holds the (node i, column pair j <= k of w_i) pairs (api.hip
+// build_hess_list; pairs with an rnea tau_j column are structurally zero and not listed).  A
+// pair's node rows are evaluated in hyper-dual numbers seeded on columns j and k (ad.h HDual)
+// and the e1 e2 parts contracted with lam: H_i[k][j] = sum_r lam_r g_r.c, written packed lower
+// (k (k + 1) / 2 + j from the node's offset d.hoff[i]), the layout k_fnode assembles Kt_ii in.
 #include "dyn.h"
 #include "eval_common.h"
 
@@ -31,35 +29,11 @@ struct HessEmit {
 
 }  // namespace
 
-template <int DYN>
-__global__ __launch_bounds__(64) void k_lag_hess(PlDev d, int N, int n, int m, int np, int hl_len, long long hl_stride) {
-  const int b = blockIdx.y;
-  if (!d.ipinfo[b].active) return;
-  const PlOcpConst& O = *d.oc;
-  const PlModel& M = *d.model;
-  const double* x = d.x + (size_t)b * n;
-  const double* p = d.p + (size_t)b * np;
-  const double* lam = d.ip_lam + (size_t)b * m;
-  double* H = d.Hlag + (size_t)b * hl_stride;
-  const int ndx = O.ndx;
-  HDual kst[PL_KIN_STORE];
-  for (int q = blockIdx.x * 64 + threadIdx.x; q < hl_len; q += gridDim.x * 64) {
-    const int2 w = d.hlist[q];
-    const int i = w.x & 0xffff, only_ch = (w.x >> 16) - 1, j = w.y & 0xffff, k = w.y >> 16;
-    const PlNode nd = d.nodes[i];
-    const PlNode nn = d.nodes[i + 1];
-    VecIn<HDual> dx{x + nd.x_off, nullptr, 0.0, j, k};
-    VecIn<HDual> u{x + nd.x_off + ndx, nullptr, 0.0, j - ndx, k - ndx};
-    VecIn<HDual> dxn{x + nn.x_off, nullptr, 0.0, j - nd.nw, k - nd.nw};
-    HessEmit e{lam + nd.row_off, 0.0, 0};
-    pl::node_rows<HDual, DYN>(M, O, i, p, dx, u, dxn, e, kst, 1, nullptr, nullptr, nullptr, only_ch);
-    H[d.hoff[i] + k * (k + 1) / 2 + j] = e.acc;
-  }
-}
-
-// The same Hessian with one pair per wave and one PROBLEM per lane (grid: pairs x problem
-// groups of 64): the seeds are wave-uniform, so the row code's seed tests (tree passes a pair
-// does not depend on are skipped) are scalar branches and every lane runs the same path.
+// k_lag_hess_pb: one pair per wave and one PROBLEM per lane (grid: pairs x problem groups of
+// 64): the seeds are wave-uniform, so the row code's seed tests (tree passes a pair does not
+// depend on are skipped) are scalar branches and every lane runs the same path.  (Until r04 a
+// kernel with one pair per lane ran beside it, 298 against 254 ms per evaluation at the
+// headline: removed.)
 template <int DYN>
 __global__ __launch_bounds__(64) void k_lag_hess_pb(PlDev d, int B, int N, int n, int m, int np, long long hl_stride) {
   const int b = blockIdx.y * 64 + threadIdx.x;
@@ -171,14 +145,8 @@ void launch_lag_hess(PlOcpHandle* h) {
     hipLaunchKernelGGL(k_lag_hess_lin, dim3(h->hlin_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,
                        h->m, h->np, h->hl_stride, make_int3(h->hl_rb_base[0], h->hl_rb_base[1], h->hl_rb_base[2]),
                        make_int3(h->hl_rb_tau[0], h->hl_rb_tau[1], h->hl_rb_tau[2]));
-  if (h->hess_pb) {
-    PL_DISPATCH_DYN(h->oc.dyn, k_lag_hess_pb, dim3(h->hl_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->N,
-                    h->n, h->m, h->np, h->hl_stride);
-  } else {
-    const int blocks = std::min((h->hl_len + 63) / 64, std::max(1, 2048 / std::max(h->B, 1)));
-    PL_DISPATCH_DYN(h->oc.dyn, k_lag_hess, dim3(blocks, h->B), dim3(64), 0, h->stream, h->d, h->N, h->n, h->m, h->np,
-                    h->hl_len, h->hl_stride);
-  }
+  PL_DISPATCH_DYN(h->oc.dyn, k_lag_hess_pb, dim3(h->hl_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->N,
+                  h->n, h->m, h->np, h->hl_stride);
   if (prof) {
     hipEventRecord(h->prof_hev[h->prof_hn][1], h->stream);
     h->prof_hn++;

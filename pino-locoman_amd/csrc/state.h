@@ -81,7 +81,7 @@ struct PlAdmmNode {
   unsigned kmagic;  // ceil(2^32 / K): t / K == umulhi(t, kmagic) for the tile counts used
   int x_off, row_off, ent_off, s_off;
   int prog, prog_len;
-  int rowe, rowc, colr, ecol, cwptr, cwp, cxptr, cxp, ccptr, ccp, xcptr, xcp;  // ecol: local column of each entry (u8)
+  int rowe, rowc, colr, cwptr, cwp, cxptr, cxp, ccptr, ccp, xcptr, xcp;
   int rchn, rch, rchptr, cchn, cch, cchptr, rchr, cchc;
   int fprog, flen, f_rowptr, f_cplr, f_rowp;
   int f_cwptr, f_cwp, f_xcptr, f_xcp, f_cxptr, f_cxp;  // coupling lists of the factor program
@@ -257,16 +257,15 @@ struct PlOcpHandle {
   int admm_fwd_asb;                 // coupling rows too dense for registers: forward steps stage A in LDS
   int sqp_iters;                    // SQP iterations per solve (reference: 1, ocp.py:382-383)
   int admm_waves;                   // ADMM sweep kernel: 2 = k_admm2 (two waves per problem), 1 = k_admm
-  int ruiz_fused;                   // 1: all equilibration passes in k_ruiz_fused (PL_RUIZ_FUSED=0: per-pass kernels)
+  int ruiz_fused;                   // 1: all equilibration passes in k_ruiz_fused (PL_PATH_RUIZ_PER_PASS: per-pass kernels)
+  unsigned debug_paths;             // pl_ocp_desc.debug_paths (PL_PATH_*), 0 in production
   int admm_rc;                      // 1: reduced-chain ADMM (k_admm_rc.hip) instead of the sweeps
-  int admm_defer;                   // 1 (default): k_admm issues a step's stores after the next step's wait; 0 (PL_ADMM_DEFER=0): at the step's end
-  int admm_scatter;                 // k_admm's backward row / column sums: 0 chunked gathers, 1 / 2 entry-order scatters for the rows / rows and columns (PL_ADMM_SCATTER, A/B)
   int rc_waves;                     // waves per problem of k_admm_rc (4 or 8)
   long long ch_stride;              // doubles of chain blocks per problem
   int chv_stride;                   // doubles of chain vectors per problem
   int jl_len;                       // k_eval_jac work-list entries (a multiple of 64 before the cheap part)
   int jl_ex;                        // jlist entries before the cheap columns
-  int jac_cheap_every;              // PL_JAC_CHEAP=1: evaluate them every time (A/B)
+  int jac_cheap_every;              // PL_PATH_JAC_CONST_EVERY: evaluate them every time (the r03 path)
   int jlin_len;                     // k_eval_jac_lin work-list entries (0: those columns stay in jlist)
   int solver;                       // PL_SOLVER_OSQP (SQP + OSQP ADMM) or PL_SOLVER_IP (interior point)
   int ip_lam_warm;                  // 1: the next interior-point solve starts from lam = ip_lam0
@@ -274,7 +273,6 @@ struct PlOcpHandle {
   int hl_len;                       // Lagrangian Hessian work list (k_lag_hess)
   int hlin_len;                     // k_lag_hess_lin work list (0: every pair by hyper-dual passes)
   int hl_rb_base[3], hl_rb_tau[3];  // per node type: first row of the RNEA base / joint-torque rows (-1: none)
-  int hess_pb;                      // 1 (default): k_lag_hess_pb, one pair per wave and one problem per lane; 0 (PL_HESS_PB=0): one pair per lane
   long long hl_stride;              // doubles per problem of d.Hlag
   int fac_hlag;                     // 1: k_fnode adds d.Hlag to Kt_ii and both factor kernels report pivots <= 0
   int fac_only;                     // 1: the factor kernels skip problems whose d.ip_iflag refactor flag is clear

@@ -34,7 +34,14 @@ class OcpDesc(C.Structure):
                 ("rho", C.c_double), ("sigma", C.c_double), ("alpha", C.c_double), ("eps_abs", C.c_double),
                 ("eps_rel", C.c_double), ("eps_prim_inf", C.c_double), ("eps_dual_inf", C.c_double),
                 ("max_iter", C.c_int), ("scaling", C.c_int), ("check_termination", C.c_int),
-                ("warm_start", C.c_int), ("gait_type", C.c_int), ("gait_period", C.c_double)]
+                ("warm_start", C.c_int), ("gait_type", C.c_int), ("gait_period", C.c_double),
+                ("debug_paths", C.c_uint)]
+
+
+# pl_ocp_desc.debug_paths bits (include/pinoloco.h PL_PATH_*): the earlier builds' paths the
+# regression tests compare with, and the phase-timing instrumentation; 0 in production
+PATHS = {"jac_dual_all": 1, "jac_const_every": 2, "hess_full_tree": 4, "hess_dual_all": 8, "fchain_list": 16,
+         "ruiz_per_pass": 32, "no_mpc_graph": 64, "admm_timing": 128}
 
 
 class Stats(C.Structure):

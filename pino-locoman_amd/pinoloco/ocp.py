@@ -156,7 +156,9 @@ class BatchedOCP:
     """A batch of independent OCPs of one (robot, dynamics, N) on one GPU."""
 
     def __init__(self, robot, dynamics, nodes, batch=1, device=0, tau_nodes=3, include_acc=True,
-                 include_base=True, gait_type="trot", gait_period=0.8, osqp_settings=None, mu=0.7):
+                 include_base=True, gait_type="trot", gait_period=0.8, osqp_settings=None, mu=0.7, debug_paths=()):
+        """debug_paths: names of _lib.PATHS (the reference paths of the regression tests and the
+        phase timing); empty in production."""
         if dynamics not in DYN_CODES:
             raise ValueError(f"Unknown dynamics type: {dynamics}")
         L = _lib.lib()
@@ -205,6 +207,12 @@ class BatchedOCP:
         d.warm_start = int(bool(s["warm_start"]))
         d.gait_type = GAIT_CODES[gait_type]
         d.gait_period = float(gait_period)
+        bits = 0
+        for name in debug_paths:
+            if name not in _lib.PATHS:
+                raise ValueError(f"unknown debug path {name} (choose from {sorted(_lib.PATHS)})")
+            bits |= _lib.PATHS[name]
+        d.debug_paths = bits
         h = C.c_void_p()
         _lib.check(L.pl_ocp_create(self.model_h.h, C.byref(d), batch, device, C.byref(h)))
         self.h = h
@@ -428,10 +436,10 @@ class BatchedOCP:
         return {"hess_ms": out[0], "launches": int(out[1])}
 
     def sizes(self):
-        out = (C.c_longlong * 12)()
+        out = (C.c_longlong * 13)()
         _lib.check(_lib.lib().pl_ocp_sizes(self.h, out))
         return dict(zip(("n", "m", "nnz", "S_stride", "nw_max", "N", "admm_prog", "admm_ppw", "admm_lds_bytes",
-                         "admm_asr", "admm_asb_cap", "nent_max"), [int(v) for v in out]))
+                         "admm_asr", "admm_asb_cap", "nent_max", "debug_paths"), [int(v) for v in out]))
 
     def close(self):
         if getattr(self, "h", None):

@@ -91,10 +91,9 @@ IP_CONFIGS = [
     ("ip_go2_rnea_n20_stand", "go2", "whole_body_rnea", 20, [("stand",), ("syn", 30)], 2, "stand"),
     ("ip_go2_cv_n20", "go2", "centroidal_vel", 20, [("syn", 0), ("syn", 1)], 0, "trot"),
     ("ip_b2_aba_n40", "b2", "whole_body_aba", 40, [("syn", 0)], 0, "trot"),
-    # the headline shapes: problems of the benchmark batch (build_batch(..., 0) = ("syn", k)),
-    # chosen by screening the first 64 with the compiled restatement (oracle/cpu) to hold both
-    # exits the benchmark sees: status -1 (iteration cap) and -2 (filter line search failed,
-    # no restoration phase; the reference falls back to opti.debug, ocp.py:362-365)
+    # the headline shapes: eight problems of the benchmark batch each (build_batch(..., 0) =
+    # ("syn", k)), cold first solves: all stop at the iteration cap (status -1); the failed
+    # line searches (-2) of the benchmark come at warm-started steps (IP_WARM_CONFIGS)
     ("ip_b2g_acc_n50", "b2g", "whole_body_acc", 50, [("syn", k) for k in (0, 1, 2, 7, 23, 29, 39, 43)], 0, "trot"),
     ("ip_b2g_rnea_n50", "b2g", "whole_body_rnea", 50, [("syn", k) for k in (0, 1, 2, 7, 10, 19, 44, 47)], 0, "trot"),
     # centroidal_vel from the feasible standing point (a well-conditioned trajectory beside the
@@ -438,8 +437,82 @@ def ip_compiled_fixture(steps=3):
     np.savez_compressed(os.path.join(HERE, "ip_b2g_rnea_n14_compiled.npz"), **{k: np.array(v) for k, v in rec.items()})
 
 
+# Warm-started interior-point solves of the benchmark loop (bench.py --solver fatrop): the cold
+# first solves of the batch never fail the filter line search, the -2 exits come at MPC steps
+# >= 2 (tools/gpu_ip_screen.py).  Problems of the benchmark batch ("syn" k), chosen from that
+# screen: five that fail at step 2 and three that stop at the iteration cap.
+IP_WARM_CONFIGS = [
+    ("ip_b2g_rnea_n50_warm", "whole_body_rnea", [1, 8, 11, 14, 17, 0, 2, 3]),
+    ("ip_b2g_acc_n50_warm", "whole_body_acc", [8, 11, 14, 17, 21, 0, 1, 2]),
+]
+
+
+def _ip_warm_one(args):
+    """Steps 0 and 1 of the problem's MPC loop with the compiled restatement (oracle/cpu, the
+    oracle's algorithm to <= 3e-12 on these shapes), then step 2 -- the fixture -- with the numpy
+    oracle from the loop's warm start (x: OracleOCP.warm_start of step 1's solution; lam_g:
+    step 1's multipliers, ocp_whole_body_rnea.py:207-235, ocp.py:373)."""
+    from oracle.cpu_baseline import CpuOCP
+    from oracle.ip_ref import IPRef
+    dyn, gidx = args
+    R = robots.ROBOTS["b2g"]()
+    R.set_gait_sequence("trot", 0.8)
+    N = 50
+    lay = Layout(R, dyn, N)
+    o = OracleOCP(R, dyn, N)
+    c = CpuOCP(R, dyn, N)
+    p, x, xs, t0 = make_problem(R, lay, dyn, N, ("syn", gidx))
+    lam = None
+    pre = []
+    for k in range(3):
+        if k > 0:
+            contact, swing = R.gait_sequence.get_gait_schedule(t0 + k * DT_MIN, horizon_dts(DT_MIN, DT_MAX, N), N)
+            vals = {"x_init": xs, "contact_schedule": contact, "swing_schedule": swing}
+            for key in vals:
+                o_, s_ = lay.poff[key]
+                p[o_:o_ + s_] = lay.pack(vals)[o_:o_ + s_]
+            x = o.warm_start(x, p)
+        if k == 2:
+            break
+        x, lam, st = c.ip_solve(x, p, lam0=lam)
+        pre.append([st["status"], st["iter"]])
+        DX, _ = o.split(x)
+        xs = o.integrate_state(xs, DX[1])
+    ip = IPRef(o)
+    xo, lo, st = ip.solve(x, p, lam0=lam)
+    print(f"  {dyn} syn {gidx}: steps 0-1 {pre}, step 2 status {st['status']} iter {st['iter']}", flush=True)
+    return dict(P=p.copy(), X=x.copy(), LAM0=np.array(lam), XS=xs.copy(), x_out=xo, lam=lo, st=st, pre=pre)
+
+
+def ip_warm_fixture(name, dyn, gidx):
+    from concurrent.futures import ProcessPoolExecutor
+    from oracle.ip_ref import IP_SETTINGS
+    workers = min(len(gidx), int(os.environ.get("GOLDEN_WORKERS", "8")))
+    with ProcessPoolExecutor(workers) as ex:
+        res = list(ex.map(_ip_warm_one, [(dyn, g) for g in gidx]))
+    mi = IP_SETTINGS["max_iter"]
+    rec = {"gidx": np.array(gidx), "step": 2, "gait": np.array("trot"), "include_base": 1}
+    for key in ("P", "X", "LAM0", "XS", "x_out", "lam"):
+        rec[key] = np.array([r[key] for r in res])
+    for key in ("status", "iter", "err", "mu", "f"):
+        rec[key] = np.array([r["st"][key] for r in res])
+    for key in ("s", "zl", "zu"):
+        rec[key] = np.array([r["st"][key] for r in res])
+    al = np.zeros((len(res), mi))
+    for b, r in enumerate(res):
+        al[b, :len(r["st"]["alphas"])] = r["st"]["alphas"]
+    rec["alphas"] = al
+    rec["trials"] = np.array([int(np.sum(r["st"]["trials"])) for r in res])
+    rec["pre_stats"] = np.array([r["pre"] for r in res])
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **rec)
+    print(name, "status", rec["status"], "iter", rec["iter"], flush=True)
+
+
 def main():
     only = sys.argv[1:]
+    for cfg in IP_WARM_CONFIGS:
+        if cfg[0] in only:
+            ip_warm_fixture(*cfg)
     if "ip_b2g_rnea_n14_compiled" in only:
         ip_compiled_fixture()
     for cfg in IP_CONFIGS:

@@ -76,12 +76,13 @@ def _kw(G):
     return {k: bool(int(G[k])) if k in G else True for k in ("include_base", "include_acc")}
 
 
-def _batched(rname, dyn, N, G, B=None):
+def _batched(rname, dyn, N, G, B=None, debug_paths=()):
     from pinoloco.ocp import BatchedOCP
     settings, gait = _settings(G)
     R = make_robot(rname, gait)
     B = B or G["P"].shape[0]
-    bo = BatchedOCP(R, dyn, N, batch=B, device=0, osqp_settings=settings, gait_type=gait, **_kw(G))
+    bo = BatchedOCP(R, dyn, N, batch=B, device=0, osqp_settings=settings, gait_type=gait, debug_paths=debug_paths,
+                    **_kw(G))
     bo.set_params(G["P"][:B])
     bo.set_x(G["X"][:B])
     bo.init_solver()

@@ -1,10 +1,8 @@
 """MPC-step graph replay (pl_mpc_step, api.hip): the OSQP-SQP launches of a step are
 captured once into a HIP graph and replayed.  A replay must be the eager launch sequence:
 states, iterates and solver statistics bit-identical to a handle created with
-PL_MPC_GRAPH=0, including across a setter that changes the handle mid-loop (re-capture), and the capture /
+the no_mpc_graph debug path, including across a setter that changes the handle mid-loop (re-capture), and the capture /
 replay counters (pl_mpc_graph_info) show that the graph path ran."""
-import os
-
 import numpy as np
 import pytest
 
@@ -16,16 +14,8 @@ pytestmark = pytest.mark.gpu
 def _loop(R, dyn, N, B, steps, graph, switch_at=None):
     from pinoloco.ocp import BatchedOCP
     from pinoloco.synthetic import build_batch
-    old = os.environ.get("PL_MPC_GRAPH")
-    os.environ["PL_MPC_GRAPH"] = "1" if graph else "0"
-    try:
-        lay, P, X, XS, T0 = build_batch(R, dyn, N, B, 0)
-        bo = BatchedOCP(R, dyn, N, batch=B, device=0)
-    finally:
-        if old is None:
-            del os.environ["PL_MPC_GRAPH"]
-        else:
-            os.environ["PL_MPC_GRAPH"] = old
+    lay, P, X, XS, T0 = build_batch(R, dyn, N, B, 0)
+    bo = BatchedOCP(R, dyn, N, batch=B, device=0, debug_paths=() if graph else ("no_mpc_graph",))
     bo.set_params(P)
     bo.set_x(X)
     bo.init_solver()

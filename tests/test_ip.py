@@ -94,16 +94,26 @@ def test_ip_oracle_lam_warm_start():
         assert np.all(t0["zu"][lam0 > 1e-7] == lam0[lam0 > 1e-7])
 
 
+# Warm-started solves of the benchmark's MPC loop at step 2 (make_golden.py ip_warm_fixture):
+# the exit the benchmark sees on ~30 % of its problems, a failed filter line search (status -2,
+# no restoration phase: the last iterate is returned, as opti.debug does, ocp.py:362-365)
+IP_WARM_FIXTURES = [("ip_b2g_rnea_n50_warm", "b2g", "whole_body_rnea", 50),
+                    ("ip_b2g_acc_n50_warm", "b2g", "whole_body_acc", 50)]
+
+
 def test_ip_fixture_coverage():
-    """The fixtures exercise convergence, the iteration limit, every dynamics family and
-    fraction-to-boundary-limited steps (alpha < 1)."""
+    """The fixtures exercise convergence, the iteration limit, the failed line search, every
+    dynamics family and fraction-to-boundary-limited steps (alpha < 1)."""
     st, dyns, alphas = [], set(), []
-    for name, _, dyn, _ in IP_FIXTURES:
+    for name, _, dyn, _ in IP_FIXTURES + IP_WARM_FIXTURES:
         G = golden(f"{name}.npz")
         st += [int(s) for s in G["status"]]
         dyns.add(dyn)
         alphas.append(np.asarray(G["alphas"]).ravel())
-    assert 1 in st and -1 in st
+    assert 1 in st and -1 in st and -2 in st
+    for name, *_ in IP_WARM_FIXTURES:  # each warm fixture holds both exits of the benchmark
+        G = golden(f"{name}.npz")
+        assert {-1, -2} <= set(int(s) for s in G["status"]) and G["P"].shape[0] >= 8, name
     assert dyns == {"whole_body_rnea", "whole_body_acc", "whole_body_aba", "centroidal_vel", "centroidal_acc"}
     # both forms of the base in u (include_base False: ocp_centroidal_vel.py:9-23, ocp_whole_body_acc.py:124-135)
     assert {int(golden(f"{n}.npz")["include_base"]) for n, *_ in IP_FIXTURES if "include_base" in golden(f"{n}.npz")} == {0, 1}
@@ -173,6 +183,41 @@ def test_ip_gpu_matches_oracle(name, rname, dyn, N):
         assert e["alphas"] <= TRAJ_TOL, e
         assert e["x"] <= TRAJ_TOL, e
         assert e["lam"] <= TRAJ_TOL, e
+    bo.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,rname,dyn,N", IP_WARM_FIXTURES)
+def test_ip_gpu_warm_started_matches_oracle(name, rname, dyn, N):
+    """The benchmark loop's step-2 solves (warm start x and lam_g from step 1) against the
+    oracle: status (-2 included), iteration count and every accepted step exact / <= 1e-7, the
+    returned iterate x and lam_g <= 1e-7 relative.  A failed solve records alpha 0 for its
+    last iteration (ip_ref.py), the GPU the same."""
+    from pinoloco.ocp import BatchedOCP
+    G = golden(f"{name}.npz")
+    B = G["P"].shape[0]
+    bo = BatchedOCP(make_robot(rname, "trot"), dyn, N, batch=B, device=0, gait_type="trot")
+    bo.set_solver("fatrop")
+    bo.set_ip_settings()
+    bo.set_params(G["P"])
+    bo.set_x(G["X"])
+    bo.init_solver()
+    bo.set_lam(G["LAM0"])
+    bo.solve()
+    X, LAM, st = bo.get_x(), bo.get_lam(), bo.ip_stats()
+    errs = []
+    for b in range(B):
+        n_it = int(G["iter"][b]) + (1 if int(G["status"][b]) == -2 else 0)  # incl. the failed iteration's 0
+        errs.append(dict(problem=b, gidx=int(G["gidx"][b]), status=int(st["status"][b]),
+                         status_oracle=int(G["status"][b]), iter=int(st["iter"][b]), iter_oracle=int(G["iter"][b]),
+                         x=_rel(X[b], G["x_out"][b]), lam=_rel(LAM[b], G["lam"][b]),
+                         alphas=_rel(st["alphas"][b][:n_it], G["alphas"][b][:n_it])))
+    os.makedirs(os.path.join(HERE, "..", "gpurun_out"), exist_ok=True)
+    with open(os.path.join(HERE, "..", "gpurun_out", f"ip_parity_{name}.json"), "w") as f:
+        json.dump(errs, f, indent=1)
+    for e in errs:
+        assert (e["status"], e["iter"]) == (e["status_oracle"], e["iter_oracle"]), e
+        assert e["alphas"] <= TRAJ_TOL and e["x"] <= TRAJ_TOL and e["lam"] <= TRAJ_TOL, e
     bo.close()
 
 

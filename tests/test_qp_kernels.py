@@ -1,9 +1,7 @@
 """QP-setup kernels on the MI355X: the fused equilibration (k_ruiz_fused, all Ruiz passes of
 OSQP 0.6 scale_data in one launch) against the per-pass kernels (k_ruiz_norms +
-k_ruiz_update, PL_RUIZ_FUSED=0): D, E, c and the scaled data bit for bit, and the SQP
+k_ruiz_update, debug path ruiz_per_pass): D, E, c and the scaled data bit for bit, and the SQP
 outcome and step bit for bit (optimization/ocp.py:391-401, osqp.update + osqp.solve)."""
-import os
-
 import numpy as np
 import pytest
 
@@ -14,12 +12,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(name, rname, dyn, N, fused):
-    os.environ["PL_RUIZ_FUSED"] = "1" if fused else "0"
-    try:
-        G = golden(f"sqp_{name}.npz")
-        R, bo = _batched(rname, dyn, N, G)
-    finally:
-        os.environ.pop("PL_RUIZ_FUSED", None)
+    G = golden(f"sqp_{name}.npz")
+    R, bo = _batched(rname, dyn, N, G, debug_paths=() if fused else ("ruiz_per_pass",))
     st = bo.solve()
     B = bo.batch
     out = {k: bo.debug(k, B * sz) for k, sz in (("D", bo.n), ("E", bo.m), ("cs", 1), ("As", bo.nnz), ("Ps", bo.n),

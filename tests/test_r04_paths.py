@@ -1,16 +1,16 @@
 """The round-4 rewrites of the Jacobian, the Lagrangian Hessian and the factor chain against
-the paths they replaced, on the same handle inputs (the A/B switches are read when a handle
-is created).  Each rewrite is an exact identity in real arithmetic, so the two paths agree to
+the paths they replaced, on the same handle inputs (the replaced paths are selected by the
+handle's pl_ocp_desc.debug_paths bits, BatchedOCP(debug_paths=...)).  Each rewrite is an exact identity in real arithmetic, so the two paths agree to
 round-off:
 
 * Jacobian (k_eval_jac_lin: the rnea / acc a and f columns from primal zero-gravity RNEA passes
   confined to one chain; the constant columns written by the first evaluation only) vs
-  PL_JAC_LIN=0 + PL_JAC_CHEAP=1 (the base-position columns skip the tree pass in both): <= 1e-13
+  jac_dual_all + jac_const_every (the base-position columns skip the tree pass in both): <= 1e-13
   relative to max |J|, at two evaluation points of one handle (the second evaluation runs
   without the constant columns);
 * Lagrangian Hessian (pairs confined to one chain, the linear-column blocks) vs
-  PL_HESS_CHAIN=0 + PL_HESS_LIN=0: <= 1e-12 relative to max |H|;
-* the factor chain's E_{i+1} on the f64 MFMA (aba, centroidal) vs PL_FCHAIN_MF=0 (the list
+  hess_full_tree + hess_dual_all: <= 1e-12 relative to max |H|;
+* the factor chain's E_{i+1} on the f64 MFMA (aba, centroidal) vs fchain_list (the list
   route): one SQP step, solver outcome exact and the QP step <= 2e-9 relative.
 """
 import numpy as np
@@ -43,14 +43,10 @@ def _handle(name, rname, dyn, N, **kw):
 @pytest.mark.parametrize("name,rname,dyn,N", [("b2g_rnea_n50", "b2g", "whole_body_rnea", 50),
                                                ("b2g_acc_n50", "b2g", "whole_body_acc", 50),
                                                ("go2_rnea_fd_n20", "go2", "whole_body_rnea", 20)])
-def test_jacobian_rewrites_match_dual_columns(name, rname, dyn, N, monkeypatch):
+def test_jacobian_rewrites_match_dual_columns(name, rname, dyn, N):
     out = {}
-    for tag, env in (("new", {}), ("old", {"PL_JAC_LIN": "0", "PL_JAC_CHEAP": "1"})):
-        for k in ("PL_JAC_LIN", "PL_JAC_CHEAP"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        G, bo = _handle(name, rname, dyn, N)
+    for tag, paths in (("new", ()), ("old", ("jac_dual_all", "jac_const_every"))):
+        G, bo = _handle(name, rname, dyn, N, debug_paths=paths)
         J1 = bo.eval_sqp_data()[1].copy()
         x2 = G["X"] + 1e-3 * np.random.default_rng(5).standard_normal(G["X"].shape)
         bo.set_x(x2)
@@ -64,19 +60,16 @@ def test_jacobian_rewrites_match_dual_columns(name, rname, dyn, N, monkeypatch):
 @pytest.mark.parametrize("name,rname,dyn,N", [("ip_b2g_rnea_n50", "b2g", "whole_body_rnea", 50),
                                                ("ip_b2g_acc_n50", "b2g", "whole_body_acc", 50),
                                                ("ip_go2_rnea_n20", "go2", "whole_body_rnea", 20)])
-def test_hessian_rewrites_match_full_pairs(name, rname, dyn, N, monkeypatch):
+def test_hessian_rewrites_match_full_pairs(name, rname, dyn, N):
     from pinoloco.ocp import BatchedOCP
     G = golden(f"{name}.npz")
     gait = str(G["gait"])
     H = {}
-    for tag, env in (("new", {}), ("old", {"PL_HESS_CHAIN": "0", "PL_HESS_LIN": "0"})):
-        for k in ("PL_HESS_CHAIN", "PL_HESS_LIN"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
+    for tag, paths in (("new", ()), ("old", ("hess_full_tree", "hess_dual_all"))):
         ib = bool(int(G["include_base"])) if "include_base" in G else True
         R = make_robot(rname, gait)
-        bo = BatchedOCP(R, dyn, N, batch=1, device=0, gait_type=gait, include_base=ib)
+        bo = BatchedOCP(R, dyn, N, batch=1, device=0, gait_type=gait, include_base=ib, debug_paths=paths)
+        assert bo.sizes()["debug_paths"] == sum(__import__("pinoloco")._lib.PATHS[p] for p in paths)
         bo.set_solver("fatrop")
         bo.set_ip_settings()
         bo.set_params(G["P"][:1])
@@ -90,13 +83,10 @@ def test_hessian_rewrites_match_full_pairs(name, rname, dyn, N, monkeypatch):
 
 @pytest.mark.parametrize("name,rname,dyn,N", [("b2_aba_n40", "b2", "whole_body_aba", 40),
                                                ("go2_cv_n20", "go2", "centroidal_vel", 20)])
-def test_factor_mfma_coupling_matches_list_route(name, rname, dyn, N, monkeypatch):
+def test_factor_mfma_coupling_matches_list_route(name, rname, dyn, N):
     res = {}
-    for tag, env in (("new", {}), ("old", {"PL_FCHAIN_MF": "0"})):
-        monkeypatch.delenv("PL_FCHAIN_MF", raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        G, bo = _handle(name, rname, dyn, N)
+    for tag, paths in (("new", ()), ("old", ("fchain_list",))):
+        G, bo = _handle(name, rname, dyn, N, debug_paths=paths)
         st = bo.solve()
         res[tag] = (bo.get_x().copy(), bo.get_step().copy(), st)
         bo.close()
@@ -104,6 +94,6 @@ def test_factor_mfma_coupling_matches_list_route(name, rname, dyn, N, monkeypatc
     xo, do, so = res["old"]
     for key in ("status", "admm_iters", "ls_accepted", "ls_branch", "ls_trials", "ls_alpha"):
         assert np.array_equal(sn[key], so[key]), key
-    # the reduced system is ill-conditioned (test_gpu.py header): each route is within 8.2e-10 of
-    # the oracle's step on these fixtures, so within 2e-9 of each other
+    # two fp64 routes through the reduced system: each within 1e-9 of the oracle's step on these
+    # fixtures (test_gpu.py header), so within 2e-9 of each other
     assert _rel(dn, do) <= 2e-9 and _rel(xn, xo) <= 2e-9

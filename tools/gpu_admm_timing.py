@@ -8,7 +8,6 @@ import time
 
 import numpy as np
 
-os.environ["PL_ADMM_TIMING"] = "1"
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "pino-locoman_amd"))
 from pinoloco import robots  # noqa: E402
@@ -20,7 +19,7 @@ N = 50
 R = robots.ROBOTS["b2g"]()
 R.set_gait_sequence("trot", 0.8)
 lay, P, X, XS, T0 = build_batch(R, "whole_body_rnea", N, B, 0)
-bo = BatchedOCP(R, "whole_body_rnea", N, batch=B, device=0)
+bo = BatchedOCP(R, "whole_body_rnea", N, batch=B, device=0, debug_paths=("admm_timing",))
 bo.set_params(P)
 bo.set_x(X)
 bo.init_solver()

@@ -7,7 +7,6 @@ import sys
 
 import numpy as np
 
-os.environ["PL_ADMM_TIMING"] = "1"
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "pino-locoman_amd"))
 from pinoloco import robots  # noqa: E402
@@ -18,7 +17,7 @@ rob, dyn, N, B = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
 R = robots.ROBOTS[rob]()
 R.set_gait_sequence("trot", 0.8)
 lay, P, X, XS, T0 = build_batch(R, dyn, N, B, 0)
-bo = BatchedOCP(R, dyn, N, batch=B, device=0)
+bo = BatchedOCP(R, dyn, N, batch=B, device=0, debug_paths=("admm_timing",))
 bo.set_admm_kernel("chain")
 bo.set_params(P)
 bo.set_x(X)
