@@ -38,6 +38,7 @@ def main():
     for k in range(K):
         bo.mpc_step(k)
     xs, X1, lam1 = bo.mpc_state()[:NP], bo.get_x()[:NP], bo.get_lam()[:NP]
+    st1 = {k: v[:NP].copy() for k, v in bo.ip_stats().items()}
     bo.mpc_step(K)
     st = bo.ip_stats()
     dev = {"status": st["status"][:NP].copy(), "iter": st["iter"][:NP].copy(), "alphas": st["alphas"][:NP].copy(),
@@ -67,7 +68,11 @@ def main():
     s2 = b2.ip_stats()
     xr, lr = b2.get_x(), b2.get_lam()
     same = (s2["status"] == dev["status"]) & (s2["iter"] == dev["iter"])
-    ex = max(float(np.abs(xr[b] - dev["x"][b]).max() / np.abs(dev["x"][b]).max()) for b in range(NP))
+    exs = [float(np.abs(xr[b] - dev["x"][b]).max() / np.abs(dev["x"][b]).max()) for b in range(NP)]
+    ex = max(exs)
+    for b in np.argsort(exs)[::-1][:6]:
+        print(f"  problem {b}: x {exs[b]:.1e}, loop status {dev['status'][b]} iter {dev['iter'][b]}, "
+              f"one solve {s2['status'][b]} iter {s2['iter'][b]}; step-1 status {st1['status'][b]} iter {st1['iter'][b]}")
     el = max(float(np.abs(lr[b] - dev["lam"][b]).max() / max(1.0, np.abs(dev["lam"][b]).max())) for b in range(NP))
     print(f"{dyn}: step {K} statuses {dict(zip(*np.unique(dev['status'], return_counts=True)))}; "
           f"one solve of the dumped inputs reproduces the loop: outcome {int(same.sum())}/{NP}, x {ex:.1e}, lam {el:.1e}")
