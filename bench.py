@@ -432,7 +432,7 @@ def main():
             ach = hf["flops_per_launch"] / (h_avg * 1e-3) / 1e12 if (hf and h_avg > 0) else None
             out["admm_roofline"] = out["roofline"]
             out["roofline"] = {"bound": "fp64_valu", "kernel": "k_lag_hess (+ k_lag_hess_lin for whole_body_rnea)",
-                               "mapping": mapping, "achieved": ach,
+                               "mapping": "pb", "achieved": ach,
                                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                                "frac": ach / FP64_PEAK_TFLOPS if ach is not None else None, "traffic": None,
                                "avg_launch_ms": h_avg, "launches": hp["launches"],

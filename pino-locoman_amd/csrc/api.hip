@@ -724,10 +724,6 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
     pl_set_error("the interior-point solver needs include_acc=True (ocp_whole_body_rnea.py:21)");
     return -1;
   }
-  if (solver == PL_SOLVER_IP && h->nw_max > 192) {  // k_ip_refine's per-wave node vectors (PL_IP_NWMAX)
-    pl_set_error("interior point: node block width %d exceeds 192", h->nw_max);
-    return -1;
-  }
   if (solver == PL_SOLVER_IP && !h->d.ipinfo) {
     const size_t Bm = (size_t)h->B * h->m;
     if (dalloc(o, &h->d.ip_s, Bm) || dalloc(o, &h->d.ip_lam, Bm) || dalloc(o, &h->d.ip_lam0, Bm) ||
@@ -1056,7 +1052,8 @@ extern "C" int pl_mpc_graph_info(const pl_ocp* o, long long* out) {
 
 extern "C" int pl_mpc_step(pl_ocp* o, int k) {
   REQUIRE_DEVICE(o);
-  if (o->h.profile && o->h.prof_n > 48) prof_collect(&o->h);
+  // the event slots: 64 ADMM launches, 16 Hessian launches (an interior-point step makes <= 10)
+  if (o->h.profile && (o->h.prof_n > 48 || o->h.prof_hn > 0)) prof_collect(&o->h);
   launch_mpc_prepare(&o->h, k);
   if (o->h.solver != PL_SOLVER_IP && !o->h.profile && !o->mpc_graph_off) {
     if (mpc_sqp_graph(o)) {

@@ -821,15 +821,19 @@ int build_factor_prog(pl_ocp* o) {
   // list route)
   const bool is_short = !h.fac_gc && cwlen_max <= 4;
   const int X16 = (X + 15) & ~15, NWS = ((h.nw_max + 15) & ~15) + 1;
-  const bool mf = !h.fac_gc && !is_short && !(h.debug_paths & PL_PATH_FCHAIN_LIST);
-  if (mf) ny = std::max(ny, (2 * X16 * NWS + 1) & ~1);
-  h.fchain_ny = ny;
-  h.fchain_short = is_short ? (cwlen_max <= 2 ? 3 : 1) : (mf ? 2 : 0);
   h.fchain_ncw = ((is_short ? std::max(ncw_max, 6 * X) : ncw_max) + 1) & ~1;
   h.fchain_nc = h.fac_gc ? nc_max : 0;
   h.fchain_nxc = h.fac_gc ? (nxc_max + 1) & ~1 : 0;
   const int ngc = h.fac_gc ? ((nc_max * nc_max + h.fchain_nxc + nc_max + 1) & ~1) : 0;
-  h.fchain_lds = (nS + ny + nE + h.fchain_ncw + 2 * X + 10 + ngc) * 8;  // + timing stamps
+  const auto chain_lds = [&](int ny_) { return (nS + ny_ + nE + h.fchain_ncw + 2 * X + 10 + ngc) * 8; };  // + stamps
+  bool mf = !h.fac_gc && !is_short && !(h.debug_paths & PL_PATH_FCHAIN_LIST);
+  // the MFMA route's dense Wc / Y buffers must fit beside S_i: a model too wide for them takes
+  // the list route (which needs only the halves of Y)
+  if (mf && chain_lds(std::max(ny, (2 * X16 * NWS + 1) & ~1)) > 160 * 1024) mf = false;
+  if (mf) ny = std::max(ny, (2 * X16 * NWS + 1) & ~1);
+  h.fchain_ny = ny;
+  h.fchain_short = is_short ? (cwlen_max <= 2 ? 3 : 1) : (mf ? 2 : 0);
+  h.fchain_lds = chain_lds(ny);
   if (h.fchain_lds > 160 * 1024) { pl_set_error("factor kernel: chain needs %d bytes of LDS", h.fchain_lds); return -1; }
   if (o->kasm.empty()) o->kasm.assign(NT, 0);
   if (o->kcpl.empty()) o->kcpl.assign(4, 0);

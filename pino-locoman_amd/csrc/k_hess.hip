@@ -139,7 +139,7 @@ __global__ __launch_bounds__(64) void k_lag_hess_lin(PlDev d, int B, int n, int 
   }
 
 void launch_lag_hess(PlOcpHandle* h) {
-  const bool prof = h->profile && h->prof_hn < 16;
+  const bool prof = h->profile && h->prof_hn < 16;  // pl_mpc_step collects the slots before every step
   if (prof) hipEventRecord(h->prof_hev[h->prof_hn][0], h->stream);
   if (h->hlin_len > 0)
     hipLaunchKernelGGL(k_lag_hess_lin, dim3(h->hlin_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,

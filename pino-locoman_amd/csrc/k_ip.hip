@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void k_ip_kkt(PlDev d, int N, int n, int m, in
 // block read in storage order (coalesced) and both halves of every entry added into a
 // wave-private LDS vector by ds_add_f64 (fixed lane / instruction order: deterministic);
 // the per-column gather of the block (strided, uncoalesced) took 2.1 ms per call at the
-// headline size.
+// headline size, and serves the blocks wider than the LDS vectors (PL_IP_NWMAX).
 #define PL_IP_NWMAX 192
 __device__ __forceinline__ void ip_lds_add(double* p, double v) {
   typedef __attribute__((address_space(3))) double* LPtr;
@@ -430,6 +430,17 @@ __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int N, int n, int m,
     for (int i = wv; i <= N; i += 4) {
       const PlNode nd = d.nodes[i];
       const int nw = nd.nw;
+      if (nw > PL_IP_NWMAX) {  // wider blocks than the LDS vectors: the per-column global gather
+        const double* Hi = i < N ? Hb + d.hoff[i] : nullptr;
+        for (int c = lane; c < nw; c += 64) {
+          double acc = 0.0;
+          if (Hi)
+            for (int r = 0; r < nw; ++r)
+              acc = fma(Hi[r >= c ? r * (r + 1) / 2 + c : c * (c + 1) / 2 + r], dx[nd.x_off + r], acc);
+          qs[nd.x_off + c] = acc;
+        }
+        continue;
+      }
       for (int c = lane; c < nw; c += 64) {
         y[c] = 0.0;
         xv[c] = dx[nd.x_off + c];

@@ -390,6 +390,7 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
   for (int k = 0; k < 6; ++k) Fw[k] = S(0.0);
   // arm frame world data (for the relative velocity)
   S arm_lin[3], arm_pos[3];
+  bool arm_skipped = false;  // the arm's chain skipped (only_ch): its velocity rows are zero
 
   for (int ch = 0; ch < M.nchains; ++ch) {
     const int first = M.chain_first[ch];
@@ -406,11 +407,13 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
         for (int e = 0; e < O.nfeet; ++e)
           if (O.feet[e].joint >= first && O.feet[e].joint < first + L)
             for (int c = 0; c < 3; ++c) out.foot_vel(e, c) = S(0.0);
-        if (O.arm.valid && O.arm.joint >= first && O.arm.joint < first + L)
+        if (O.arm.valid && O.arm.joint >= first && O.arm.joint < first + L) {
+          arm_skipped = true;
           for (int k = 0; k < 3; ++k) {
             arm_lin[k] = S(0.0);
             arm_pos[k] = S(0.0);
           }
+        }
       }
       continue;
     }
@@ -544,7 +547,11 @@ PL_HD void tree_pass(const PlModel& M, const PlOcpConst& O, const S* qb, const Q
     mattvec(R0, d, nl);
     for (int k = 0; k < 3; ++k) { out.tau[k] = f1[k] + fl[k]; out.tau[3 + k] = f1[3 + k] + nl[k]; }
   }
-  if (want_vel && O.arm.valid) {
+  if (want_vel && O.arm.valid && arm_skipped) {
+    // a pass confined to another chain: the arm rows have zero tangents, value and all (as the
+    // skipped chains' other outputs above), not the base-only remainder of the formula below
+    for (int k = 0; k < 3; ++k) out.arm_vel[k] = S(0.0);
+  } else if (want_vel && O.arm.valid) {
     // Dynamics.get_frame_velocity(relative_to_base=True) (dynamics/dynamics.py:86-113)
     // base frame on the root joint: LWA velocity = R0 (v + w x p_b), angular R0 w
     S pb[3] = {S(O.base.p[0]), S(O.base.p[1]), S(O.base.p[2])};
