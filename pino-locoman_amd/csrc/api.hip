@@ -736,7 +736,7 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
     // Lagrangian Hessian work list (k_hess.hip): the structurally non-zero column pairs
     // j <= k of every w_i block (hess_pattern, one probe per node type); node blocks packed
     // lower, the pairs not listed stay 0
-    std::vector<int2> hl, hlin;
+    std::vector<int2> hl, hlin, hvv, htr, hcone, htrf;
     std::vector<int> hoff;
     long long off = 0;
     const PlOcpConst& O = h->oc;
@@ -793,8 +793,20 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
       for (int k = 0; k < nw; ++k)
         for (int j = 0; j <= k; ++j) {
           if (lin && j < O.nv && k >= lin_lo && k < lin_hi) continue;
-          if (pat[type][(size_t)k * (k + 1) / 2 + j])
-            hl.push_back(make_int2(i | ((pair_chain(j, k) + 1) << 16), j | (k << 16)));
+          if (!pat[type][(size_t)k * (k + 1) / 2 + j]) continue;
+          // two state columns: the curvature of the tree-pass rows alone (k_lag_hess_tree), and for
+          // (dv, dv) the quadratic form of the RNEA bias term (k_lag_hess_vv)
+          const int ff = O.ndx + O.na;  // the foot forces
+          if (lin && j == k && j >= ff && j < ff + 3 * O.nfeet) {  // the friction cones (k_lag_hess_cone)
+            hcone.push_back(make_int2(i, j));
+            continue;
+          }
+          if (lin && j >= 3 && j < O.nv && k >= ff + 3 * O.nfeet && k < ff + 3 * O.nee) {  // (dq, f_ext)
+            htrf.push_back(make_int2(i | ((pair_chain(j, k) + 1) << 16), j | (k << 16)));
+            continue;
+          }
+          const bool st = lin && k < O.ndx;
+          (st ? (j >= O.nv ? hvv : htr) : hl).push_back(make_int2(i | ((pair_chain(j, k) + 1) << 16), j | (k << 16)));
         }
       if (lin)  // RNEA ignores the base position
         for (int k = 3; k < O.nv; ++k) hlin.push_back(make_int2(i, k | ((chains ? vidx_chain(k) + 1 : 0) << 16)));
@@ -810,14 +822,21 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
     }
     h->hl_len = (int)hl.size();
     h->hlin_len = (int)hlin.size();
+    h->hvv_len = (int)hvv.size();
+    h->htr_len = (int)htr.size();
+    h->hcone_len = (int)hcone.size();
+    h->htrf_len = (int)htrf.size();
     h->hl_stride = (off + 1) & ~1LL;
-    if (upload(o, &h->d.hlist, hl) || upload(o, &h->d.hoff, hoff) ||
+    if ((!hl.empty() && upload(o, &h->d.hlist, hl)) || upload(o, &h->d.hoff, hoff) ||
         dalloc(o, &h->d.Hlag, (size_t)h->B * h->hl_stride))
       return -2;
     if (lin) {
       PlModel m0 = h->model;
       for (int k = 0; k < 3; ++k) m0.gravity[k] = 0.0;
-      if (upload(o, &h->d.hlin, hlin)) return -2;
+      if (upload(o, &h->d.hlin, hlin) || (!hvv.empty() && upload(o, &h->d.hvv, hvv)) ||
+          (!htr.empty() && upload(o, &h->d.htr, htr)) || (!hcone.empty() && upload(o, &h->d.hcone, hcone)) ||
+          (!htrf.empty() && upload(o, &h->d.htrf, htrf)))
+        return -2;
       if (!h->d.model0 && (dalloc(o, &h->d.model0, 1) ||
                            hipMemcpy(h->d.model0, &m0, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess))
         return -2;

@@ -127,6 +127,369 @@ __global__ __launch_bounds__(64) void k_lag_hess_lin(PlDev d, int B, int n, int 
     for (int c = 0; c < 3; ++c) H[slot(f0 + 3 * e + c)] = -Dual(kin.foot_vel(e, c)).d;
 }
 
+// whole_body_rnea / whole_body_acc, the (dq, dq) and (dq, dv) pairs: of the node's rows only those that read
+// the tree pass's outputs are nonlinear in the state (the RNEA base and joint-torque rows, the
+// foot-velocity rows, the arm-velocity rows; every other row is linear in dx, rows.h node_rows), so
+// the pair's curvature is that of
+//     phi = lambda_tau^T tau(q, v, a, f) + sum_e mu_e . v_foot,e(q, v) + lambda_arm^T v_arm(q, v)
+// (mu_e: the foot-velocity rows' multipliers times their coefficients, world axes).  By virtual work
+// the first two terms are one forward sweep with no backward accumulation:
+//     lambda_tau^T tau = sum_bodies L_b . f_b,   L_b = X_b,parent L_parent + S_b lambda_b   (L_root = lambda_base)
+// with f_b the body's net wrench (I a + v x* I v - contact forces, body axes), and
+//     mu_e . v_foot,e = (v_lin + w x p_e) . (oR_b^T mu_e)
+// so a pair costs one hyper-dual sweep whose carried state is v, a, L and the world rotation of the
+// current body (k_lag_hess_pb's node_rows<HDual> carries the world-frame force prefix, the joint
+// subspaces and every row block as well, and spills).  The arm rows (relative to the base,
+// dynamics/dynamics.py:86-113) keep the velocity-only tree pass, for the pairs on the base or the
+// arm's chain.  d.htr packs pairs as d.hlist; one pair per wave, one problem per lane.
+namespace {
+template <class S> __device__ void crossd(const double* a, const S* b, S* o) {  // a x b, a constant
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+// out = R_j^T d for the revolute joint rotation R_j = jR Rot(axis, q_j) (rbd.h rev_rot), applied as
+// Rot^T (jR^T d) so that no hyper-dual 3x3 matrix is formed (jR constant; Rot a plane rotation for
+// the axis-aligned joints)
+template <class S, class C> __device__ void rot_t(const PlModel& M, int j, const C& s, const C& c, const S* d, S* out) {
+  S e[3];
+  pl::mattvec(M.jR[j], d, e);
+  switch (M.axis_kind[j]) {
+    case PL_AX_X:
+      out[0] = e[0]; out[1] = c * e[1] + s * e[2]; out[2] = c * e[2] - s * e[1];
+      break;
+    case PL_AX_Y:
+      out[0] = c * e[0] - s * e[2]; out[1] = e[1]; out[2] = s * e[0] + c * e[2];
+      break;
+    case PL_AX_Z:
+      out[0] = c * e[0] + s * e[1]; out[1] = c * e[1] - s * e[0]; out[2] = e[2];
+      break;
+    default: {  // Rodrigues I + s [a]x + (1 - c) [a]x^2, transposed
+      const double* a = M.axis[j];
+      const double K[9] = {0, -a[2], a[1], a[2], 0, -a[0], -a[1], a[0], 0};
+      const C oc = 1.0 - c;
+      for (int r = 0; r < 3; ++r) {
+        S t = e[r];
+        for (int q = 0; q < 3; ++q) {
+          const double kk = K[3 * q] * K[r] + K[3 * q + 1] * K[3 + r] + K[3 * q + 2] * K[6 + r];  // ([a]x^2)_qr
+          t += (s * K[3 * q + r] + oc * kk) * e[q];
+        }
+        out[r] = t;
+      }
+    }
+  }
+}
+// actInv of a motion through joint j: [R^T (m_lin - p x m_ang); R^T m_ang], p the joint placement
+template <class S, class C> __device__ void act_inv_j(const PlModel& M, int j, const C& s, const C& c, const S* m, S* out) {
+  S pxw[3];
+  crossd(M.jp[j], m + 3, pxw);
+  S d[3] = {m[0] - pxw[0], m[1] - pxw[1], m[2] - pxw[2]};
+  rot_t(M, j, s, c, d, out);
+  rot_t(M, j, s, c, m + 3, out + 3);
+}
+// f = I a + v x* I v  (body axes; inertia (m, c, Ic) constant)
+template <class S> __device__ void body_wrench(double m, const double* c, const double* Ic, const S* a, const S* v,
+                                               S* f) {
+  S t[3], h[6];
+  crossd(c, v + 3, t);
+  for (int k = 0; k < 3; ++k) h[k] = m * (v[k] - t[k]);
+  crossd(c, h, t);
+  for (int k = 0; k < 3; ++k) h[3 + k] = Ic[3 * k] * v[3] + Ic[3 * k + 1] * v[4] + Ic[3 * k + 2] * v[5] + t[k];
+  pl::motion_cross_force(v, h, f);
+  crossd(c, a + 3, t);
+  S fl[3];
+  for (int k = 0; k < 3; ++k) fl[k] = m * (a[k] - t[k]);
+  crossd(c, fl, t);
+  for (int k = 0; k < 3; ++k) {
+    f[k] += fl[k];
+    f[3 + k] += Ic[3 * k] * a[3] + Ic[3 * k + 1] * a[4] + Ic[3 * k + 2] * a[5] + t[k];
+  }
+}
+__device__ int block_row(const PlOcpConst& O, int type, int kind, int arg) {  // first row of a block, -1: none
+  int r = 0;
+  for (int bi = 0; bi < O.nblk[type]; ++bi) {
+    const PlRowBlock B = O.blk[type][bi];
+    if (B.kind == kind && (arg < 0 || B.arg == arg)) return r;
+    r += B.count;
+  }
+  return -1;
+}
+}  // namespace
+
+// The sweep's view of one node: the root pose, the state accessors and the world-axis vectors it
+// rotates into a body's axes (oR_b^T x, by a walk from the root: R0^T, then R_j^T joint by joint)
+struct TreeSweep {
+  const PlModel& M;
+  const HDual* qb;
+  const pl::RevQ<HDual, VecIn<HDual>>& qrev;
+  template <class X> __device__ void to_body(int first, int kk, const X* xw, HDual* out) const {
+    HDual R0[9];
+    pl::quat_to_R(qb + 3, R0);
+    pl::mattvec(R0, xw, out);
+    for (int k2 = 0; k2 <= kk; ++k2) {
+      const int j2 = first + k2;
+      HDual s2, c2, t[3];
+      sincos_s(qrev(M.idx_q[j2]), &s2, &c2);
+      rot_t(M, j2, s2, c2, out, t);
+      for (int q = 0; q < 3; ++q) out[q] = t[q];
+    }
+  }
+};
+
+// contact forces on body j (f_b -= [fl; p x fl], fl = oR^T f_world) and its feet's velocity rows
+// (phi += (v_lin + w x p) . oR^T mu); first / kk: body j's place in its chain (first = -1: the root)
+// (f: the contact forces, plain or seeded -- k_lag_hess_tree<true>)
+template <class F3>
+__device__ void body_frames(const PlOcpConst& O, const TreeSweep& T, int first, int kk, int j, int type, int node,
+                            const HDual* vj, const F3& f, const double* lam, const double* p, HDual* fb, HDual& phi) {
+  for (int e = 0; e < O.nee; ++e) {
+    const PlFrameRef& F = (e < O.nfeet) ? O.feet[e] : O.ext;
+    if (F.joint != j) continue;
+    HDual fl[3], t[3];
+    const decltype(f(0, 0)) fw[3] = {f(e, 0), f(e, 1), f(e, 2)};
+    T.to_body(first, kk, fw, fl);
+    crossd(F.p, fl, t);
+    for (int k = 0; k < 3; ++k) { fb[k] -= fl[k]; fb[3 + k] -= t[k]; }
+    if (e >= O.nfeet) continue;
+    const int rxy = block_row(O, type, PL_RB_FVXY, e), rz = block_row(O, type, PL_RB_FVZ, e);
+    if (rxy < 0 && rz < 0) continue;
+    const double c = p[O.P.contact + 4 * node + e];
+    const double mu[3] = {rxy >= 0 ? c * lam[rxy] : 0.0, rxy >= 0 ? c * lam[rxy + 1] : 0.0, rz >= 0 ? lam[rz] : 0.0};
+    HDual g[3], wxp[3];
+    T.to_body(first, kk, mu, g);
+    crossd(F.p, vj + 3, wxp);  // p x w = -(w x p)
+    for (int k = 0; k < 3; ++k) phi += (vj[k] - wxp[k]) * g[k];
+  }
+}
+
+namespace {
+// The root pose for the state pairs: nothing downstream reads the base position (translation
+// invariance: it is set to 0), and the orientation is q0 (x) exp(w / 2), w = dq_3..5, whose
+// rotation matrix is R(q0) Exp(w) -- what integrate_ff's SE3 exponential, R -> quaternion and
+// renormalisation give (the last two are the identity on rotations: their derivatives cancel
+// analytically), without carrying them in hyper-duals.  Below the exp6 series threshold
+// (rbd.h PL_TAYLOR_PREC3) sin(t/2)/t and cos(t/2) are their series in t^2 through t^4.
+__device__ void base_pose(const double* xi, const VecIn<HDual>& dx, HDual* qb) {
+  const HDual w[3] = {dx[3], dx[4], dx[5]};
+  const HDual t2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  HDual f, g;
+  if (val(t2) < PL_TAYLOR_PREC3 * PL_TAYLOR_PREC3) {
+    f = 0.5 - t2 * (1.0 / 48.0) + (t2 * t2) * (1.0 / 3840.0);
+    g = 1.0 - t2 * 0.125 + (t2 * t2) * (1.0 / 384.0);
+  } else {
+    const HDual th = sqrt_s(t2);
+    HDual sh, ch;
+    sincos_s(th * 0.5, &sh, &ch);
+    f = sh / th;
+    g = ch;
+  }
+  const HDual u[3] = {f * w[0], f * w[1], f * w[2]};  // exp(w / 2) = [u; g]
+  const double* q0 = xi + 3;                           // [x y z w]
+  HDual cr[3];
+  crossd(q0, u, cr);
+  for (int k = 0; k < 3; ++k) qb[3 + k] = q0[3] * u[k] + q0[k] * g + cr[k];
+  qb[6] = q0[3] * g - (q0[0] * u[0] + q0[1] * u[1] + q0[2] * u[2]);
+  for (int k = 0; k < 3; ++k) qb[k] = HDual(0.0);
+}
+}  // namespace
+
+// whole_body_rnea / whole_body_acc, the (dv, dv) block: the only rows with curvature in v are the RNEA rows,
+// and at a = 0, f = 0 without gravity the RNEA torque is the bias term C(q, v) v, a quadratic form
+// in v.  With Q(v) = lambda_tau^T C(q, v) v the block is d^2 L / dv_j dv_k = d^2 Q / dv_j dv_k, and
+// because Q is quadratic
+//     Q(e_j + eps e_k) = Q(e_j) + eps d^2 Q / dv_j dv_k + eps^2 Q(e_k)
+// so one dual sweep at v = e_j with tangent e_k gives the entry exactly (j = k: v = (1 + eps) e_j,
+// the tangent is 2 Q(e_j)), with no cancellation.  Q by virtual work as in k_lag_hess_tree below:
+// q is a constant here, so the joint rotations and the virtual velocities L_b are plain doubles and
+// only v, a and the body wrenches carry a tangent.  d.hvv packs pairs as d.hlist (chain
+// confinement included); one pair per wave, one problem per lane.
+__global__ __launch_bounds__(64) void k_lag_hess_vv(PlDev d, int B, int n, int m, int np, long long hl_stride,
+                                                    int3 rb_base, int3 rb_tau) {
+  const int b = blockIdx.y * 64 + threadIdx.x;
+  if (b >= B || !d.ipinfo[b].active) return;
+  const PlOcpConst& O = *d.oc;
+  const PlModel& M = *d.model;
+  const int2 w = d.hvv[blockIdx.x];
+  const int wx = __builtin_amdgcn_readfirstlane(w.x);
+  const int i = wx & 0xffff, only_ch = (wx >> 16) - 1;
+  const int jk = __builtin_amdgcn_readfirstlane(w.y);
+  const int j = jk & 0xffff, k = jk >> 16;  // w_i columns nv + (velocity index)
+  const PlNode nd = d.nodes[i];
+  const double* x = d.x + (size_t)b * n + nd.x_off;
+  const double* p = d.p + (size_t)b * np;
+  const double* lam = d.ip_lam + (size_t)b * m + nd.row_off;
+  const int type = pl::node_type(O, i);
+  const int rbb = type == 0 ? rb_base.x : (type == 1 ? rb_base.y : rb_base.z);
+  const int rbt = type == 0 ? rb_tau.x : (type == 1 ? rb_tau.y : rb_tau.z);
+  const double* xi = p + O.P.x_init;
+  const int nv = O.nv, vj_ = j - nv, vk_ = k - nv;
+  const auto vin = [&](int q) { return Dual(q == vj_ ? 1.0 : 0.0, q == vk_ ? 1.0 : 0.0); };
+  Dual phi(0.0, 0.0);
+  if (only_ch < 0 && rbb >= 0) {  // the root body: f = v x* I v
+    Dual v1[6], a1[6], f1[6];
+    for (int c = 0; c < 6; ++c) { v1[c] = vin(c); a1[c] = Dual(0.0, 0.0); }
+    body_wrench(M.mass[1], M.lever[1], M.Ic[1], a1, v1, f1);
+    for (int c = 0; c < 6; ++c) phi += lam[rbb + c] * f1[c];
+  }
+  for (int ch = 0; ch < M.nchains; ++ch) {
+    if (only_ch >= 0 && ch != only_ch) continue;
+    const int first = M.chain_first[ch], L = M.chain_len[ch];
+    Dual pv[6], pa[6];
+    double pL[6];
+    for (int c = 0; c < 6; ++c) { pv[c] = vin(c); pa[c] = Dual(0.0, 0.0); pL[c] = rbb >= 0 ? lam[rbb + c] : 0.0; }
+    for (int kk = 0; kk < L; ++kk) {
+      const int jt = first + kk;
+      double s, c;
+      sincos(xi[M.idx_q[jt]] + x[M.idx_q[jt] - 1], &s, &c);  // q_j = x_init + dq (rbd.h RevQ)
+      const double* ax = M.axis[jt];
+      const int iv = M.idx_v[jt];
+      const Dual qd = vin(iv);
+      Dual vj[6], aj[6], t[3];
+      act_inv_j(M, jt, s, c, pv, vj);
+      for (int q = 0; q < 3; ++q) vj[3 + q] += ax[q] * qd;
+      act_inv_j(M, jt, s, c, pa, aj);
+      crossd(ax, vj, t);
+      for (int q = 0; q < 3; ++q) aj[q] -= t[q] * qd;
+      crossd(ax, vj + 3, t);
+      for (int q = 0; q < 3; ++q) aj[3 + q] -= t[q] * qd;
+      double Lj[6];
+      act_inv_j(M, jt, s, c, pL, Lj);
+      const double lj = rbt >= 0 ? lam[rbt + iv - 6] : 0.0;
+      for (int q = 0; q < 3; ++q) Lj[3 + q] += ax[q] * lj;
+      Dual fj[6];
+      body_wrench(M.mass[jt], M.lever[jt], M.Ic[jt], aj, vj, fj);
+      for (int q = 0; q < 6; ++q) { phi += Lj[q] * fj[q]; pv[q] = vj[q]; pa[q] = aj[q]; pL[q] = Lj[q]; }
+    }
+  }
+  d.Hlag[(size_t)b * hl_stride + d.hoff[i] + k * (k + 1) / 2 + j] = phi.d;
+}
+
+// SF: the (dq, f_ext) pairs (an external force frame, O.ext: the RNEA rows are linear in its force but
+// it moves with q, so those pairs are this sweep with the force seeded); d.htrf
+template <bool SF>
+__global__ __launch_bounds__(64) void k_lag_hess_tree(PlDev d, int B, int n, int m, int np, long long hl_stride) {
+  const int b = blockIdx.y * 64 + threadIdx.x;
+  if (b >= B || !d.ipinfo[b].active) return;
+  const PlOcpConst& O = *d.oc;
+  const PlModel& M = *d.model;
+  const int2 w = (SF ? d.htrf : d.htr)[blockIdx.x];
+  const int wx = __builtin_amdgcn_readfirstlane(w.x);
+  const int i = wx & 0xffff, only_ch = (wx >> 16) - 1;
+  const int jk = __builtin_amdgcn_readfirstlane(w.y);
+  const int j = jk & 0xffff, k = jk >> 16;
+  const PlNode nd = d.nodes[i];
+  const double* x = d.x + (size_t)b * n + nd.x_off;
+  const double* p = d.p + (size_t)b * np;
+  const double* lam = d.ip_lam + (size_t)b * m + nd.row_off;
+  double* H = d.Hlag + (size_t)b * hl_stride + d.hoff[i] + k * (k + 1) / 2 + j;
+  if (j < 3) {  // the RNEA and the frame velocities do not read the base position (rows.h seed_pos)
+    *H = 0.0;
+    return;
+  }
+  const double* xi = p + O.P.x_init;
+  const int nv = O.nv, ndx = O.ndx, type = pl::node_type(O, i);
+  const VecIn<HDual> dx{x, nullptr, 0.0, j, k};
+  HDual qb[7];
+  base_pose(xi, dx, qb);
+  const pl::RevQ<HDual, VecIn<HDual>> qrev{xi, dx};
+  const pl::VelAcc<HDual, VecIn<HDual>> vel{xi + O.nq, pl::sub_in(dx, nv)};
+  const double* a = x + ndx;           // u = [a | f | tau_j]: constants for a state pair
+  const double* fx = x + ndx + O.na;
+  const int fk = k - ndx - O.na;  // SF: the seeded force component
+  const auto f = [&](int e, int c) {
+    if constexpr (SF) return HDual(fx[3 * e + c], 0.0, 3 * e + c == fk ? 1.0 : 0.0, 0.0);
+    else return fx[3 * e + c];
+  };
+  const int rb = block_row(O, type, PL_RB_RNEA_BASE, -1), rt = block_row(O, type, PL_RB_TAU_EQ, -1);
+  HDual phi(0.0);
+  // the sweep's carried state is v, a and L of the current body; the root's pose and motion are
+  // recomputed per chain from q_b, and a body's world rotation (its frames) by a walk from the root
+  const double mg[3] = {-M.gravity[0], -M.gravity[1], -M.gravity[2]};
+  const TreeSweep T{M, qb, qrev};
+  if (only_ch < 0 && rb >= 0) {  // the root body's own term (base coordinates only)
+    HDual v1[6], a1[6], f1[6];
+    for (int c = 0; c < 6; ++c) v1[c] = vel[c];
+    T.to_body(0, -1, mg, a1);
+    for (int c = 0; c < 3; ++c) { a1[c] = a1[c] + a[c]; a1[3 + c] = HDual(a[3 + c]); }
+    body_wrench(M.mass[1], M.lever[1], M.Ic[1], a1, v1, f1);
+    body_frames(O, T, 0, -1, 1, type, i, v1, f, lam, p, f1, phi);
+    for (int c = 0; c < 6; ++c) phi += lam[rb + c] * f1[c];
+  }
+  for (int ch = 0; ch < M.nchains; ++ch) {
+    if (only_ch >= 0 && ch != only_ch) continue;
+    const int first = M.chain_first[ch], L = M.chain_len[ch];
+    HDual pv[6], pa[6], pL[6];
+    T.to_body(0, -1, mg, pa);
+    for (int c = 0; c < 3; ++c) { pa[c] = pa[c] + a[c]; pa[3 + c] = HDual(a[3 + c]); }
+    for (int c = 0; c < 6; ++c) { pv[c] = vel[c]; pL[c] = HDual(rb >= 0 ? lam[rb + c] : 0.0); }
+    for (int kk = 0; kk < L; ++kk) {
+      const int jt = first + kk;
+      HDual s, c;
+      sincos_s(qrev(M.idx_q[jt]), &s, &c);
+      const double* ax = M.axis[jt];
+      const int iv = M.idx_v[jt];
+      const HDual qd = vel[iv];
+      HDual vj[6], aj[6], t[3];
+      act_inv_j(M, jt, s, c, pv, vj);
+      for (int q = 0; q < 3; ++q) vj[3 + q] += ax[q] * qd;
+      act_inv_j(M, jt, s, c, pa, aj);
+      // + S qdd + v x vJ, vJ = [0; ax qd]:  [v_lin x ax; w x ax] qd
+      crossd(ax, vj, t);
+      for (int q = 0; q < 3; ++q) aj[q] -= t[q] * qd;
+      crossd(ax, vj + 3, t);
+      for (int q = 0; q < 3; ++q) aj[3 + q] += ax[q] * a[iv] - t[q] * qd;
+      for (int q = 0; q < 6; ++q) { pv[q] = vj[q]; pa[q] = aj[q]; }
+      act_inv_j(M, jt, s, c, pL, aj);  // L_j (aj: scratch)
+      const double lj = rt >= 0 ? lam[rt + iv - 6] : 0.0;
+      for (int q = 0; q < 3; ++q) aj[3 + q] += ax[q] * lj;
+      for (int q = 0; q < 6; ++q) pL[q] = aj[q];
+      HDual fj[6];
+      body_wrench(M.mass[jt], M.lever[jt], M.Ic[jt], pa, pv, fj);
+      body_frames(O, T, first, kk, jt, type, i, pv, f, lam, p, fj, phi);
+      for (int q = 0; q < 6; ++q) phi += pL[q] * fj[q];
+    }
+  }
+  double acc = phi.c;
+  // ---- the arm rows: the velocity-only tree pass on the arm's chain (pairs on the base or that chain)
+  const int ra = O.arm.valid ? block_row(O, type, PL_RB_ARM, -1) : -1;
+  if (ra >= 0) {
+    int arm_ch = -1;
+    for (int ch = 0; ch < M.nchains; ++ch)
+      if (O.arm.joint >= M.chain_first[ch] && O.arm.joint < M.chain_first[ch] + M.chain_len[ch]) arm_ch = ch;
+    if (only_ch < 0 || only_ch == arm_ch) {
+      HDual kst[PL_KIN_STORE];
+      pl::NodeKin<HDual> kin;
+      kin.store = kst;
+      kin.stride = 1;
+      const VecIn<HDual> u{x + ndx, nullptr, 0.0, j - ndx, k - ndx};
+      pl::tree_pass<HDual>(M, O, qb, qrev, vel, u, pl::sub_in(u, O.na), false, true, kin, nullptr, std::false_type{},
+                           arm_ch);
+      for (int q = 0; q < 3; ++q) acc = fma(lam[ra + q], kin.arm_vel[q].c, acc);
+    }
+  }
+  *H = acc;
+}
+
+// whole_body_rnea / whole_body_acc, the (f, f) pairs: of the rows only the friction cones
+// c (f_x^2 + f_y^2) - c mu^2 f_z^2 (rows.h PL_RB_CONE) are nonlinear in a foot force, so the
+// block is diagonal with 2 c lambda and -2 c mu^2 lambda.  d.hcone: (node, w_i column); one entry
+// per lane.
+__global__ __launch_bounds__(64) void k_lag_hess_cone(PlDev d, int B, int m, int np, long long hl_stride, int len) {
+  const int q = blockIdx.x * 64 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (q >= len || !d.ipinfo[b].active) return;
+  const PlOcpConst& O = *d.oc;
+  const int2 w = d.hcone[q];
+  const int i = w.x, col = w.y;
+  const int e = (col - O.ndx - O.na) / 3, comp = (col - O.ndx - O.na) % 3;
+  const int type = pl::node_type(O, i);
+  const int r = block_row(O, type, PL_RB_CONE, e);
+  const double c = d.p[(size_t)b * np + O.P.contact + 4 * i + e];
+  const double h = comp < 2 ? c * 2.0 : -(c * O.mu * O.mu) * 2.0;
+  const double lam = r >= 0 ? d.ip_lam[(size_t)b * m + d.nodes[i].row_off + r] : 0.0;
+  d.Hlag[(size_t)b * hl_stride + d.hoff[i] + col * (col + 1) / 2 + col] = lam * h;
+}
+
 #define PL_DISPATCH_DYN(dyn, KERNEL, ...)                                            \
   switch (dyn) {                                                                      \
     case PL_DYN_RNEA: hipLaunchKernelGGL(KERNEL<PL_DYN_RNEA>, __VA_ARGS__); break;   \
@@ -145,7 +508,21 @@ void launch_lag_hess(PlOcpHandle* h) {
     hipLaunchKernelGGL(k_lag_hess_lin, dim3(h->hlin_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,
                        h->m, h->np, h->hl_stride, make_int3(h->hl_rb_base[0], h->hl_rb_base[1], h->hl_rb_base[2]),
                        make_int3(h->hl_rb_tau[0], h->hl_rb_tau[1], h->hl_rb_tau[2]));
-  PL_DISPATCH_DYN(h->oc.dyn, k_lag_hess_pb, dim3(h->hl_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->N,
+  if (h->hvv_len > 0)
+    hipLaunchKernelGGL(k_lag_hess_vv, dim3(h->hvv_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,
+                       h->m, h->np, h->hl_stride, make_int3(h->hl_rb_base[0], h->hl_rb_base[1], h->hl_rb_base[2]),
+                       make_int3(h->hl_rb_tau[0], h->hl_rb_tau[1], h->hl_rb_tau[2]));
+  if (h->htr_len > 0)
+    hipLaunchKernelGGL(k_lag_hess_tree<false>, dim3(h->htr_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B,
+                       h->n, h->m, h->np, h->hl_stride);
+  if (h->htrf_len > 0)
+    hipLaunchKernelGGL(k_lag_hess_tree<true>, dim3(h->htrf_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B,
+                       h->n, h->m, h->np, h->hl_stride);
+  if (h->hcone_len > 0)
+    hipLaunchKernelGGL(k_lag_hess_cone, dim3((h->hcone_len + 63) / 64, h->B), dim3(64), 0, h->stream, h->d, h->B, h->m,
+                       h->np, h->hl_stride, h->hcone_len);
+  if (h->hl_len > 0)
+    PL_DISPATCH_DYN(h->oc.dyn, k_lag_hess_pb, dim3(h->hl_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->N,
                   h->n, h->m, h->np, h->hl_stride);
   if (prof) {
     hipEventRecord(h->prof_hev[h->prof_hn][1], h->stream);

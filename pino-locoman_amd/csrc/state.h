@@ -225,6 +225,10 @@ struct PlDev {
   double* ip_lam0;   // lam_g warm start (opti.set_initial(opti.lam_g, lam_g), ocp_whole_body_rnea.py:234-235)
   // exact Lagrangian Hessian (k_hess.hip) and its inertia correction (k_ip.hip)
   int2* hlist;       // (node, j | k << 16) column pairs of the w_i blocks
+  int2* hcone;       // whole_body_rnea / whole_body_acc: (node, foot-force column) of the cone curvature (k_lag_hess_cone)
+  int2* htrf;        // the (dq, external force) pairs (k_lag_hess_tree<true>)
+  int2* htr;         // whole_body_rnea / whole_body_acc: the (dq, dq) and (dq, dv) pairs (k_lag_hess_tree)
+  int2* hvv;         // whole_body_rnea / whole_body_acc: the (dv, dv) pairs, packed as hlist (k_lag_hess_vv)
   int2* hlin;        // whole_body_rnea: (node, dq column k) of the linear-column Hessian blocks (k_lag_hess_lin)
   PlModel* model0;   // the model with zero gravity (M(q) lambda by an RNEA pass at v = 0)
   int* hoff;         // packed-lower offset of node i's block
@@ -271,6 +275,10 @@ struct PlOcpHandle {
   int ip_lam_warm;                  // 1: the next interior-point solve starts from lam = ip_lam0
   int ip_hess;                      // interior point: PL_IP_HESS_EXACT (Lagrangian) or PL_IP_HESS_GN
   int hl_len;                       // Lagrangian Hessian work list (k_lag_hess)
+  int hcone_len;                    // k_lag_hess_cone work list
+  int htrf_len;                     // k_lag_hess_tree<true> work list
+  int htr_len;                      // k_lag_hess_tree work list
+  int hvv_len;                      // k_lag_hess_vv work list
   int hlin_len;                     // k_lag_hess_lin work list (0: every pair by hyper-dual passes)
   int hl_rb_base[3], hl_rb_tau[3];  // per node type: first row of the RNEA base / joint-torque rows (-1: none)
   long long hl_stride;              // doubles per problem of d.Hlag
