@@ -820,6 +820,22 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
         r += O.blk[t][bi].count;
       }
     }
+    // the written entries of a node block per node type (k_ip_refine's H_i dx): the pattern and,
+    // with the linear-column identity, the whole (dq_k, a | f_feet) rows k_lag_hess_lin stores
+    std::vector<int> hnz;
+    for (int t = 0; t < 3; ++t) {
+      h->hnz_off[t] = (int)hnz.size();
+      int nw = -1;
+      for (int i = 0; i < h->N; ++i)
+        if (pl::node_type(O, i) == t) { nw = o->nodes[i].nw; break; }
+      if (nw < 0 || pat[t].empty()) continue;
+      for (int k = 0; k < nw; ++k)
+        for (int j = 0; j <= k; ++j)
+          if (pat[t][(size_t)k * (k + 1) / 2 + j] || (lin && j >= 3 && j < O.nv && k >= lin_lo && k < lin_hi))
+            hnz.push_back(k | (j << 16));
+    }
+    h->hnz_off[3] = (int)hnz.size();
+    if (!hnz.empty() && upload(o, &h->d.hnz, hnz)) return -2;
     h->hl_len = (int)hl.size();
     h->hlin_len = (int)hlin.size();
     h->hvv_len = (int)hvv.size();

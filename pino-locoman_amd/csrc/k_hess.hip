@@ -222,6 +222,23 @@ struct TreeSweep {
   const PlModel& M;
   const HDual* qb;
   const pl::RevQ<HDual, VecIn<HDual>>& qrev;
+  // two vectors in one walk (a foot's force and its velocity rows' multipliers)
+  template <class X> __device__ void to_body2(int first, int kk, const X* xw, const double* yw, HDual* ox,
+                                              HDual* oy) const {
+    HDual R0[9];
+    pl::quat_to_R(qb + 3, R0);
+    pl::mattvec(R0, xw, ox);
+    pl::mattvec(R0, yw, oy);
+    for (int k2 = 0; k2 <= kk; ++k2) {
+      const int j2 = first + k2;
+      HDual s2, c2, t[3];
+      sincos_s(qrev(M.idx_q[j2]), &s2, &c2);
+      rot_t(M, j2, s2, c2, ox, t);
+      for (int q = 0; q < 3; ++q) ox[q] = t[q];
+      rot_t(M, j2, s2, c2, oy, t);
+      for (int q = 0; q < 3; ++q) oy[q] = t[q];
+    }
+  }
   template <class X> __device__ void to_body(int first, int kk, const X* xw, HDual* out) const {
     HDual R0[9];
     pl::quat_to_R(qb + 3, R0);
@@ -247,18 +264,21 @@ __device__ void body_frames(const PlOcpConst& O, const TreeSweep& T, int first, 
     if (F.joint != j) continue;
     HDual fl[3], t[3];
     const decltype(f(0, 0)) fw[3] = {f(e, 0), f(e, 1), f(e, 2)};
-    T.to_body(first, kk, fw, fl);
+    const int rxy = e < O.nfeet ? block_row(O, type, PL_RB_FVXY, e) : -1;
+    const int rz = e < O.nfeet ? block_row(O, type, PL_RB_FVZ, e) : -1;
+    if (rxy >= 0 || rz >= 0) {
+      const double c = p[O.P.contact + 4 * node + e];
+      const double mu[3] = {rxy >= 0 ? c * lam[rxy] : 0.0, rxy >= 0 ? c * lam[rxy + 1] : 0.0,
+                            rz >= 0 ? lam[rz] : 0.0};
+      HDual g[3], wxp[3];
+      T.to_body2(first, kk, fw, mu, fl, g);
+      crossd(F.p, vj + 3, wxp);  // p x w = -(w x p)
+      for (int k = 0; k < 3; ++k) phi += (vj[k] - wxp[k]) * g[k];
+    } else {
+      T.to_body(first, kk, fw, fl);
+    }
     crossd(F.p, fl, t);
     for (int k = 0; k < 3; ++k) { fb[k] -= fl[k]; fb[3 + k] -= t[k]; }
-    if (e >= O.nfeet) continue;
-    const int rxy = block_row(O, type, PL_RB_FVXY, e), rz = block_row(O, type, PL_RB_FVZ, e);
-    if (rxy < 0 && rz < 0) continue;
-    const double c = p[O.P.contact + 4 * node + e];
-    const double mu[3] = {rxy >= 0 ? c * lam[rxy] : 0.0, rxy >= 0 ? c * lam[rxy + 1] : 0.0, rz >= 0 ? lam[rz] : 0.0};
-    HDual g[3], wxp[3];
-    T.to_body(first, kk, mu, g);
-    crossd(F.p, vj + 3, wxp);  // p x w = -(w x p)
-    for (int k = 0; k < 3; ++k) phi += (vj[k] - wxp[k]) * g[k];
   }
 }
 

@@ -379,9 +379,11 @@ __global__ __launch_bounds__(256) void k_ip_kkt(PlDev d, int N, int n, int m, in
 // W_E = 1 / delta_c = 1e4 one block-inverse solve agrees with the oracle's sparse LU to
 // ~1e-12 and the refinement keeps the step at that level as the multipliers grow
 // (at W_E = 1e6 the explicit inverses lose ~5 digits and the refinement diverges).
-// H_i dx of a node block (r04): one wave per node (nodes w, w + 4, ...), the packed-lower
-// block read in storage order (coalesced) and both halves of every entry added into a
-// wave-private LDS vector by ds_add_f64 (fixed lane / instruction order: deterministic);
+// H_i dx of a node block (r04): one wave per node (nodes w, w + 4, ...), the block's written
+// entries (d.hnz, r05: a B2G node writes ~1/5 of its packed-lower block; until r05 every entry
+// was read and its row recovered by a square root) in storage order and both halves of every
+// entry added into a wave-private LDS vector by ds_add_f64 (fixed lane / instruction order:
+// deterministic);
 // the per-column gather of the block (strided, uncoalesced) took 2.1 ms per call at the
 // headline size, and serves the blocks wider than the LDS vectors (PL_IP_NWMAX).
 #define PL_IP_NWMAX 192
@@ -395,7 +397,7 @@ __device__ __forceinline__ void ip_wsync() {
 }
 
 __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int N, int n, int m, int nnz, double delta_w, int hlag,
-                                                   long long hl_stride) {
+                                                   long long hl_stride, int4 hnz_off, int tau_nodes) {
   const int b = blockIdx.x;
   if (!d.ipinfo[b].active) return;
   const double* A = d.Araw + (size_t)b * nnz;
@@ -446,15 +448,15 @@ __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int N, int n, int m,
         xv[c] = dx[nd.x_off + c];
       }
       ip_wsync();
-      if (i < N) {
+      if (i < N) {  // the block's written entries only (d.hnz, the node type's list)
         const double* Hi = Hb + d.hoff[i];
-        const int ne = nw * (nw + 1) / 2;
-        for (int e = lane; e < ne; e += 64) {
-          int r = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-          while (r * (r + 1) / 2 > e) --r;
-          while ((r + 1) * (r + 2) / 2 <= e) ++r;
-          const int c = e - r * (r + 1) / 2;
-          const double h = Hi[e];
+        const int t = i == 0 ? 0 : (i < tau_nodes ? 1 : 2);  // rows.h node_type
+        const int q0 = t == 0 ? hnz_off.x : (t == 1 ? hnz_off.y : hnz_off.z);
+        const int q1 = t == 0 ? hnz_off.y : (t == 1 ? hnz_off.z : hnz_off.w);
+        for (int q = q0 + lane; q < q1; q += 64) {
+          const int rc = d.hnz[q];
+          const int r = rc & 0xffff, c = rc >> 16;
+          const double h = Hi[r * (r + 1) / 2 + c];
           ip_lds_add(y + r, h * xv[c]);
           if (c != r) ip_lds_add(y + c, h * xv[r]);
         }
@@ -783,7 +785,8 @@ static void ip_factor(PlOcpHandle* h) {
 
 static void ip_refine(PlOcpHandle* h, const PlIpSettings& st) {
   hipLaunchKernelGGL(k_ip_refine, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz, st.delta_w,
-                     h->ip_hess == PL_IP_HESS_EXACT ? 1 : 0, h->hl_stride);
+                     h->ip_hess == PL_IP_HESS_EXACT ? 1 : 0, h->hl_stride,
+                     make_int4(h->hnz_off[0], h->hnz_off[1], h->hnz_off[2], h->hnz_off[3]), h->oc.tau_nodes);
 }
 
 // One interior-point solve of every problem from d.x (the warm start), enqueued on the

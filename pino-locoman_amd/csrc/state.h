@@ -224,6 +224,7 @@ struct PlDev {
   double* ip_lam;    // constraint multipliers (lam_g)
   double* ip_lam0;   // lam_g warm start (opti.set_initial(opti.lam_g, lam_g), ocp_whole_body_rnea.py:234-235)
   // exact Lagrangian Hessian (k_hess.hip) and its inertia correction (k_ip.hip)
+  int* hnz;          // per node type: the written entries (row | col << 16) of a Lagrangian Hessian block
   int2* hlist;       // (node, j | k << 16) column pairs of the w_i blocks
   int2* hcone;       // whole_body_rnea / whole_body_acc: (node, foot-force column) of the cone curvature (k_lag_hess_cone)
   int2* htrf;        // the (dq, external force) pairs (k_lag_hess_tree<true>)
@@ -275,6 +276,7 @@ struct PlOcpHandle {
   int ip_lam_warm;                  // 1: the next interior-point solve starts from lam = ip_lam0
   int ip_hess;                      // interior point: PL_IP_HESS_EXACT (Lagrangian) or PL_IP_HESS_GN
   int hl_len;                       // Lagrangian Hessian work list (k_lag_hess)
+  int hnz_off[4];                   // d.hnz per node type: [hnz_off[t], hnz_off[t + 1])
   int hcone_len;                    // k_lag_hess_cone work list
   int htrf_len;                     // k_lag_hess_tree<true> work list
   int htr_len;                      // k_lag_hess_tree work list
