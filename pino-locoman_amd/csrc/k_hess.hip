@@ -255,27 +255,30 @@ struct TreeSweep {
 
 // contact forces on body j (f_b -= [fl; p x fl], fl = oR^T f_world) and its feet's velocity rows
 // (phi += (v_lin + w x p) . oR^T mu); first / kk: body j's place in its chain (first = -1: the root)
-// (f: the contact forces, plain or seeded -- k_lag_hess_tree<true>)
+// (fx: the contact forces; f(e, c): the external frame's, plain or seeded -- k_lag_hess_tree<true>)
 template <class F3>
 __device__ void body_frames(const PlOcpConst& O, const TreeSweep& T, int first, int kk, int j, int type, int node,
-                            const HDual* vj, const F3& f, const double* lam, const double* p, HDual* fb, HDual& phi) {
+                            const HDual* vj, const double* fx, const F3& f, const double* lam, const double* p,
+                            HDual* fb, HDual& phi) {
   for (int e = 0; e < O.nee; ++e) {
     const PlFrameRef& F = (e < O.nfeet) ? O.feet[e] : O.ext;
     if (F.joint != j) continue;
     HDual fl[3], t[3];
-    const decltype(f(0, 0)) fw[3] = {f(e, 0), f(e, 1), f(e, 2)};
     const int rxy = e < O.nfeet ? block_row(O, type, PL_RB_FVXY, e) : -1;
     const int rz = e < O.nfeet ? block_row(O, type, PL_RB_FVZ, e) : -1;
-    if (rxy >= 0 || rz >= 0) {
+    if (e >= O.nfeet) {  // the external force frame (seeded in k_lag_hess_tree<true>)
+      const decltype(f(0, 0)) fw[3] = {f(e, 0), f(e, 1), f(e, 2)};
+      T.to_body(first, kk, fw, fl);
+    } else if (rxy >= 0 || rz >= 0) {
       const double c = p[O.P.contact + 4 * node + e];
       const double mu[3] = {rxy >= 0 ? c * lam[rxy] : 0.0, rxy >= 0 ? c * lam[rxy + 1] : 0.0,
                             rz >= 0 ? lam[rz] : 0.0};
       HDual g[3], wxp[3];
-      T.to_body2(first, kk, fw, mu, fl, g);
+      T.to_body2(first, kk, fx + 3 * e, mu, fl, g);
       crossd(F.p, vj + 3, wxp);  // p x w = -(w x p)
       for (int k = 0; k < 3; ++k) phi += (vj[k] - wxp[k]) * g[k];
     } else {
-      T.to_body(first, kk, fw, fl);
+      T.to_body(first, kk, fx + 3 * e, fl);
     }
     crossd(F.p, fl, t);
     for (int k = 0; k < 3; ++k) { fb[k] -= fl[k]; fb[3 + k] -= t[k]; }
@@ -432,7 +435,7 @@ __global__ __launch_bounds__(64) void k_lag_hess_tree(PlDev d, int B, int n, int
     T.to_body(0, -1, mg, a1);
     for (int c = 0; c < 3; ++c) { a1[c] = a1[c] + a[c]; a1[3 + c] = HDual(a[3 + c]); }
     body_wrench(M.mass[1], M.lever[1], M.Ic[1], a1, v1, f1);
-    body_frames(O, T, 0, -1, 1, type, i, v1, f, lam, p, f1, phi);
+    body_frames(O, T, 0, -1, 1, type, i, v1, fx, f, lam, p, f1, phi);
     for (int c = 0; c < 6; ++c) phi += lam[rb + c] * f1[c];
   }
   for (int ch = 0; ch < M.nchains; ++ch) {
@@ -465,7 +468,7 @@ __global__ __launch_bounds__(64) void k_lag_hess_tree(PlDev d, int B, int n, int
       for (int q = 0; q < 6; ++q) pL[q] = aj[q];
       HDual fj[6];
       body_wrench(M.mass[jt], M.lever[jt], M.Ic[jt], pa, pv, fj);
-      body_frames(O, T, first, kk, jt, type, i, pv, f, lam, p, fj, phi);
+      body_frames(O, T, first, kk, jt, type, i, pv, fx, f, lam, p, fj, phi);
       for (int q = 0; q < 6; ++q) phi += pL[q] * fj[q];
     }
   }
