@@ -428,11 +428,13 @@ def main():
             # roofline; the ADMM sweeps' HBM line above moves to admm_roofline
             hp = hprof
             h_avg = hp["hess_ms"] / max(1, hp["launches"])
-            hf = measured_hess_flops(B, args.nodes, workload, "pb")
+            hf = measured_hess_flops(B, args.nodes, workload, "sweep")
             ach = hf["flops_per_launch"] / (h_avg * 1e-3) / 1e12 if (hf and h_avg > 0) else None
             out["admm_roofline"] = out["roofline"]
-            out["roofline"] = {"bound": "fp64_valu", "kernel": "k_lag_hess (+ k_lag_hess_lin for whole_body_rnea)",
-                               "mapping": "pb", "achieved": ach,
+            out["roofline"] = {"bound": "fp64_valu",
+                               "kernel": "Lagrangian Hessian (k_lag_hess_tree + _vv + _lin + _cone; k_lag_hess_pb "
+                                         "off the rnea family)",
+                               "mapping": "sweep", "achieved": ach,
                                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                                "frac": ach / FP64_PEAK_TFLOPS if ach is not None else None, "traffic": None,
                                "avg_launch_ms": h_avg, "launches": hp["launches"],

@@ -1,16 +1,14 @@
 #!/bin/bash
 # SQ instruction-mix / stall counters of k_lag_hess (interior-point Hessian) at B2G rnea N=50,
 # B = 1024 (or the third argument), one IP MPC step (separate --pmc passes), plus its rocprof kernel stats and the F64
-# flops per launch (tools/hess_flops.py).  Usage: bash tools/gpu_hess_pmc.sh <tag> [pairs|pb] [batch]
-# (pairs: PL_HESS_PB=0, the one-pair-per-lane mapping; default: one problem per lane)
+# flops per evaluation (tools/hess_flops.py).  Usage: bash tools/gpu_hess_pmc.sh <tag> [batch]
 set -o pipefail
 export TMPDIR=/tmp
 T=${1:-r04_hess}
 O=gpurun_out/$T
 mkdir -p $O
-MAP=pb
-if [ "$2" = "pairs" ]; then export PL_HESS_PB=0; MAP=pairs; fi
-BATCH=${3:-1024}
+MAP=sweep
+BATCH=${2:-1024}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --solver fatrop --steps 1 --warmup 0 --no-cpu-baseline --batch $BATCH --host-io-steps 0 > $O/prof.log 2>&1 || { echo "prof failed"; tail -5 $O/prof.log; exit 1; }
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
 P2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VMEM"

@@ -17,6 +17,6 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || exit 1
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 bench.py --no-cpu-baseline > gpurun_out/prof.log 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'k_admm<' --output-format csv -d "$R/gpurun_out/pmc_fetch" -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'k_admm<' --output-format csv -d "$R/gpurun_out/pmc_write" -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'k_admm<' --output-format csv -d "$R/gpurun_out/pmc_fetch" -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline --host-io-steps 0 > gpurun_out/pmc_fetch.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'k_admm<' --output-format csv -d "$R/gpurun_out/pmc_write" -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline --host-io-steps 0 > gpurun_out/pmc_write.log 2>&1 || exit 1
 python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_fetch.log gpurun_out/admm_traffic.json

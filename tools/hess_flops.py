@@ -1,5 +1,4 @@
-"""F64 flops per Lagrangian-Hessian evaluation (k_lag_hess_pb / k_lag_hess, plus
-k_lag_hess_lin for whole_body_rnea) from a rocprofv3 --pmc pass (tools/gpu_hess_pmc.sh pass 3:
+"""F64 flops per Lagrangian-Hessian evaluation (every k_lag_hess_* kernel of one evaluation) from a rocprofv3 --pmc pass (tools/gpu_hess_pmc.sh pass 3:
 SQ_INSTS_VALU_FMA_F64, SQ_INSTS_VALU_MUL_F64, SQ_INSTS_VALU_ADD_F64 are wave-level instruction
 counts: flops = 64 lanes x (2 FMA + MUL + ADD)), keyed to the Hessian sources (bench.py
 hess_source_sha) so bench.py never applies it to another kernel revision.
@@ -27,17 +26,17 @@ def main():
             per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
     if not per:
         raise SystemExit("no k_lag_hess dispatches")
-    # one Hessian evaluation = the pair kernel's dispatch (+ k_lag_hess_lin's for whole_body_rnea):
-    # total flops over the number of pair-kernel dispatches
+    # one Hessian evaluation = one dispatch of each of its kernels (k_lag_hess_tree / _vv / _lin /
+    # _cone for the rnea family, k_lag_hess_pb otherwise): total flops over the evaluations
     names = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if "k_lag_hess" in r["Kernel_Name"]:
                 names[r["Dispatch_Id"]] = r["Kernel_Name"]
-    npair = sum(1 for k in per if "k_lag_hess_lin" not in names[k])
+    n_eval = max(collections.Counter(names[k] for k in per).values())
     tot = sum(64.0 * (2 * c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_ADD_F64"])
               for c in per.values())
-    fl = [tot / max(1, npair)] * max(1, npair)
+    fl = [tot / n_eval] * n_eval
     import bench
     rec = {"flops_per_launch": sum(fl) / len(fl), "dispatches": len(fl), "batch": batch, "nodes": nodes,
            "workload": f"b2g whole_body_rnea N={nodes} MPC step", "mapping": mapping, "src_sha": bench.hess_source_sha(),
