@@ -175,9 +175,11 @@ typedef struct {
   double delta_c;      /* 1e-4  dual regularisation (equality rows weighted 1 / delta_c) */
   int max_iter;        /* 10    (ocp.py:256), at most 32 */
   int ls_max;          /* 12    line-search trials */
-  int n_refine;        /* 8     iterative-refinement solves of each Newton system (the Lagrangian
+  int n_refine;        /* 8     most iterative-refinement solves of each Newton system (the Lagrangian
                           Hessian makes the reduced systems stiffer: B2G rnea needs ~6 to
-                          reach the sparse LU's direction to 1e-9 with the block inverses) */
+                          reach the sparse LU's direction to 1e-9 with the block inverses); a
+                          problem stops refining once a correction is below 1e-12 |dx|_inf or
+                          more than half the previous one */
   int hessian;         /* PL_IP_HESS_EXACT: the Lagrangian Hessian of f + lam^T g (CasADi's
                           exact Hessian of the Opti/Fatrop solve, ocp.py:248-263) with the
                           inertia correction; PL_IP_HESS_GN: the objective's diagonal only */

@@ -397,9 +397,9 @@ __device__ __forceinline__ void ip_wsync() {
 }
 
 __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int N, int n, int m, int nnz, double delta_w, int hlag,
-                                                   long long hl_stride, int4 hnz_off, int tau_nodes) {
+                                                   long long hl_stride, int4 hnz_off, int tau_nodes, int iref) {
   const int b = blockIdx.x;
-  if (!d.ipinfo[b].active) return;
+  if (!d.ipinfo[b].active || d.info[b].done) return;  // done: this solve's refinement has converged
   const double* A = d.Araw + (size_t)b * nnz;
   const double* W = d.rho + (size_t)b * m;
   const double* rh = d.ip_rh + (size_t)b * m;
@@ -421,8 +421,43 @@ __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int N, int n, int m,
     ya[r] = 0.0;
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < n; j += 256) dx[j] += xa[j];
-  __syncthreads();
+  double cmax = 0.0, dmax = 0.0;
+  for (int j = threadIdx.x; j < n; j += 256) {
+    const double c = xa[j], dn = dx[j] + c;
+    dx[j] = dn;
+    cmax = fmax(cmax, fabs(c));
+    dmax = fmax(dmax, fabs(dn));
+  }
+  {  // converged: the last correction is below 1e-12 |dx| (IPOPT's refinement stops at a residual
+     // ratio of 1e-10) or no longer shrinks (more than half the one before: the solves have
+     // reached the factor's noise floor); n_refine is the most solves a system gets.  The problem
+     // then skips the remaining refinement solves of this Newton system (info->done, which the
+     // sweep kernels test; k_ip_step clears it), and its correction buffer is zeroed
+    __shared__ double s_c[256], s_d[256];
+    __shared__ int s_stop;
+    s_c[threadIdx.x] = cmax;
+    s_d[threadIdx.x] = dmax;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (threadIdx.x < w) {
+        s_c[threadIdx.x] = fmax(s_c[threadIdx.x], s_c[threadIdx.x + w]);
+        s_d[threadIdx.x] = fmax(s_d[threadIdx.x], s_d[threadIdx.x + w]);
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      PlIpInfo* ip = d.ipinfo + b;
+      const double c = s_c[0];
+      s_stop = iref >= 1 && (c <= 1e-12 * s_d[0] || (iref >= 2 && c > 0.5 * ip->ref_last));
+      ip->ref_last = c;
+      if (s_stop) d.info[b].done = 1;
+    }
+    __syncthreads();
+    if (s_stop) {
+      for (int j = threadIdx.x; j < n; j += 256) xa[j] = 0.0;
+      return;
+    }
+  }
   const double* Hb = hlag ? d.Hlag + (size_t)b * hl_stride : nullptr;
   if (Hb) {  // qs = H_i dx_{w_i} per node block (k_lag_hess's packed lower blocks; none on node N)
     __shared__ double hy[4][PL_IP_NWMAX], hx[4][PL_IP_NWMAX];
@@ -555,6 +590,7 @@ __global__ __launch_bounds__(256) void k_ip_step(PlDev d, int N, int n, int m, i
   const double* grad = d.grad + (size_t)b * n;
   const double mu = ip->mu;
   const double tau = fmax(TAU_MIN, 1.0 - mu);
+  if (threadIdx.x == 0) d.info[b].done = 0;  // k_ip_refine's converged flag (set again below on termination)
   {  // the last sweep's correction completes the step
     const double* xa = d.xa + (size_t)b * n;
     const double* za = d.za + (size_t)b * m;
@@ -783,10 +819,10 @@ static void ip_factor(PlOcpHandle* h) {
   h->fac_hlag = 0;
 }
 
-static void ip_refine(PlOcpHandle* h, const PlIpSettings& st) {
+static void ip_refine(PlOcpHandle* h, const PlIpSettings& st, int iref) {
   hipLaunchKernelGGL(k_ip_refine, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz, st.delta_w,
                      h->ip_hess == PL_IP_HESS_EXACT ? 1 : 0, h->hl_stride,
-                     make_int4(h->hnz_off[0], h->hnz_off[1], h->hnz_off[2], h->hnz_off[3]), h->oc.tau_nodes);
+                     make_int4(h->hnz_off[0], h->hnz_off[1], h->hnz_off[2], h->hnz_off[3]), h->oc.tau_nodes, iref);
 }
 
 // One interior-point solve of every problem from d.x (the warm start), enqueued on the
@@ -810,7 +846,7 @@ void enqueue_ip(PlOcpHandle* h) {
     launch_admm_init(h);
     launch_admm(h, 1, 0, 0);
     for (int r = 0; r < st.n_refine; ++r) {
-      ip_refine(h, st);
+      ip_refine(h, st, r);
       launch_admm_init_zero(h);  // k_ip_refine zeroed x, z, y
       launch_admm(h, 1, 0, 0);
     }
@@ -839,7 +875,7 @@ void enqueue_ip_direction(PlOcpHandle* h) {
   launch_admm_init(h);
   launch_admm(h, 1, 0, 0);
   for (int r = 0; r < st.n_refine; ++r) {
-    ip_refine(h, st);
+    ip_refine(h, st, r);
     launch_admm_init_zero(h);
     launch_admm(h, 1, 0, 0);
   }
