@@ -96,7 +96,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   PlProbInfo* info = d.info + b;
   if (info->done) return;
   // optional phase timing (s_memtime, per wave) into d.dbg[b][0..15]
-  unsigned long long tacc[TIMING ? 12 : 1] = {}, tlast = 0;
+  unsigned long long tacc[TIMING ? 14 : 1] = {}, tlast = 0;
   auto T = [&](int slot) __attribute__((always_inline)) {
     if constexpr (TIMING) {
       const unsigned long long now = __builtin_amdgcn_s_memtime();
@@ -452,14 +452,18 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     // ---- start: everything prefetched for this step becomes current (the one wait),
     // this step's A goes to LDS, then the previous step's deferred stores
     __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): step q-1's loads (and stores) are done
+    T(10);
     E = En;
     LR = LRn;
     LC = LCn;
     // the next step's row / column operands right away: a whole step of cover (r05; issued after
     // the mat-vec / the row gathers until r04, the x update then waited ~2 k cycles for them)
     prefetch_LR(kind1, i1, LRn);
+    T(11);
     prefetch_LC(kind1, i1, LCn);
+    T(12);
     if (pend.kind >= 0) issue_stores(pend);  // step q-1's stores, behind its wait
+    T(13);
     if (bw) stage(ne, Ai);
     else if (fwd_asb && kind != KF0) stage(an[i - 1].nent, As + an[i - 1].ent_off);
     T(0);
@@ -777,7 +781,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   }
   if constexpr (TIMING) {
     if (lane == 0 && d.dbg)
-      for (int k = 0; k < 10; ++k) d.dbg[(size_t)b * 16 + k] += (double)tacc[k];
+      for (int k = 0; k < 14; ++k) d.dbg[(size_t)b * 16 + k] += (double)tacc[k];
   }
 }
 

@@ -30,13 +30,18 @@ ALL = bo.debug("admm_t", B * 40)[:B * 32]
 T = ALL[:B * 16].reshape(B, 16)
 it = st["admm_iters"].astype(float)
 steps = it * (2 * N)  # one factor block per step
-names = ["start(wait+stage)", "flush stores", "gathers+v", "prefetch issue", "matvec", "rows gather",
+names = ["start(issue+stage)", "flush stores", "gathers+v", "prefetch issue", "matvec", "rows gather",
          "z update", "cols gather", "x update", "T0 + end"]
 per = T[:, :10] / steps[:, None]
+wait = T[:, 10] / steps
+print(f"{'vmcnt wait':18s} mean cycles/step {wait.mean():9.1f}")
+for k, nm in ((11, "  prefetch LR"), (12, "  prefetch LC"), (13, "  issue stores")):
+    print(f"{nm:18s} mean cycles/step {(T[:, k] / steps).mean():9.1f}")
+sub = T[:, 11:14].sum(1) / steps
 for k, nm in enumerate(names):
     print(f"{nm:18s} mean cycles/step {per[:, k].mean():9.1f}  p10 {np.percentile(per[:, k], 10):9.1f}  "
           f"p90 {np.percentile(per[:, k], 90):9.1f}")
-print("total cycles/step", per.sum(1).mean())
+print("total cycles/step", per.sum(1).mean() + wait.mean() + sub.mean())
 F = ALL[B * 16:].reshape(B, 16)[:, :8] / (N + 1)
 fn = ["sweep+symm+wait", "S_ux", "S_uu", "Y", "E", "(sweep only)", "last store", "(waves1-3 work)"]
 for k, nm in enumerate(fn):
