@@ -731,7 +731,7 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
         dalloc(o, &h->d.ip_zu, Bm) || dalloc(o, &h->d.ip_rh, Bm) || dalloc(o, &h->d.ip_dl, Bm) ||
         dalloc(o, &h->d.ip_ds, Bm) || dalloc(o, &h->d.ip_jdx, Bm) || dalloc(o, &h->d.ip_dx, (size_t)h->B * h->n) ||
         dalloc(o, &h->d.ipinfo, (size_t)h->B) || dalloc(o, &h->d.ip_dwi, (size_t)2 * h->B) ||
-        dalloc(o, &h->d.ip_iflag, (size_t)4 * h->B))
+        dalloc(o, &h->d.ip_iflag, (size_t)4 * h->B) || dalloc(o, &h->d.ip_act, (size_t)h->B + 1))
       return -2;
     // Lagrangian Hessian work list (k_hess.hip): the structurally non-zero column pairs
     // j <= k of every w_i block (hess_pattern, one probe per node type); node blocks packed

@@ -792,6 +792,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
 // node's whole A slice (~56 lines of 128 B) for ~150 values; here they are 1.5 KB contiguous.
 __global__ __launch_bounds__(64) void k_acpl(PlDev d, int N, int nnz, int ndx) {
   const int b = blockIdx.x / (N + 1), i = blockIdx.x - b * (N + 1);
+  if (ip_skip(d, b)) return;
   const int lane = threadIdx.x;
   const PlAdmmNode& a = d.anodes[i];
   double* out = d.Acpl + ((size_t)b * (N + 1) + i) * PL_ACPL;

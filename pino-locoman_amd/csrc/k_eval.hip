@@ -56,6 +56,7 @@ __global__ __launch_bounds__(64) void k_eval_values(PlDev d, int B, int N, int n
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= B * N) return;
   const int b = tid / N, i = tid - b * N;
+  if (ip_skip(d, b)) return;
   const PlOcpConst& O = *d.oc;
   const PlModel& M = *d.model;
   const PlNode nd = d.nodes[i];
@@ -82,6 +83,7 @@ template <int DYN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PL_JAC_WAVES)))
 void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz, int jl_len) {
   const int b = blockIdx.y;
+  if (ip_skip(d, b)) return;
   const int q = (int)blockIdx.x * 64 + threadIdx.x;
   const int first = d.jlist[blockIdx.x * 64].x;  // the wave's first node (never padding)
   const bool valid = q < jl_len && d.jlist[min(q, jl_len - 1)].x >= 0;
@@ -155,6 +157,7 @@ struct UnitIn {  // e_k (k < 0: zero)
 template <int DYN>
 __global__ __launch_bounds__(64) void k_eval_jac_lin(PlDev d, int B, int n, int np, int nnz, int len) {
   const int b = blockIdx.y;
+  if (ip_skip(d, b)) return;
   const int q = (int)blockIdx.x * 64 + threadIdx.x;
   __shared__ double kst[PL_KIN_STORE * 64];
   __shared__ double kval[PL_KIN_STORE];  // the (unused) values of the kinematic outputs
@@ -194,6 +197,7 @@ __global__ __launch_bounds__(64) void k_eval_jac_lin(PlDev d, int B, int n, int 
 
 __global__ __launch_bounds__(256) void k_objective(PlDev d, int N, int n, int np) {
   const int b = blockIdx.x;
+  if (ip_skip(d, b)) return;
   __shared__ double red[256];
   double f = objective_wg<true>(d, b, N, n, np, d.x + (size_t)b * n, nullptr, 0.0, d.grad + (size_t)b * n, red);
   if (threadIdx.x == 0) d.work[(size_t)b * 8 + 0] = f;

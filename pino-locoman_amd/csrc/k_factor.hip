@@ -255,6 +255,7 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
   const int task = blockIdx.x;
   const int b = task / ni;
   const int i = i0 + (task - b * ni);
+  if (ip_skip(d, b)) return;
   if constexpr (HL) {
     if (fac_only && !d.ip_iflag[4 * b + 1]) return;
   }
@@ -476,6 +477,7 @@ __global__ __launch_bounds__(NT) void k_fchain(PlDev d, int N, int m, int nnz, i
                                                int nwm, int ny, int ncw, int fac_only, int gc, int ncm, int nxcm,
                                                int short_cw) {
   const int b = blockIdx.x;
+  if (ip_skip(d, b)) return;
   if constexpr (HL) {
     if (fac_only && !d.ip_iflag[4 * b + 1]) return;
   }

@@ -36,8 +36,9 @@ struct HessEmit {
 // headline: removed.)
 template <int DYN>
 __global__ __launch_bounds__(64) void k_lag_hess_pb(PlDev d, int B, int N, int n, int m, int np, long long hl_stride) {
-  const int b = blockIdx.y * 64 + threadIdx.x;
-  if (b >= B || !d.ipinfo[b].active) return;
+  const int qa = blockIdx.y * 64 + threadIdx.x;  // the active problems, compacted (k_ip_compact)
+  if (qa >= d.ip_act[B]) return;
+  const int b = d.ip_act[qa];
   const PlOcpConst& O = *d.oc;
   const PlModel& M = *d.model;
   const double* x = d.x + (size_t)b * n;
@@ -85,8 +86,9 @@ struct LamIn {  // lambda_tau over v: the base rows' multipliers, then the joint
 
 __global__ __launch_bounds__(64) void k_lag_hess_lin(PlDev d, int B, int n, int m, int np, long long hl_stride,
                                                      int3 rb_base, int3 rb_tau) {
-  const int b = blockIdx.y * 64 + threadIdx.x;
-  if (b >= B || !d.ipinfo[b].active) return;
+  const int qa = blockIdx.y * 64 + threadIdx.x;  // the active problems, compacted (k_ip_compact)
+  if (qa >= d.ip_act[B]) return;
+  const int b = d.ip_act[qa];
   const PlOcpConst& O = *d.oc;
   const int2 w = d.hlin[blockIdx.x];
   const int i = __builtin_amdgcn_readfirstlane(w.x);
@@ -328,8 +330,9 @@ __device__ void base_pose(const double* xi, const VecIn<HDual>& dx, HDual* qb) {
 // confinement included); one pair per wave, one problem per lane.
 __global__ __launch_bounds__(64) void k_lag_hess_vv(PlDev d, int B, int n, int m, int np, long long hl_stride,
                                                     int3 rb_base, int3 rb_tau) {
-  const int b = blockIdx.y * 64 + threadIdx.x;
-  if (b >= B || !d.ipinfo[b].active) return;
+  const int qa = blockIdx.y * 64 + threadIdx.x;  // the active problems, compacted (k_ip_compact)
+  if (qa >= d.ip_act[B]) return;
+  const int b = d.ip_act[qa];
   const PlOcpConst& O = *d.oc;
   const PlModel& M = *d.model;
   const int2 w = d.hvv[blockIdx.x];
@@ -391,8 +394,9 @@ __global__ __launch_bounds__(64) void k_lag_hess_vv(PlDev d, int B, int n, int m
 // it moves with q, so those pairs are this sweep with the force seeded); d.htrf
 template <bool SF>
 __global__ __launch_bounds__(64) void k_lag_hess_tree(PlDev d, int B, int n, int m, int np, long long hl_stride) {
-  const int b = blockIdx.y * 64 + threadIdx.x;
-  if (b >= B || !d.ipinfo[b].active) return;
+  const int qa = blockIdx.y * 64 + threadIdx.x;  // the active problems, compacted (k_ip_compact)
+  if (qa >= d.ip_act[B]) return;
+  const int b = d.ip_act[qa];
   const PlOcpConst& O = *d.oc;
   const PlModel& M = *d.model;
   const int2 w = (SF ? d.htrf : d.htr)[blockIdx.x];
@@ -524,9 +528,37 @@ __global__ __launch_bounds__(64) void k_lag_hess_cone(PlDev d, int B, int m, int
     default: hipLaunchKernelGGL(KERNEL<PL_DYN_ABA>, __VA_ARGS__); break;             \
   }
 
+// The active problems of this interior-point iteration in ascending order (one 256-thread
+// block; a ballot prefix per wave, wave offsets in LDS): the Hessian kernels map lanes to
+// d.ip_act, so the waves past the active count exit at once when most problems have
+// terminated (a warm-started MPC step's line-search failures).  Lanes write only their own
+// problem's entries, so the results do not depend on the mapping.
+__global__ __launch_bounds__(256) void k_ip_compact(PlDev d, int B) {
+  __shared__ int s_wave[4], s_base;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_base = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < B; c0 += 256) {
+    const int b = c0 + threadIdx.x;
+    const bool act = b < B && d.ipinfo[b].active;
+    const unsigned long long m = __ballot(act);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wave[w] = __popcll(m);
+    __syncthreads();
+    int off = s_base;
+    for (int k = 0; k < w; ++k) off += s_wave[k];
+    if (act) d.ip_act[off + before] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) s_base += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) d.ip_act[B] = s_base;
+}
+
 void launch_lag_hess(PlOcpHandle* h) {
   const bool prof = h->profile && h->prof_hn < 16;  // pl_mpc_step collects the slots before every step
   if (prof) hipEventRecord(h->prof_hev[h->prof_hn][0], h->stream);
+  hipLaunchKernelGGL(k_ip_compact, dim3(1), dim3(256), 0, h->stream, h->d, h->B);
   if (h->hlin_len > 0)
     hipLaunchKernelGGL(k_lag_hess_lin, dim3(h->hlin_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,
                        h->m, h->np, h->hl_stride, make_int3(h->hl_rb_base[0], h->hl_rb_base[1], h->hl_rb_base[2]),

@@ -832,6 +832,7 @@ void enqueue_ip(PlOcpHandle* h) {
   const PlSettings saved = h->set;
   launch_eval_values(h, h->d.x);
   hipLaunchKernelGGL(k_ip_init, dim3(h->B), dim3(256), 0, h->stream, h->d, h->m, st, h->ip_lam_warm);
+  h->d.ipskip = h->d.ipinfo;  // from here on the terminated problems skip evaluation and factor
   h->set.sigma = st.delta_w;  // factor: Ps + delta_w on the diagonal
   h->set.alpha = 1.0;         // ADMM sweep: x = x~, z = A x~
   for (int k = 0; k <= st.max_iter; ++k) {
@@ -854,6 +855,7 @@ void enqueue_ip(PlOcpHandle* h) {
                     0);
   }
   h->set = saved;
+  h->d.ipskip = nullptr;
   hipLaunchKernelGGL(k_ip_finish, dim3((h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B);
 }
 

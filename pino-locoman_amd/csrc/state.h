@@ -226,6 +226,8 @@ struct PlDev {
   double* ip_lam0;   // lam_g warm start (opti.set_initial(opti.lam_g, lam_g), ocp_whole_body_rnea.py:234-235)
   // exact Lagrangian Hessian (k_hess.hip) and its inertia correction (k_ip.hip)
   int* hnz;          // per node type: the written entries (row | col << 16) of a Lagrangian Hessian block
+  const PlIpInfo* ipskip;  // set only inside an interior-point solve (enqueue_ip): the evaluation and
+                           // factor kernels skip the problems that have terminated (active == 0)
   int2* hlist;       // (node, j | k << 16) column pairs of the w_i blocks
   int2* hcone;       // whole_body_rnea / whole_body_acc: (node, foot-force column) of the cone curvature (k_lag_hess_cone)
   int2* htrf;        // the (dq, external force) pairs (k_lag_hess_tree<true>)
@@ -236,6 +238,8 @@ struct PlDev {
   int* hoff;         // packed-lower offset of node i's block
   double* Hlag;      // [B][hl_stride] sum_r lam_r d^2 g_r / dw_i^2, packed lower per node
   double* ip_dwi;    // [B][2]: the inertia shift of this Newton system, the last nonzero one
+  int* ip_act;       // [B + 1]: the active problems of the current IP iteration, compacted (k_ip_compact);
+                     // ip_act[B] = their count
   int* ip_iflag;     // [B][4]: not-SPD seen by the factor, refactor, resolved, tries
   double* ip_zl;     // lower / upper bound multipliers of the slacks
   double* ip_zu;
@@ -246,6 +250,11 @@ struct PlDev {
   double* ip_jdx;
   PlIpInfo* ipinfo;  // [B]
 };
+
+// an interior-point solve's terminated problem (PlDev::ipskip): nothing downstream reads its
+// evaluation or factor any more
+__device__ inline bool ip_skip(const PlDev& d, int b) { return d.ipskip && !d.ipskip[b].active; }
+
 
 struct PlOcpHandle {
   int device;

@@ -36,7 +36,7 @@ def main():
         rec = {"step": k, "counts": {int(v): int((s == v).sum()) for v in np.unique(s)},
                "fail": [[int(b), int(it[b])] for b in np.flatnonzero(s == -2)[:64]]}
         out.append(rec)
-        print(json.dumps({"step": k, "counts": rec["counts"], "fail_first": rec["fail"][:16]}), flush=True)
+        print(json.dumps({"step": k, "counts": rec["counts"], "mean_iter": float(it.mean()), "fail_first": rec["fail"][:8]}), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"ip_screen_{dyn}.json"), "w") as f:
         json.dump(out, f)
