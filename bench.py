@@ -429,7 +429,11 @@ def main():
             hp = hprof
             h_avg = hp["hess_ms"] / max(1, hp["launches"])
             hf = measured_hess_flops(B, args.nodes, workload, "sweep")
-            ach = hf["flops_per_launch"] / (h_avg * 1e-3) / 1e12 if (hf and h_avg > 0) else None
+            # the PMC pass ran every problem in every evaluation; the kernels' waves follow the
+            # active problems (k_ip_compact), so the flops of a launch scale with its lanes
+            lane_frac = hp["lanes"] / (-(-B // 64) * 64) if hp.get("lanes") else 1.0
+            flops = hf["flops_per_launch"] * lane_frac if hf else None
+            ach = flops / (h_avg * 1e-3) / 1e12 if (hf and h_avg > 0) else None
             out["admm_roofline"] = out["roofline"]
             out["roofline"] = {"bound": "fp64_valu",
                                "kernel": "Lagrangian Hessian (k_lag_hess_tree + _vv + _lin + _cone; k_lag_hess_pb "
@@ -438,7 +442,8 @@ def main():
                                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                                "frac": ach / FP64_PEAK_TFLOPS if ach is not None else None, "traffic": None,
                                "avg_launch_ms": h_avg, "launches": hp["launches"],
-                               "flops_per_launch": hf["flops_per_launch"] if hf else None,
+                               "flops_per_launch": flops,
+                               "active_lane_fraction": lane_frac,
                                "flops_source": (f"profiles/traffic/hess_flops.json (PMC F64 instruction counts, "
                                                 f"src {hf['src_sha']})" if hf else None)}
             ist = bo.ip_stats()  # the last MPC step's solves

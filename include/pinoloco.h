@@ -310,8 +310,9 @@ int pl_ocp_get_admm_kernel(const pl_ocp* o);
  * largest node's A count, the descriptor's debug_paths bits]. */
 int pl_ocp_profile(pl_ocp* o, int enable);
 int pl_ocp_profile_read(pl_ocp* o, double* out);
-/* The same for the interior point's Lagrangian-Hessian launches (k_lag_hess): out[0] total ms,
- * out[1] launches (bench.py --solver fatrop: the IP line's roofline kernel). */
+/* The same for the interior point's Lagrangian-Hessian launches (k_lag_hess_*): out[0] total ms,
+ * out[1] launches, out[2] problem lanes per launch (the active problems rounded up to whole
+ * waves; bench.py --solver fatrop scales the per-launch flops by it). */
 int pl_ocp_profile_read_hess(pl_ocp* o, double* out);
 int pl_ocp_sizes(const pl_ocp* o, long long* out);
 

@@ -731,7 +731,7 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
         dalloc(o, &h->d.ip_zu, Bm) || dalloc(o, &h->d.ip_rh, Bm) || dalloc(o, &h->d.ip_dl, Bm) ||
         dalloc(o, &h->d.ip_ds, Bm) || dalloc(o, &h->d.ip_jdx, Bm) || dalloc(o, &h->d.ip_dx, (size_t)h->B * h->n) ||
         dalloc(o, &h->d.ipinfo, (size_t)h->B) || dalloc(o, &h->d.ip_dwi, (size_t)2 * h->B) ||
-        dalloc(o, &h->d.ip_iflag, (size_t)4 * h->B) || dalloc(o, &h->d.ip_act, (size_t)h->B + 1))
+        dalloc(o, &h->d.ip_iflag, (size_t)4 * h->B) || dalloc(o, &h->d.ip_act, (size_t)h->B + 2))
       return -2;
     // Lagrangian Hessian work list (k_hess.hip): the structurally non-zero column pairs
     // j <= k of every w_i block (hess_pattern, one probe per node type); node blocks packed
@@ -1215,6 +1215,7 @@ extern "C" int pl_ocp_profile(pl_ocp* o, int enable) {
   h->prof_hn = 0;
   h->prof_hess_ms = 0.0;
   h->prof_hess_launches = 0;
+  if (enable && h->d.ip_act) PL_CHECK_HIP(hipMemsetAsync(h->d.ip_act + h->B + 1, 0, sizeof(int), h->stream));
   if (enable) {
     launch_reset_prof(h);
     PL_CHECK_HIP(hipStreamSynchronize(h->stream));
@@ -1248,6 +1249,10 @@ extern "C" int pl_ocp_profile_read_hess(pl_ocp* o, double* out) {
   prof_collect(&o->h);
   out[0] = o->h.prof_hess_ms;
   out[1] = (double)o->h.prof_hess_launches;
+  int lanes = 0;  // Hessian lanes launched since profiling started (k_ip_compact)
+  if (o->h.d.ip_act)
+    PL_CHECK_HIP(hipMemcpy(&lanes, o->h.d.ip_act + o->h.B + 1, sizeof(int), hipMemcpyDeviceToHost));
+  out[2] = o->h.prof_hess_launches > 0 ? (double)lanes / o->h.prof_hess_launches : 0.0;
   return 0;
 }
 

@@ -552,7 +552,10 @@ __global__ __launch_bounds__(256) void k_ip_compact(PlDev d, int B) {
     if (threadIdx.x == 0) s_base += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
     __syncthreads();
   }
-  if (threadIdx.x == 0) d.ip_act[B] = s_base;
+  if (threadIdx.x == 0) {
+    d.ip_act[B] = s_base;
+    d.ip_act[B + 1] += (s_base + 63) / 64 * 64;  // lanes of the Hessian waves that will run
+  }
 }
 
 void launch_lag_hess(PlOcpHandle* h) {

@@ -238,8 +238,9 @@ struct PlDev {
   int* hoff;         // packed-lower offset of node i's block
   double* Hlag;      // [B][hl_stride] sum_r lam_r d^2 g_r / dw_i^2, packed lower per node
   double* ip_dwi;    // [B][2]: the inertia shift of this Newton system, the last nonzero one
-  int* ip_act;       // [B + 1]: the active problems of the current IP iteration, compacted (k_ip_compact);
-                     // ip_act[B] = their count
+  int* ip_act;       // [B + 2]: the active problems of the current IP iteration, compacted (k_ip_compact);
+                     // ip_act[B] = their count, ip_act[B + 1] = the lanes of the Hessian waves launched
+                     // since pl_ocp_profile(1) (the IP line's flop scaling)
   int* ip_iflag;     // [B][4]: not-SPD seen by the factor, refactor, resolved, tries
   double* ip_zl;     // lower / upper bound multipliers of the slacks
   double* ip_zu;

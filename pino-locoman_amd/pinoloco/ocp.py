@@ -431,9 +431,9 @@ class BatchedOCP:
         return {"admm_ms": out[0], "launches": int(out[1]), "problem_iters": int(out[2])}
 
     def profile_read_hess(self):
-        out = np.zeros(2)
+        out = np.zeros(3)
         _lib.check(_lib.lib().pl_ocp_profile_read_hess(self.h, _lib.dptr(out)))
-        return {"hess_ms": out[0], "launches": int(out[1])}
+        return {"hess_ms": out[0], "launches": int(out[1]), "lanes": out[2]}
 
     def sizes(self):
         out = (C.c_longlong * 13)()
