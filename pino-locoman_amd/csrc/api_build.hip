@@ -849,6 +849,22 @@ int build_factor_prog(pl_ocp* o) {
 int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, bool use_lin, int* n_ex) {
   const PlOcpConst& O = o->h.oc;
   std::vector<int2> ex, ch;
+  const PlModel& Mo = o->h.model;
+  const auto chain_of = [&](int j) {
+    for (int c = 0; c < Mo.nchains; ++c)
+      if (j >= Mo.chain_first[c] && j < Mo.chain_first[c] + Mo.chain_len[c]) return c;
+    return -1;
+  };
+  const auto vidx_chain = [&](int vi) {  // the chain of velocity index vi (-1: the base)
+    if (vi < 6) return -1;
+    for (int j = 2; j < Mo.njoints; ++j)
+      if (Mo.idx_v[j] == vi) return chain_of(j);
+    return -1;
+  };
+  // whole_body_rnea / _acc with the linear a / f columns: the dq / dv tree-pass columns run
+  // confined to their chain (k_eval_jac only_ch); the r03 path (PL_PATH_JAC_DUAL_ALL) does not
+  const bool confine = use_lin && (O.dyn == PL_DYN_RNEA || O.dyn == PL_DYN_ACC);
+  const int slots = confine ? PL_JAC_SLOTS_CH : PL_JAC_SLOTS;
   lin.clear();
   for (int i = 0; i < o->h.N; ++i) {
     const PlNode& nd = o->nodes[i];
@@ -870,16 +886,28 @@ int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, b
           continue;
         }
       }
-      (cheap ? ch : ex).push_back(make_int2(i, lc));
+      int tag = 0;
+      if (confine && !cheap && lc < O.ndx) tag = (vidx_chain(lc < O.nv ? lc : lc - O.nv) + 1) << 16;
+      (cheap ? ch : ex).push_back(make_int2(i, lc | tag));
     }
   }
+  if (confine) {  // grouped by chain (the base columns first), each group padded to whole waves
+    std::stable_sort(ex.begin(), ex.end(), [](const int2& a, const int2& b) { return (a.y >> 16) < (b.y >> 16); });
+    std::vector<int2> g;
+    for (size_t q = 0; q < ex.size(); ++q) {
+      if (q > 0 && (ex[q].y >> 16) != (ex[q - 1].y >> 16))
+        while (g.size() % 64) g.push_back(make_int2(-1, -1));
+      g.push_back(ex[q]);
+    }
+    ex.swap(g);
+  }
   while (ex.size() % 64) ex.push_back(make_int2(-1, -1));
-  // a wave's lanes hold at most PL_JAC_SLOTS consecutive nodes (shared-value slots)
+  // a wave's lanes hold at most `slots` consecutive nodes (shared-value slots)
   for (size_t w = 0; w < ex.size(); w += 64) {
     int last = ex[w].x;
     for (size_t q = w; q < w + 64; ++q) last = std::max(last, ex[q].x);
-    if (last - ex[w].x >= PL_JAC_SLOTS) {
-      pl_set_error("Jacobian wave spans more than %d nodes", PL_JAC_SLOTS);
+    if (last - ex[w].x >= slots) {
+      pl_set_error("Jacobian wave spans more than %d nodes", slots);
       return -1;
     }
   }
@@ -890,12 +918,6 @@ int build_jac_list(pl_ocp* o, std::vector<int2>& list, std::vector<int2>& lin, b
     // the chain a column's RNEA pass is confined to (k_eval_jac_lin: tree_pass only_ch; -1:
     // a base acceleration, which moves every chain); the list is grouped by chain so that a
     // wave's lanes walk the same chain.  .y = local column | (chain + 1) << 16.
-    const PlModel& Mo = o->h.model;
-    const auto chain_of = [&](int j) {
-      for (int c = 0; c < Mo.nchains; ++c)
-        if (j >= Mo.chain_first[c] && j < Mo.chain_first[c] + Mo.chain_len[c]) return c;
-      return -1;
-    };
     for (int2& w : lin) {
       const int k = w.y - O.ndx;
       int c = -1;

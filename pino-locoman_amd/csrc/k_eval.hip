@@ -85,15 +85,20 @@ void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz, int jl_len) {
   const int b = blockIdx.y;
   if (ip_skip(d, b)) return;
   const int q = (int)blockIdx.x * 64 + threadIdx.x;
+  // whole_body_rnea / _acc: a tree-pass column of chain c moves only chain c's terms (rows.h,
+  // k_hess.hip), so its pass is confined to it (tree_pass only_ch; .y = column | (c + 1) << 16,
+  // the list grouped by chain so that a wave walks one chain)
+  constexpr bool CH = DYN == PL_DYN_RNEA || DYN == PL_DYN_ACC;
+  constexpr int SLOTS = CH ? PL_JAC_SLOTS_CH : PL_JAC_SLOTS;
   const int first = d.jlist[blockIdx.x * 64].x;  // the wave's first node (never padding)
   const bool valid = q < jl_len && d.jlist[min(q, jl_len - 1)].x >= 0;
   const int2 jw = valid ? d.jlist[q] : make_int2(first, 0);
-  const int i = jw.x, lc = jw.y;
-  const int slot = min(i - first, PL_JAC_SLOTS - 1);
+  const int i = jw.x, lc = jw.y & 0xffff, only_ch = CH ? (jw.y >> 16) - 1 : -1;
+  const int slot = min(i - first, SLOTS - 1);
   // kinematic outputs: per-lane tangents + one shared value per entry and node of the
   // wave (NodeKin<Dual>; the cheap columns read no stored value)
   __shared__ double kst_tan[PL_KIN_STORE_DUAL * 64];
-  __shared__ double kst_val[PL_JAC_SLOTS * PL_KIN_STORE_DUAL];
+  __shared__ double kst_val[SLOTS * PL_KIN_STORE_DUAL];
   double* aba_slot = nullptr;
   if constexpr (DYN == PL_DYN_ABA) {
     // the shared primal of each node of the wave (tree-pass columns only): its lanes split
@@ -133,7 +138,7 @@ void k_eval_jac(PlDev d, int B, int N, int n, int np, int nnz, int jl_len) {
   VecIn<Dual> dxn{x + nn.x_off, nullptr, 0.0, lc - nd.nw};
   JacEmit e{d.rowidx + nd.ent_off, d.Araw + (size_t)b * nnz + nd.ent_off, e0, e1, 0};
   pl::node_rows<Dual, DYN>(M, O, i, p, dx, u, dxn, e, reinterpret_cast<Dual*>(kst_tan + threadIdx.x), 64,
-                           kst_val + slot * PL_KIN_STORE_DUAL, aba_slot);
+                           kst_val + slot * PL_KIN_STORE_DUAL, aba_slot, nullptr, only_ch);
 }
 
 namespace {

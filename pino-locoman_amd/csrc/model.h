@@ -18,6 +18,7 @@
 #define PL_MAXFEET 4
 #define PL_MAXNU 128
 #define PL_JAC_SLOTS 3  // nodes per Jacobian wave (k_eval_jac shared-value slots; 4 would exceed 40 KB of LDS per wave)
+#define PL_JAC_SLOTS_CH 12  // the same for the chain-confined columns of whole_body_rnea / _acc (no ABA slots)
 
 enum { PL_JT_UNIVERSE = 0, PL_JT_FREEFLYER = 1, PL_JT_REVOLUTE = 2 };
 enum { PL_AX_X = 0, PL_AX_Y = 1, PL_AX_Z = 2, PL_AX_GEN = 3 };
