@@ -349,9 +349,20 @@ __global__ __launch_bounds__(NT) void k_fnode(PlDev d, int n, int m, int nnz, in
     for (int c = tid; c < nw; c += NT) K[lidx(c, c)] += Ps[c] + sigma;
   }
   if constexpr (HL) {
+    // + H_i: a thread's entries of the packed block loaded together (one round trip per 16,
+    // not per entry: 20 k of a B2G node's cycles, r05)
     __syncthreads();
     const double* __restrict__ Hb = d.Hlag + (size_t)b * hl_stride + d.hoff[i];
-    for (int k = tid; k < nw * (nw + 1) / 2; k += NT) K[k] += Hb[k];
+    const int ne = nw * (nw + 1) / 2;
+    constexpr int HB = 16;
+    for (int k0 = 0; k0 < ne; k0 += NT * HB) {
+      double hv[HB];
+#pragma unroll
+      for (int u = 0; u < HB; ++u) hv[u] = Hb[min(k0 + u * NT + tid, ne - 1)];
+#pragma unroll
+      for (int u = 0; u < HB; ++u)
+        if (k0 + u * NT + tid < ne) K[k0 + u * NT + tid] += hv[u];
+    }
   }
   __syncthreads();
   T(2);
