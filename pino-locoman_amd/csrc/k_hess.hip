@@ -257,15 +257,38 @@ struct TreeSweep {
 
 // contact forces on body j (f_b -= [fl; p x fl], fl = oR^T f_world) and its feet's velocity rows
 // (phi += (v_lin + w x p) . oR^T mu); first / kk: body j's place in its chain (first = -1: the root)
-// (fx: the contact forces; f(e, c): the external frame's, plain or seeded -- k_lag_hess_tree<true>)
+// (fx: the contact forces; f(e, c): the external frame's, plain or seeded -- k_lag_hess_tree<true>;
+// frame ef's force and multipliers arrive already in body axes: cf, cg (cg only if has_mu))
+__device__ void foot_mu(const PlOcpConst& O, int type, int node, int e, const double* lam, const double* p,
+                        double* mu, bool* has) {  // a foot's velocity-row multipliers times coefficients
+  const int rxy = e < O.nfeet ? block_row(O, type, PL_RB_FVXY, e) : -1;
+  const int rz = e < O.nfeet ? block_row(O, type, PL_RB_FVZ, e) : -1;
+  *has = rxy >= 0 || rz >= 0;
+  const double c = e < O.nfeet ? p[O.P.contact + 4 * node + e] : 0.0;
+  mu[0] = rxy >= 0 ? c * lam[rxy] : 0.0;
+  mu[1] = rxy >= 0 ? c * lam[rxy + 1] : 0.0;
+  mu[2] = rz >= 0 ? lam[rz] : 0.0;
+}
 template <class F3>
 __device__ void body_frames(const PlOcpConst& O, const TreeSweep& T, int first, int kk, int j, int type, int node,
                             const HDual* vj, const double* fx, const F3& f, const double* lam, const double* p,
-                            HDual* fb, HDual& phi) {
+                            HDual* fb, HDual& phi, int ef = -1, const HDual* cf = nullptr, const HDual* cg = nullptr,
+                            bool has_mu = false) {
   for (int e = 0; e < O.nee; ++e) {
     const PlFrameRef& F = (e < O.nfeet) ? O.feet[e] : O.ext;
     if (F.joint != j) continue;
     HDual fl[3], t[3];
+    if (e == ef) {  // carried along the chain
+      for (int k = 0; k < 3; ++k) fl[k] = cf[k];
+      if (has_mu) {
+        HDual wxp[3];
+        crossd(F.p, vj + 3, wxp);  // p x w = -(w x p)
+        for (int k = 0; k < 3; ++k) phi += (vj[k] - wxp[k]) * cg[k];
+      }
+      crossd(F.p, fl, t);
+      for (int k = 0; k < 3; ++k) { fb[k] -= fl[k]; fb[3 + k] -= t[k]; }
+      continue;
+    }
     const int rxy = e < O.nfeet ? block_row(O, type, PL_RB_FVXY, e) : -1;
     const int rz = e < O.nfeet ? block_row(O, type, PL_RB_FVZ, e) : -1;
     if (e >= O.nfeet) {  // the external force frame (seeded in k_lag_hess_tree<true>)
@@ -445,14 +468,43 @@ __global__ __launch_bounds__(64) void k_lag_hess_tree(PlDev d, int B, int n, int
   for (int ch = 0; ch < M.nchains; ++ch) {
     if (only_ch >= 0 && ch != only_ch) continue;
     const int first = M.chain_first[ch], L = M.chain_len[ch];
-    HDual pv[6], pa[6], pL[6];
-    T.to_body(0, -1, mg, pa);
+    // the chain's first frame (a foot, or the external force frame): its world force and
+    // velocity-row multipliers are rotated into body axes joint by joint with the sweep's own
+    // rotations (cf, cg) instead of a walk from the root at the frame
+    int ef = -1, ej = -1;
+    for (int e = 0; e < O.nee && ef < 0; ++e) {
+      const int fj = e < O.nfeet ? O.feet[e].joint : O.ext.joint;
+      if (fj >= first && fj < first + L) { ef = e; ej = fj; }
+    }
+    HDual pv[6], pa[6], pL[6], cf[3], cg[3];
+    bool has_mu = false;
+    {
+      HDual R0[9];
+      pl::quat_to_R(qb + 3, R0);
+      pl::mattvec(R0, mg, pa);
+      if (ef >= 0) {
+        const decltype(f(0, 0)) fw[3] = {f(ef, 0), f(ef, 1), f(ef, 2)};
+        pl::mattvec(R0, fw, cf);
+        double mu[3];
+        foot_mu(O, type, i, ef, lam, p, mu, &has_mu);
+        if (has_mu) pl::mattvec(R0, mu, cg);
+      }
+    }
     for (int c = 0; c < 3; ++c) { pa[c] = pa[c] + a[c]; pa[3 + c] = HDual(a[3 + c]); }
     for (int c = 0; c < 6; ++c) { pv[c] = vel[c]; pL[c] = HDual(rb >= 0 ? lam[rb + c] : 0.0); }
     for (int kk = 0; kk < L; ++kk) {
       const int jt = first + kk;
       HDual s, c;
       sincos_s(qrev(M.idx_q[jt]), &s, &c);
+      if (ef >= 0 && jt <= ej) {
+        HDual t3[3];
+        rot_t(M, jt, s, c, cf, t3);
+        for (int q = 0; q < 3; ++q) cf[q] = t3[q];
+        if (has_mu) {
+          rot_t(M, jt, s, c, cg, t3);
+          for (int q = 0; q < 3; ++q) cg[q] = t3[q];
+        }
+      }
       const double* ax = M.axis[jt];
       const int iv = M.idx_v[jt];
       const HDual qd = vel[iv];
@@ -472,26 +524,59 @@ __global__ __launch_bounds__(64) void k_lag_hess_tree(PlDev d, int B, int n, int
       for (int q = 0; q < 6; ++q) pL[q] = aj[q];
       HDual fj[6];
       body_wrench(M.mass[jt], M.lever[jt], M.Ic[jt], pa, pv, fj);
-      body_frames(O, T, first, kk, jt, type, i, pv, fx, f, lam, p, fj, phi);
+      body_frames(O, T, first, kk, jt, type, i, pv, fx, f, lam, p, fj, phi, ef, cf, cg, has_mu);
       for (int q = 0; q < 6; ++q) phi += pL[q] * fj[q];
     }
   }
   double acc = phi.c;
-  // ---- the arm rows: the velocity-only tree pass on the arm's chain (pairs on the base or that chain)
+  // ---- the arm rows (Dynamics.get_frame_velocity relative to the base, dynamics/dynamics.py:86-113;
+  // rbd.h tree_pass): with l = [lam_0, lam_1, 0], l_b = R_base l (the base frame's placement on
+  // the root) and mu_b = R0 l_b,
+  //     lam_arm . v_arm = (mu_b + lam_2 e_z) . v_ee - mu_b . v_basept - l_b . (w1 x rel0)
+  // where v_ee is the arm frame's world velocity, v_basept the base point's (linear in v_base with
+  // constant coefficients: no curvature) and rel0 the arm frame's position relative to the base
+  // point in root axes, which reads the arm joints only.  So the curvature is that of
+  //     c_J . (v_J,lin - p x w_J)  -  sum_k pl_k . m_(k-1)  -  p . m_J
+  // with c = R_chain^T (l_b + lam_2 R0^T e_z) and m = R_chain^T (l_b x w1) carried joint by joint
+  // (pl_k the joint placements): one short sweep over the arm chain, for the pairs on the base or it.
   const int ra = O.arm.valid ? block_row(O, type, PL_RB_ARM, -1) : -1;
   if (ra >= 0) {
     int arm_ch = -1;
     for (int ch = 0; ch < M.nchains; ++ch)
       if (O.arm.joint >= M.chain_first[ch] && O.arm.joint < M.chain_first[ch] + M.chain_len[ch]) arm_ch = ch;
-    if (only_ch < 0 || only_ch == arm_ch) {
-      HDual kst[PL_KIN_STORE];
-      pl::NodeKin<HDual> kin;
-      kin.store = kst;
-      kin.stride = 1;
-      const VecIn<HDual> u{x + ndx, nullptr, 0.0, j - ndx, k - ndx};
-      pl::tree_pass<HDual>(M, O, qb, qrev, vel, u, pl::sub_in(u, O.na), false, true, kin, nullptr, std::false_type{},
-                           arm_ch);
-      for (int q = 0; q < 3; ++q) acc = fma(lam[ra + q], kin.arm_vel[q].c, acc);
+    if (arm_ch >= 0 && (only_ch < 0 || only_ch == arm_ch)) {
+      const double l3[3] = {lam[ra], lam[ra + 1], 0.0};
+      double lb[3];
+      pl::matvec(O.base.R, l3, lb);
+      HDual cm[3], mm[3], pv[6], psi(0.0);
+      {
+        HDual R0[9];
+        pl::quat_to_R(qb + 3, R0);
+        for (int q = 0; q < 3; ++q) cm[q] = lb[q] + lam[ra + 2] * R0[6 + q];  // R0^T e_z = row 3 of R0
+      }
+      for (int q = 0; q < 6; ++q) pv[q] = vel[q];
+      crossd(lb, pv + 3, mm);
+      const int first = M.chain_first[arm_ch];
+      for (int jt = first; jt <= O.arm.joint; ++jt) {
+        HDual s, c, t3[3], vj[6];
+        sincos_s(qrev(M.idx_q[jt]), &s, &c);
+        const double* pj = M.jp[jt];
+        psi -= pj[0] * mm[0] + pj[1] * mm[1] + pj[2] * mm[2];
+        rot_t(M, jt, s, c, mm, t3);
+        for (int q = 0; q < 3; ++q) mm[q] = t3[q];
+        rot_t(M, jt, s, c, cm, t3);
+        for (int q = 0; q < 3; ++q) cm[q] = t3[q];
+        act_inv_j(M, jt, s, c, pv, vj);
+        const HDual qd = vel[M.idx_v[jt]];
+        const double* ax = M.axis[jt];
+        for (int q = 0; q < 3; ++q) { pv[q] = vj[q]; pv[3 + q] = vj[3 + q] + ax[q] * qd; }
+      }
+      const double* pf = O.arm.p;
+      HDual pxw[3];
+      crossd(pf, pv + 3, pxw);
+      psi -= pf[0] * mm[0] + pf[1] * mm[1] + pf[2] * mm[2];
+      for (int q = 0; q < 3; ++q) psi += (pv[q] - pxw[q]) * cm[q];
+      acc += psi.c;
     }
   }
   *H = acc;
