@@ -134,6 +134,7 @@ __global__ __launch_bounds__(64) void k_lag_hess_lin(PlDev d, int B, int n, int 
 // foot-velocity rows, the arm-velocity rows; every other row is linear in dx, rows.h node_rows), so
 // the pair's curvature is that of
 //     phi = lambda_tau^T tau(q, v, a, f) + sum_e mu_e . v_foot,e(q, v) + lambda_arm^T v_arm(q, v)
+// (the last term in k_lag_hess_arm, launched after this kernel)
 // (mu_e: the foot-velocity rows' multipliers times their coefficients, world axes).  By virtual work
 // the first two terms are one forward sweep with no backward accumulation:
 //     lambda_tau^T tau = sum_bodies L_b . f_b,   L_b = X_b,parent L_parent + S_b lambda_b   (L_root = lambda_base)
@@ -529,6 +530,37 @@ __global__ __launch_bounds__(64) void k_lag_hess_tree(PlDev d, int B, int n, int
     }
   }
   double acc = phi.c;
+  *H = acc;
+}
+
+
+// The arm rows of the (dq, dq) / (dq, dv) pairs, added to k_lag_hess_tree<false>'s entries (a
+// kernel of their own: inside the sweep they pushed it past the register file).  Same pair list
+// and lane mapping; the pairs on another chain exit at once.
+__global__ __launch_bounds__(64) void k_lag_hess_arm(PlDev d, int B, int n, int m, int np, long long hl_stride) {
+  const int qa = blockIdx.y * 64 + threadIdx.x;
+  if (qa >= d.ip_act[B]) return;
+  const int b = d.ip_act[qa];
+  const PlOcpConst& O = *d.oc;
+  const PlModel& M = *d.model;
+  const int2 w = d.htr[blockIdx.x];
+  const int wx = __builtin_amdgcn_readfirstlane(w.x);
+  const int i = wx & 0xffff, only_ch = (wx >> 16) - 1;
+  const int jk = __builtin_amdgcn_readfirstlane(w.y);
+  const int j = jk & 0xffff, k = jk >> 16;
+  if (j < 3) return;  // (k_lag_hess_tree wrote 0)
+  const int type = pl::node_type(O, i);
+  const PlNode nd = d.nodes[i];
+  const double* x = d.x + (size_t)b * n + nd.x_off;
+  const double* p = d.p + (size_t)b * np;
+  const double* lam = d.ip_lam + (size_t)b * m + nd.row_off;
+  const double* xi = p + O.P.x_init;
+  const VecIn<HDual> dx{x, nullptr, 0.0, j, k};
+  HDual qb[7];
+  base_pose(xi, dx, qb);
+  const pl::RevQ<HDual, VecIn<HDual>> qrev{xi, dx};
+  const pl::VelAcc<HDual, VecIn<HDual>> vel{xi + O.nq, pl::sub_in(dx, O.nv)};
+  double acc = 0.0;
   // ---- the arm rows (Dynamics.get_frame_velocity relative to the base, dynamics/dynamics.py:86-113;
   // rbd.h tree_pass): with l = [lam_0, lam_1, 0], l_b = R_base l (the base frame's placement on
   // the root) and mu_b = R0 l_b,
@@ -579,7 +611,7 @@ __global__ __launch_bounds__(64) void k_lag_hess_tree(PlDev d, int B, int n, int
       acc += psi.c;
     }
   }
-  *H = acc;
+  if (acc != 0.0) d.Hlag[(size_t)b * hl_stride + d.hoff[i] + k * (k + 1) / 2 + j] += acc;
 }
 
 // whole_body_rnea / whole_body_acc, the (f, f) pairs: of the rows only the friction cones
@@ -658,6 +690,9 @@ void launch_lag_hess(PlOcpHandle* h) {
   if (h->htr_len > 0)
     hipLaunchKernelGGL(k_lag_hess_tree<false>, dim3(h->htr_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B,
                        h->n, h->m, h->np, h->hl_stride);
+  if (h->htr_len > 0 && h->oc.arm.valid)
+    hipLaunchKernelGGL(k_lag_hess_arm, dim3(h->htr_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,
+                       h->m, h->np, h->hl_stride);
   if (h->htrf_len > 0)
     hipLaunchKernelGGL(k_lag_hess_tree<true>, dim3(h->htrf_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B,
                        h->n, h->m, h->np, h->hl_stride);
