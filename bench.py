@@ -419,6 +419,11 @@ def main():
                          "traffic_source": (f"profiles/traffic/admm_traffic.json (k_admm src {tj['src_sha']})"
                                             if tj else None)},
         }
+        from pinoloco import _lib as plib
+        from pinoloco import build as pbuild
+        # provenance: the source hash compiled into the loaded library (pl_build_info) and
+        # whether it is this tree's
+        out["build"] = {"lib_src_sha256": plib.build_sha(), "tree_matches": plib.build_sha() == pbuild.source_sha()}
         if host_io is not None:
             out["host_io"] = host_io
         if base is not None:

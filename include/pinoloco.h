@@ -104,7 +104,8 @@ typedef struct {
   /* 0 in production.  Bits of PL_PATH_*: the paths earlier builds used, kept as the references
      the regression tests compare the current kernels with (tests/test_r04_paths.py,
      tests/test_qp_kernels.py, tests/test_graph_gpu.py), and the phase-timing instrumentation.
-     No environment variable changes a kernel path; pl_ocp_sizes reports this field. */
+     No environment variable changes a kernel path; pl_ocp_sizes reports this field.
+     Callers must zero-initialise the struct: pl_ocp_create rejects bits outside PL_PATH_ALL. */
   unsigned debug_paths;
 } pl_ocp_desc;
 
@@ -116,6 +117,8 @@ typedef struct {
 #define PL_PATH_RUIZ_PER_PASS   32u  /* Ruiz equilibration as per-pass kernels (not k_ruiz_fused) */
 #define PL_PATH_NO_MPC_GRAPH    64u  /* pl_mpc_step launches eagerly (no HIP graph) */
 #define PL_PATH_ADMM_TIMING     128u /* s_memtime phase timing in the sweep / factor kernels (pl_debug_get "admm_t") */
+#define PL_PATH_IP_REFINE_GATHER 256u /* k_ip_refine's H_i dx by the per-column global gather (the nw > 192 path) */
+#define PL_PATH_ALL             511u /* pl_ocp_create rejects any other bit: callers zero the struct */
 
 typedef struct {
   int status;                  /* OSQP status code (1 solved, 2 inaccurate, -2 max iter, ...) */
@@ -132,6 +135,9 @@ typedef struct {
 
 const char* pl_last_error(void);
 int pl_version(void);
+/* "pl_src_sha256=<hex> arch=gfx950": the sha256 of the csrc/ and include/ sources this
+   library was built from (pinoloco/build.py source_sha). */
+const char* pl_build_info(void);
 
 int pl_model_create(const pl_model_desc* desc, pl_model** out);
 void pl_model_destroy(pl_model* m);
@@ -179,7 +185,8 @@ typedef struct {
                           Hessian makes the reduced systems stiffer: B2G rnea needs ~6 to
                           reach the sparse LU's direction to 1e-9 with the block inverses); a
                           problem stops refining once a correction is below 1e-12 |dx|_inf or
-                          more than half the previous one */
+                          more than 0.9 of the previous one (stagnation); a correction larger
+                          than the previous one is not applied and ends the refinement */
   int hessian;         /* PL_IP_HESS_EXACT: the Lagrangian Hessian of f + lam^T g (CasADi's
                           exact Hessian of the Opti/Fatrop solve, ocp.py:248-263) with the
                           inertia correction; PL_IP_HESS_GN: the objective's diagonal only */
@@ -190,6 +197,9 @@ typedef struct {
   int status, iter, ls_trials, nfilter;
   double err, mu, alpha, alpha_z, f, viol_max;
   double alphas[32];   /* accepted step of each iteration (0: failed line search) */
+  int ref_solves;      /* linear solves of the Newton systems of this solve (first solve + the
+                          refinement corrections applied), summed over its iterations */
+  int pad;
 } pl_ip_stats;
 int pl_ocp_set_solver(pl_ocp* o, int solver);
 int pl_ocp_set_ip_settings(pl_ocp* o, const pl_ip_settings* s);

@@ -12,6 +12,7 @@ Only tests/, bench.py's cpu_baseline leg and __graft_entry__ use this module.
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
 import os
 import subprocess
 
@@ -36,8 +37,21 @@ def _inputs():
     return [SRC, os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in hdrs]
 
 
+def source_sha():
+    """sha256 of the baseline's inputs (the C++ source, this driver, the shared row headers) and
+    flags; the library is rebuilt whenever its stamp file holds another hash (not by mtime)."""
+    h = hashlib.sha256(" ".join(CXXFLAGS).encode())
+    for p in _inputs():
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def build(force=False):
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(p) for p in _inputs()):
+    sha = source_sha()
+    stamp = LIB + ".sha256"
+    if not force and os.path.exists(LIB) and os.path.exists(stamp) and open(stamp).read().strip() == sha:
         return LIB
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     cmd = ["g++"] + CXXFLAGS + ["-I", CSRC, SRC, "-o", LIB + ".tmp"]
@@ -45,6 +59,8 @@ def build(force=False):
     if r.returncode != 0:
         raise RuntimeError(f"CPU baseline build failed:\n{r.stderr[-4000:]}")
     os.replace(LIB + ".tmp", LIB)
+    with open(stamp, "w") as f:
+        f.write(sha + "\n")
     return LIB
 
 

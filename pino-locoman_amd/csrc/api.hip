@@ -22,6 +22,14 @@ void pl_set_error(const char* fmt, ...) {
 extern "C" const char* pl_last_error(void) { return g_err; }
 extern "C" int pl_version(void) { return 1; }
 
+// Build provenance: build.py passes the sha256 of csrc/* + include/*.h (PL_SRC_SHA), so a
+// caller can tell which sources a pushed binary was built from (bench.py prints it,
+// __graft_entry__.smoke() asserts it against the tree).
+#ifndef PL_SRC_SHA
+#define PL_SRC_SHA "unknown"
+#endif
+extern "C" const char* pl_build_info(void) { return "pl_src_sha256=" PL_SRC_SHA " arch=gfx950"; }
+
 // ---------------------------------------------------------------------------
 // model
 extern "C" int pl_model_create(const pl_model_desc* d, pl_model** out) {
@@ -134,7 +142,13 @@ int admm_select(pl_ocp* o, int kind) {
 extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int batch, int device, pl_ocp** out) {
   if (!model || !d || !out || batch <= 0) { pl_set_error("bad arguments"); return -1; }
   if (d->dynamics < 0 || d->dynamics > 4) { pl_set_error("Unknown dynamics type: %d", d->dynamics); return -1; }
+  // nodes >= 2 is also what k_admm's software pipeline relies on (the prefetch / deferred-store
+  // invariant in its header: steps q - 1 and q + 1 never meet at a node both touch)
   if (d->nodes < 2 || d->n_feet != 4) { pl_set_error("need nodes >= 2 and 4 feet"); return -1; }
+  if (d->debug_paths & ~PL_PATH_ALL) {
+    pl_set_error("debug_paths 0x%x has bits outside PL_PATH_* (0x%x): zero the pl_ocp_desc", d->debug_paths, PL_PATH_ALL);
+    return -1;
+  }
   pl_ocp* o = new pl_ocp();
   PlOcpHandle& h = o->h;
   memset(&h, 0, sizeof(h));
@@ -930,6 +944,7 @@ extern "C" int pl_ocp_ip_stats(pl_ocp* o, pl_ip_stats* out) {
     s.f = info[b].f;
     s.viol_max = info[b].viol_max;
     for (int q = 0; q < PL_IP_MAXFILT; ++q) s.alphas[q] = info[b].alphas[q];
+    s.ref_solves = info[b].ref_solves;
   }
   return 0;
 }

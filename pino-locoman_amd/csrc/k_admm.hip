@@ -139,11 +139,23 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   CNode an = (CNode)d.anodes;
   const int Q = 1 + niter * 2 * N;
 
-  // Software pipeline.  Step q issues, in this order: the deferred end-of-step
-  // stores of step q-1, the operands of step q+1 (E, las, LR, LC -- right after
-  // their step-q copies are consumed), then the factor block of step q+1 slot by
-  // slot inside its own mat-vec.  So the only vector-memory wait of a step is at
-  // its start, and it is for data issued a whole step earlier.
+  // Software pipeline.  Step q opens with its one vector-memory wait (vmcnt(0): everything
+  // issued during step q-1, its stores included), then issues, in this order: the row /
+  // column operands of step q+1 (LR, LC -- right after their step-q copies become current),
+  // the deferred end-of-step stores of step q-1, the A staging, then the other step q+1
+  // operands (E, las) and the factor block of step q+1 slot by slot inside its own mat-vec.
+  // So the wait at a step's start is for data issued a whole step earlier.
+  //
+  // Invariant that makes it safe to read step q+1's LR / LC BEFORE step q-1's deferred stores
+  // are issued (requires N >= 2, which pl_ocp_create enforces).  LR / LC are consumed only by
+  // a backward step (rows z, y, rho, l, u and columns x, q of node i1) or TN (columns of node
+  // N).  Step q-1's pending stores are bt_i (forward), or z, y, x of node i and rhs of nodes
+  // i, i + 1 (backward / TN / T0).  The schedule F0 | FWD 1..N-1, TN, BWD N-1..1, T0 moves one
+  // node per step, so a consumed prefetch could meet a pending store only at a turn: at
+  // FWD N-1 -> TN -> BWD N-1 step q-1 is forward and stores only bt, which LR / LC never read;
+  // at BWD 1 -> T0 -> FWD 1 step q+1 is forward and consumes no LR / LC.  (With N = 1,
+  // TN -> T0 -> TN would read x of node N before the first TN's store of it.)  The other
+  // operands of step q+1 (E, las) are issued after the stores, in order.
   Sbuf SR;  // factor slots of the current block; refilled with the next block's as they are consumed
   Early E, En;  // current / next step (the copy at the start of a step is its only vmcnt wait)
   double las[ASR];

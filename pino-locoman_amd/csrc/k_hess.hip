@@ -650,7 +650,7 @@ __global__ __launch_bounds__(64) void k_lag_hess_cone(PlDev d, int B, int m, int
 // d.ip_act, so the waves past the active count exit at once when most problems have
 // terminated (a warm-started MPC step's line-search failures).  Lanes write only their own
 // problem's entries, so the results do not depend on the mapping.
-__global__ __launch_bounds__(256) void k_ip_compact(PlDev d, int B) {
+__global__ __launch_bounds__(256) void k_ip_compact(PlDev d, int B, int count_lanes) {
   __shared__ int s_wave[4], s_base;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_base = 0;
@@ -671,14 +671,16 @@ __global__ __launch_bounds__(256) void k_ip_compact(PlDev d, int B) {
   }
   if (threadIdx.x == 0) {
     d.ip_act[B] = s_base;
-    d.ip_act[B + 1] += (s_base + 63) / 64 * 64;  // lanes of the Hessian waves that will run
+    // lanes of the Hessian waves that will run, for the launches that get a profiling event
+    // slot only (pl_ocp_profile_read_hess averages over those)
+    if (count_lanes) d.ip_act[B + 1] += (s_base + 63) / 64 * 64;
   }
 }
 
 void launch_lag_hess(PlOcpHandle* h) {
   const bool prof = h->profile && h->prof_hn < 16;  // pl_mpc_step collects the slots before every step
   if (prof) hipEventRecord(h->prof_hev[h->prof_hn][0], h->stream);
-  hipLaunchKernelGGL(k_ip_compact, dim3(1), dim3(256), 0, h->stream, h->d, h->B);
+  hipLaunchKernelGGL(k_ip_compact, dim3(1), dim3(256), 0, h->stream, h->d, h->B, prof ? 1 : 0);
   if (h->hlin_len > 0)
     hipLaunchKernelGGL(k_lag_hess_lin, dim3(h->hlin_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,
                        h->m, h->np, h->hl_stride, make_int3(h->hl_rb_base[0], h->hl_rb_base[1], h->hl_rb_base[2]),

@@ -21,6 +21,7 @@
 #include <math.h>
 
 #include "eval_common.h"
+#include "pinoloco.h"  // PL_PATH_* (pl_ocp_desc.debug_paths)
 
 using pl::VecIn;
 
@@ -189,6 +190,7 @@ __global__ __launch_bounds__(256) void k_ip_init(PlDev d, int m, PlIpSettings st
     ip->status = ST_MAX_ITER;
     ip->nfilt = 0;
     ip->trials = 0;
+    ip->ref_solves = 0;
     ip->active = 1;
     for (int q = 0; q < PL_IP_MAXFILT; ++q) ip->alphas[q] = 0.0;
     d.info[b].done = 0;
@@ -397,7 +399,8 @@ __device__ __forceinline__ void ip_wsync() {
 }
 
 __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int N, int n, int m, int nnz, double delta_w, int hlag,
-                                                   long long hl_stride, int4 hnz_off, int tau_nodes, int iref) {
+                                                   long long hl_stride, int4 hnz_off, int tau_nodes, int iref,
+                                                   int gather) {
   const int b = blockIdx.x;
   if (!d.ipinfo[b].active || d.info[b].done) return;  // done: this solve's refinement has converged
   const double* A = d.Araw + (size_t)b * nnz;
@@ -413,28 +416,23 @@ __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int N, int n, int m,
   double* dx = d.ip_dx + (size_t)b * n;
   double* jdx = d.ip_jdx + (size_t)b * m;
   double* t = d.ip_dl + (size_t)b * m;  // lam + dlam (scratch; k_ip_step recomputes dlam)
-  for (int r = threadIdx.x; r < m; r += 256) {
-    const double jr = jdx[r] + za[r];
-    jdx[r] = jr;
-    t[r] = lam[r] + W[r] * (jr + rh[r]);
-    za[r] = 0.0;
-    ya[r] = 0.0;
-  }
-  __syncthreads();
-  double cmax = 0.0, dmax = 0.0;
-  for (int j = threadIdx.x; j < n; j += 256) {
-    const double c = xa[j], dn = dx[j] + c;
-    dx[j] = dn;
-    cmax = fmax(cmax, fabs(c));
-    dmax = fmax(dmax, fabs(dn));
-  }
-  {  // converged: the last correction is below 1e-12 |dx| (IPOPT's refinement stops at a residual
-     // ratio of 1e-10) or no longer shrinks (more than half the one before: the solves have
-     // reached the factor's noise floor); n_refine is the most solves a system gets.  The problem
-     // then skips the remaining refinement solves of this Newton system (info->done, which the
-     // sweep kernels test; k_ip_step clears it), and its correction buffer is zeroed
+  {  // iref = 0: xa is the first solve's direction; iref >= 1: xa is a refinement correction.
+     // A correction larger than the one before it (the refinement diverges: the block inverses'
+     // noise floor) is not applied and ends the refinement.  Otherwise it is applied, and the
+     // refinement has converged once the correction is below 1e-12 |dx| (IPOPT's refinement
+     // stops at a residual ratio of 1e-10) or has stopped contracting (more than 0.9 of the one
+     // before: stagnation; a linearly converging refinement with a rate in (0.5, 0.9) keeps
+     // going up to n_refine solves).  A stopped problem skips the remaining refinement solves of
+     // this Newton system (info->done, which the sweep kernels test; k_ip_step clears it), and
+     // its correction buffer is zeroed.  ref_solves counts the solves applied (k_ip_init resets).
     __shared__ double s_c[256], s_d[256];
-    __shared__ int s_stop;
+    __shared__ int s_stop, s_apply;
+    double cmax = 0.0, dmax = 0.0;
+    for (int j = threadIdx.x; j < n; j += 256) {
+      const double c = xa[j];
+      cmax = fmax(cmax, fabs(c));
+      dmax = fmax(dmax, fabs(dx[j] + c));
+    }
     s_c[threadIdx.x] = cmax;
     s_d[threadIdx.x] = dmax;
     __syncthreads();
@@ -448,12 +446,28 @@ __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int N, int n, int m,
     if (threadIdx.x == 0) {
       PlIpInfo* ip = d.ipinfo + b;
       const double c = s_c[0];
-      s_stop = iref >= 1 && (c <= 1e-12 * s_d[0] || (iref >= 2 && c > 0.5 * ip->ref_last));
-      ip->ref_last = c;
+      const bool grew = iref >= 2 && !(c <= ip->ref_last);
+      s_apply = !grew;
+      s_stop = grew || (iref >= 1 && (c <= 1e-12 * s_d[0] || (iref >= 2 && c > 0.9 * ip->ref_last)));
+      if (!grew) {
+        ip->ref_last = c;
+        ip->ref_solves += 1;
+      }
       if (s_stop) d.info[b].done = 1;
     }
     __syncthreads();
-    if (s_stop) {
+    const bool apply = s_apply, stop = s_stop;
+    for (int r = threadIdx.x; r < m; r += 256) {  // J dx follows dx (za = J xa of the last sweep)
+      const double jr = apply ? jdx[r] + za[r] : jdx[r];
+      jdx[r] = jr;
+      t[r] = lam[r] + W[r] * (jr + rh[r]);
+      za[r] = 0.0;
+      ya[r] = 0.0;
+    }
+    if (apply)
+      for (int j = threadIdx.x; j < n; j += 256) dx[j] += xa[j];
+    __syncthreads();
+    if (stop) {
       for (int j = threadIdx.x; j < n; j += 256) xa[j] = 0.0;
       return;
     }
@@ -467,7 +481,8 @@ __global__ __launch_bounds__(256) void k_ip_refine(PlDev d, int N, int n, int m,
     for (int i = wv; i <= N; i += 4) {
       const PlNode nd = d.nodes[i];
       const int nw = nd.nw;
-      if (nw > PL_IP_NWMAX) {  // wider blocks than the LDS vectors: the per-column global gather
+      if (nw > PL_IP_NWMAX || gather) {  // wider blocks than the LDS vectors: the per-column global gather
+                                         // (gather: PL_PATH_IP_REFINE_GATHER, its regression test)
         const double* Hi = i < N ? Hb + d.hoff[i] : nullptr;
         for (int c = lane; c < nw; c += 64) {
           double acc = 0.0;
@@ -590,12 +605,32 @@ __global__ __launch_bounds__(256) void k_ip_step(PlDev d, int N, int n, int m, i
   const double* grad = d.grad + (size_t)b * n;
   const double mu = ip->mu;
   const double tau = fmax(TAU_MIN, 1.0 - mu);
-  if (threadIdx.x == 0) d.info[b].done = 0;  // k_ip_refine's converged flag (set again below on termination)
-  {  // the last sweep's correction completes the step
+  {  // the last sweep's correction completes the step -- unless the refinement ran all n_refine
+     // solves and this correction grew (k_ip_refine's rule); a problem whose refinement stopped
+     // has xa = za = 0 here.  info->done (k_ip_refine's stop flag) is cleared for the next system
     const double* xa = d.xa + (size_t)b * n;
     const double* za = d.za + (size_t)b * m;
-    for (int j = threadIdx.x; j < n; j += 256) dx[j] += xa[j];
-    for (int r = threadIdx.x; r < m; r += 256) jdx[r] += za[r];
+    __shared__ int s_app;
+    double cmax = 0.0;
+    for (int j = threadIdx.x; j < n; j += 256) cmax = fmax(cmax, fabs(xa[j]));
+    red[threadIdx.x] = cmax;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (threadIdx.x < w) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + w]);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      const bool pending = !d.info[b].done;
+      const bool app = !(pending && st.n_refine >= 2 && !(red[0] <= ip->ref_last));
+      if (pending && app) ip->ref_solves += 1;
+      s_app = app;
+      d.info[b].done = 0;  // set again below on termination
+    }
+    __syncthreads();
+    if (s_app) {
+      for (int j = threadIdx.x; j < n; j += 256) dx[j] += xa[j];
+      for (int r = threadIdx.x; r < m; r += 256) jdx[r] += za[r];
+    }
     __syncthreads();
   }
   // v: 0 alpha_max, 1 alpha_z, 2 theta, 3 barrier sum, 4 dphi, 5 non-finite
@@ -822,7 +857,8 @@ static void ip_factor(PlOcpHandle* h) {
 static void ip_refine(PlOcpHandle* h, const PlIpSettings& st, int iref) {
   hipLaunchKernelGGL(k_ip_refine, dim3(h->B), dim3(256), 0, h->stream, h->d, h->N, h->n, h->m, h->nnz, st.delta_w,
                      h->ip_hess == PL_IP_HESS_EXACT ? 1 : 0, h->hl_stride,
-                     make_int4(h->hnz_off[0], h->hnz_off[1], h->hnz_off[2], h->hnz_off[3]), h->oc.tau_nodes, iref);
+                     make_int4(h->hnz_off[0], h->hnz_off[1], h->hnz_off[2], h->hnz_off[3]), h->oc.tau_nodes, iref,
+                     (h->debug_paths & PL_PATH_IP_REFINE_GATHER) ? 1 : 0);
 }
 
 // One interior-point solve of every problem from d.x (the warm start), enqueued on the

@@ -143,7 +143,7 @@ struct PlIpSettings {
 };
 struct PlIpInfo {
   double mu, theta_max, theta_min, err, f, alpha, alpha_z, viol_max;
-  int iter, status, nfilt, trials, active, pad;
+  int iter, status, nfilt, trials, active, ref_solves;  // ref_solves: linear solves applied (k_ip_refine)
   double ref_last;                 // |correction|_inf of the last refinement solve (k_ip_refine)
   double filt[2 * PL_IP_MAXFILT];  // (theta, phi) pairs
   double alphas[PL_IP_MAXFILT];    // accepted step of each iteration

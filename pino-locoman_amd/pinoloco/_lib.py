@@ -41,7 +41,7 @@ class OcpDesc(C.Structure):
 # pl_ocp_desc.debug_paths bits (include/pinoloco.h PL_PATH_*): the earlier builds' paths the
 # regression tests compare with, and the phase-timing instrumentation; 0 in production
 PATHS = {"jac_dual_all": 1, "jac_const_every": 2, "hess_full_tree": 4, "hess_dual_all": 8, "fchain_list": 16,
-         "ruiz_per_pass": 32, "no_mpc_graph": 64, "admm_timing": 128}
+         "ruiz_per_pass": 32, "no_mpc_graph": 64, "admm_timing": 128, "ip_refine_gather": 256}
 
 
 class Stats(C.Structure):
@@ -59,12 +59,14 @@ class IpSettings(C.Structure):
 class IpStats(C.Structure):
     _fields_ = [("status", C.c_int), ("iter", C.c_int), ("ls_trials", C.c_int), ("nfilter", C.c_int),
                 ("err", C.c_double), ("mu", C.c_double), ("alpha", C.c_double), ("alpha_z", C.c_double),
-                ("f", C.c_double), ("viol_max", C.c_double), ("alphas", C.c_double * 32)]
+                ("f", C.c_double), ("viol_max", C.c_double), ("alphas", C.c_double * 32),
+                ("ref_solves", C.c_int), ("pad", C.c_int)]
 
 
 EXPORTS = {
     "pl_last_error": (C.c_char_p, []),
     "pl_version": (C.c_int, []),
+    "pl_build_info": (C.c_char_p, []),
     "pl_model_create": (C.c_int, [C.POINTER(ModelDesc), C.POINTER(C.c_void_p)]),
     "pl_model_destroy": (None, [C.c_void_p]),
     "pl_ocp_create": (C.c_int, [C.c_void_p, C.POINTER(OcpDesc), C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
@@ -141,6 +143,12 @@ def lib():
         fn.argtypes = args
     _lib = L
     return L
+
+
+def build_sha() -> str:
+    """The sha256 of the sources the loaded library was built from (pl_build_info)."""
+    info = lib().pl_build_info().decode()
+    return info.split("pl_src_sha256=")[1].split()[0]
 
 
 def check(rc):

@@ -6,6 +6,7 @@ repository snapshot to the GPU box (``pino-locoman_amd/pinoloco/libpinoloco.so``
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -43,14 +44,45 @@ for _src in filter(None, os.environ.get("PL_ILP_SOURCES", "").split(",")):
     SOURCE_FLAGS[_src] = _ILP
 
 
-def _newest_input():
-    paths = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [
-        os.path.join(CSRC, "..", "..", "include", "pinoloco.h"), os.path.abspath(__file__)]
-    return max(os.path.getmtime(p) for p in paths if os.path.exists(p))
+INCLUDE = os.path.normpath(os.path.join(CSRC, "..", "..", "include"))
+
+
+def source_sha() -> str:
+    """sha256 over the library's sources: every file of csrc/ and include/ (name and bytes, in
+    sorted order) plus this build script.  It is compiled into the library
+    (``pl_build_info``), and ``build()`` rebuilds whenever the library on disk carries another
+    hash -- file times are not trusted (a pushed tree keeps the builder's mtimes)."""
+    h = hashlib.sha256()
+    files = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC))]
+    files += [os.path.join(INCLUDE, f) for f in sorted(os.listdir(INCLUDE)) if f.endswith(".h")]
+    files.append(os.path.abspath(__file__))
+    for path in files:
+        if not os.path.isfile(path):
+            continue
+        h.update(os.path.relpath(path, os.path.join(CSRC, "..", "..")).encode())
+        h.update(b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    h.update(" ".join(_flags()).encode())
+    return h.hexdigest()
+
+
+def embedded_sha(path: str = LIB):
+    """The source hash compiled into a built library (its pl_build_info string), or None."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        data = f.read()
+    k = data.find(b"pl_src_sha256=")
+    if k < 0:
+        return None
+    return data[k + 14:k + 14 + 64].decode("ascii", "replace")
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest_input():
+    sha = source_sha()
+    if not force and embedded_sha() == sha:
         return LIB
     hipcc = _hipcc()
     objdir = os.path.join(HERE, "_build")
@@ -59,6 +91,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
     def compile_one(src):
         obj = os.path.join(objdir, src.replace(".hip", ".o"))
         cmd = [hipcc] + _flags() + SOURCE_FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if src == "api.hip":
+            cmd.append(f'-DPL_SRC_SHA="{sha}"')
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
@@ -73,7 +107,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
         raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
     os.replace(tmp, LIB)
     if verbose:
-        print(f"[pinoloco] built {LIB}", file=sys.stderr)
+        print(f"[pinoloco] built {LIB} (sources sha256 {sha[:16]})", file=sys.stderr)
     return LIB
 
 

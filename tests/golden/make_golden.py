@@ -508,8 +508,67 @@ def ip_warm_fixture(name, dyn, gidx):
     print(name, "status", rec["status"], "iter", rec["iter"], flush=True)
 
 
+# Closed loops over every MPC step the benchmark runs (bench.py --warmup 5 --steps 20: steps
+# 0-24) for problems of the benchmark batch (build_batch(..., 0) = ("syn", gidx)): per step the
+# gait at t0 + k dt_min, x_init, the OCP warm start, one SQP iteration, x <- integrate(x, DX[1])
+# (run_mpc.py:127-143).  tests/test_gpu.py checks these problems inside the B = 1024 / 256 batch.
+LOOP_CONFIGS = [
+    ("loop_b2g_rnea_n50", "b2g", "whole_body_rnea", 50, [0, 1, 2, 3], 25),
+    ("loop_b2g_acc_n50", "b2g", "whole_body_acc", 50, [0, 1, 2, 3], 25),
+    ("loop_b2_aba_n40", "b2", "whole_body_aba", 40, [0, 1, 2, 3], 25),
+]
+
+
+def _loop_one(args):
+    rname, dyn, N, gidx, steps = args
+    R = robots.ROBOTS[rname]()
+    R.set_gait_sequence("trot", 0.8)
+    lay = Layout(R, dyn, N)
+    o = OracleOCP(R, dyn, N)
+    P0, X0, XS0, t0 = make_problem(R, lay, dyn, N, ("syn", gidx))
+    xs, x = XS0.copy(), X0.copy()
+    states, u0s, lst = [], [], []
+    for k in range(steps):
+        p = P0.copy()
+        contact, swing = R.gait_sequence.get_gait_schedule(t0 + k * DT_MIN, horizon_dts(DT_MIN, DT_MAX, N), N)
+        vals = {"x_init": xs, "contact_schedule": contact, "swing_schedule": swing}
+        for key in vals:
+            o_, s_ = lay.poff[key]
+            p[o_:o_ + s_] = lay.pack(vals)[o_:o_ + s_]
+        if k == 0:
+            o.init_solver(x, p)
+        else:
+            x = o.warm_start(x, p)
+        x, _, st = o.sqp_step(x, p)
+        DX, U = o.split(x)
+        xs = o.integrate_state(xs, DX[1])
+        states.append(xs)
+        u0s.append(U[0])
+        lst.append([st["status"], st["iter"], st["branch"], st["trials"]])
+    print(f"  {dyn} syn {gidx}: status {[s[0] for s in lst]}", flush=True)
+    return dict(P=P0, X=X0, XS=XS0, T0=t0, states=np.array(states), u0=np.array(u0s), stats=np.array(lst))
+
+
+def loop_fixture(name, rname, dyn, N, gidx, steps):
+    from concurrent.futures import ProcessPoolExecutor
+    workers = min(len(gidx), int(os.environ.get("GOLDEN_WORKERS", "4")))
+    with ProcessPoolExecutor(workers) as ex:
+        res = list(ex.map(_loop_one, [(rname, dyn, N, g, steps) for g in gidx]))
+    rec = {"gidx": np.array(gidx), "gait": np.array("trot")}
+    for key, out in (("P", "P"), ("X", "X"), ("XS", "XS"), ("T0", "T0"), ("states", "loop_states"),
+                     ("u0", "loop_u0"), ("stats", "loop_stats")):
+        rec[out] = np.array([r[key] for r in res])
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **rec)
+    print(name, "statuses", sorted(set(rec["loop_stats"][:, :, 0].ravel().tolist())), flush=True)
+
+
 def main():
     only = sys.argv[1:]
+    for cfg in LOOP_CONFIGS:
+        if cfg[0] in only:
+            loop_fixture(*cfg)
+    if only and all(o.startswith("loop_") for o in only):
+        return
     for cfg in IP_WARM_CONFIGS:
         if cfg[0] in only:
             ip_warm_fixture(*cfg)

@@ -53,7 +53,8 @@ def test_struct_layouts_match_header(tmp_path):
     src = tmp_path / "sz.c"
     fields = {"pl_stats": (_lib.Stats, ["f", "ls_alpha", "viol_max"]),
               "pl_ocp_desc": (_lib.OcpDesc, ["gait_period", "rho", "mu", "foot_frames", "max_iter"]),
-              "pl_model_desc": (_lib.ModelDesc, ["nframes", "frame_p", "gravity"])}
+              "pl_model_desc": (_lib.ModelDesc, ["nframes", "frame_p", "gravity"]),
+              "pl_ip_stats": (_lib.IpStats, ["err", "alphas", "ref_solves"])}
     body = "".join(f'printf("{t} %zu\\n", sizeof({t}));' + "".join(
         f'printf("{t}.{f} %zu\\n", offsetof({t}, {f}));' for f in fl) for t, (_, fl) in fields.items())
     src.write_text(f'#include <stdio.h>\n#include <stddef.h>\n#include "pinoloco.h"\nint main(void){{{body}return 0;}}\n')
@@ -122,6 +123,31 @@ def test_host_handle_rnea_include_acc_false(rname, N):
     nt = bo.node_table()
     dv2 = set(range(nt[2, 2] + R.nv, nt[2, 2] + 2 * R.nv))
     assert any(c in dv2 for r, c in big if nt[1, 3] <= r < nt[1, 3] + nt[1, 4])
+    bo.close()
+
+
+def test_build_info_matches_tree():
+    """pl_build_info carries the sha256 of the sources the library was built from, and build()
+    rebuilds by that hash (not by file times): the library under test is this tree's."""
+    from pinoloco import _lib
+    from pinoloco import build as _build
+    info = _lib.lib().pl_build_info().decode()
+    assert info.startswith("pl_src_sha256=") and "arch=gfx950" in info
+    assert _lib.build_sha() == _build.source_sha() == _build.embedded_sha()
+
+
+def test_debug_paths_outside_mask_rejected(monkeypatch):
+    """pl_ocp_create rejects debug_paths bits outside PL_PATH_ALL (a caller that does not zero
+    the pl_ocp_desc gets an error, not a silently different kernel path)."""
+    from pinoloco import _lib
+    from pinoloco.ocp import BatchedOCP
+    R = make_robot("go2")
+    monkeypatch.setitem(_lib.PATHS, "undefined_bit", 1 << 20)
+    with pytest.raises(_lib.PinolocoError, match="debug_paths"):
+        BatchedOCP(R, "whole_body_rnea", 10, batch=1, device=-1, debug_paths=("undefined_bit",))
+    bo = BatchedOCP(R, "whole_body_rnea", 10, batch=1, device=-1, debug_paths=tuple(k for k in _lib.PATHS
+                                                                                   if k != "undefined_bit"))
+    assert bo.sizes()["debug_paths"] == 511
     bo.close()
 
 

@@ -234,6 +234,53 @@ def test_device_mpc_loop_inside_benchmark_batch(name, rname, dyn, N, B):
     bo.close()
 
 
+# Every MPC step the benchmark runs (bench.py --warmup 5 --steps 20: steps 0-24), for problems
+# of the benchmark batch (tests/golden/make_golden.py LOOP_CONFIGS), SURVEY 8c's closed-loop bar.
+LOOP_BENCH = [("loop_b2g_rnea_n50", "b2g", "whole_body_rnea", 50, 1024),
+              ("loop_b2g_acc_n50", "b2g", "whole_body_acc", 50, 1024),
+              ("loop_b2_aba_n40", "b2", "whole_body_aba", 40, 256)]
+
+
+@pytest.mark.parametrize("name,rname,dyn,N,B", LOOP_BENCH)
+def test_device_mpc_loop_over_bench_steps_inside_batch(name, rname, dyn, N, B):
+    """bench.py's loop (the BASELINE config's batch, AUTO's ADMM kernel -- k_admm at 1024,
+    k_admm_rc at 256 -- pl_mpc_step with the HIP-graph replay) for all the steps the benchmark
+    times and warms up: each fixture problem of the batch follows the oracle's closed loop
+    (run_mpc.py:127-143) with states <= 1e-7 and every step's solver outcome (OSQP status, ADMM
+    iterations, line-search branch, trials) exact."""
+    from pinoloco.ocp import BatchedOCP
+    from pinoloco.synthetic import build_batch
+    G = golden(f"{name}.npz")
+    steps = G["loop_states"].shape[1]
+    assert steps >= 25 and len(G["gidx"]) >= 4
+    R = make_robot(rname)
+    lay, P, X, XS, T0 = build_batch(R, dyn, N, B, 0)
+    for j, g in enumerate(G["gidx"]):
+        assert np.array_equal(P[g], G["P"][j]) and np.array_equal(X[g], G["X"][j])
+        assert np.array_equal(XS[g], G["XS"][j]) and T0[g] == G["T0"][j]
+    bo = BatchedOCP(R, dyn, N, batch=B, device=0, gait_type="trot", gait_period=0.8)
+    assert bo.admm_kernel() == ("sweep" if B >= 1024 else "chain")
+    bo.set_params(P)
+    bo.set_x(X)
+    bo.init_solver()
+    bo.mpc_setup(XS, T0)
+    worst = 0.0
+    for k in range(steps):
+        bo.mpc_step(k)
+        S = bo.mpc_state()
+        st = bo.mpc_stats()
+        for j, g in enumerate(G["gidx"]):
+            err = _rel(S[g], G["loop_states"][j, k])
+            worst = max(worst, err)
+            assert err < 1e-7, (g, k, err)
+            assert [st["status"][g], st["admm_iters"][g], st["ls_branch"][g], st["ls_trials"][g]] == \
+                G["loop_stats"][j, k].tolist(), (g, k)
+    assert np.all(np.isfinite(bo.mpc_state()))
+    assert bo.mpc_graph_info()["replays"] >= steps - 2  # the timed shape: captured step replayed
+    print(f"{name}: {steps} steps x {len(G['gidx'])} problems, worst state error {worst:.2e}")
+    bo.close()
+
+
 def test_make_ocp_surface_matches_oracle():
     """The reference's own driver shape (run_mpc.py:115-143, OSQP branch) through
     make_ocp / OCP on the GPU, against the oracle's closed loop."""

