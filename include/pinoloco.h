@@ -222,6 +222,13 @@ int pl_debug_ip_direction(pl_ocp* o, const double* s, const double* lam, const d
  * ocp_whole_body_rnea.py:326-366; retract_steps = num_steps of compile_solution). */
 int pl_casadi_bind(pl_ocp* o, int retract_steps);
 void pl_casadi_unbind(void);
+/* Bind the batch-1 interior-point handle (pl_ocp_set_solver(o, PL_SOLVER_IP)) whose Fatrop
+ * solve the exported compiled_solver runs (include/pinoloco_casadi.h; replaces the generated
+ * opti.to_function("compiled_solver", ...) of ocp_whole_body_rnea.py:237-258 / ocp.py:324-342,
+ * loaded by run_mpc.py:51-53).  warm_start = the compile_solver argument (x_warm_start is then
+ * an input); x_initial [n]: the initial guess baked in without it (may be NULL with it).  The
+ * parameters the function does not take keep the handle's values at bind time. */
+int pl_casadi_bind_compiled(pl_ocp* o, int warm_start, const double* x_initial);
 /* Evaluate sqp_data at the current x: any output may be NULL. */
 int pl_eval_sqp_data(pl_ocp* o, double* grad, double* Jvals, double* g, double* lbg, double* ubg);
 /* f_data value at the current x. */
@@ -252,6 +259,13 @@ int pl_mpc_download(pl_ocp* o, double* host_dst);
 /* MPC-step HIP graph state: out[0] captures, out[1] graph launches, out[2] = 1 when the
  * step fell back to eager launches (a capture or replay failed, or PL_MPC_GRAPH=0). */
 int pl_mpc_graph_info(const pl_ocp* o, long long* out);
+/* Multipliers across pl_mpc_step with the interior-point solver.  carry = 0 (default): the
+ * reference's default driver, solver "fatrop" with compile_solver = True (run_mpc.py:34-37,
+ * 50-111): the compiled solver function takes the primal warm start only
+ * (ocp_whole_body_rnea.py:239-257), so each solve starts from cold multipliers.  carry = 1: the
+ * Opti branch (compile_solver = False, run_mpc.py:115-143 through OCP.solve): warm_start() passes
+ * the previous solve's lam_g (ocp_whole_body_rnea.py:234-235, ocp.py:373). */
+int pl_mpc_set_ip_lam(pl_ocp* o, int carry);
 int pl_ocp_sync(pl_ocp* o);
 
 /* Host-side state maps, x = [q, v], dx = [dq, dv]

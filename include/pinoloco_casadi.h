@@ -8,6 +8,8 @@
  *   g_data(x, p) -> (g, lbg, ubg)                     optimization/ocp.py:290
  *   retract_solution(sol_x, x_init) -> (q, v, a, forces, tau)
  *                                                     optimization/ocp_whole_body_rnea.py:326-366
+ *   compiled_solver(params..., [x_warm_start], [tau_prev, W_diag]) -> x
+ *                                                     ocp_whole_body_rnea.py:237-258, run_mpc.py:51-53
  *   self.sqp_data = ca.external("sqp_data", "codegen/sqp/libsqp_data_....so")
  *                                                     optimization/ocp.py:299-302, run_mpc.py:53
  * libpinoloco.so exports each NAME with CasADi's generated-code calling convention
@@ -50,6 +52,13 @@ PL_CASADI_DECLARE(f_data)
 PL_CASADI_DECLARE(g_data)
 PL_CASADI_DECLARE(hess_data)
 PL_CASADI_DECLARE(retract_solution)
+/* compiled_solver(x_init, dt_min, dt_max, contact_schedule, swing_schedule, n_contacts,
+ *                 swing_period, swing_height, swing_vel_limits, Q_diag, R_diag, base_vel_des,
+ *                 [ext_force_des], [arm_vel_des], [x_warm_start], [tau_prev, W_diag]) -> x
+ *   the Fatrop branch's generated solver (ocp_whole_body_rnea.py:237-258, ocp.py:324-342),
+ *   loaded with ca.external("compiled_solver", lib) at run_mpc.py:51-53; bound with
+ *   pl_casadi_bind_compiled (include/pinoloco.h).  One interior-point solve on the GPU. */
+PL_CASADI_DECLARE(compiled_solver)
 
 #ifdef __cplusplus
 }

@@ -678,6 +678,9 @@ enum { IP_CONVERGED = 1, IP_MAX_ITER = -1, IP_LS_FAIL = -2, IP_NONFINITE = -3 };
 struct IpSettings {
   double tol, mu_init, bound_push, bound_frac, warm_push, delta_w, delta_c;
   int max_iter, ls_max, n_refine, inertia_cap;
+  int kkt_exact;  // 1: refinement on the unregularised KKT (ip_ref.py kkt_refine="exact"), 0: "regularized"
+  int mpc_lam;    // MPC loop: 1 carries lam_g across steps (the Opti branch), 0 cold multipliers per solve
+                  // (the reference's default compiled-solver driver, run_mpc.py:34-37, 50-111)
 };
 
 struct HEmit {
@@ -1076,10 +1079,6 @@ IpStats ip_solve(const Problem& pr, Work& w, IpWork& iw, const IpSettings& S, co
       ldl_solve(pr.ipk, iw.ldl, iw.sol.data());
       for (int j = 0; j < n; ++j) out_x[j] = iw.sol[pr.iperm_x[j]];
     };
-    for (int r = 0; r < m; ++r) iw.st[r] = iw.W[r] * iw.rhat[r];
-    jt_mul(pr, iw.J.data(), iw.st.data(), iw.rhs.data());
-    for (int j = 0; j < n; ++j) iw.rhs[j] = -iw.rx[j] - iw.rhs[j];
-    kkt_solve(iw.rhs.data(), iw.dx.data());
     // H_L dx for the refinement residual: the KKT's upper-left block (H + dwi + H_L) times dx
     auto hl_mul = [&](const double* v, double* outv) {  // (H + dwi + H_L) v over the stored pairs
       for (int j = 0; j < n; ++j) outv[j] = (H[j] + dwi) * v[j];
@@ -1099,19 +1098,50 @@ IpStats ip_solve(const Problem& pr, Work& w, IpWork& iw, const IpSettings& S, co
       }
     };
     std::vector<double> Hdx(n), corr(n);
-    for (int t = 0; t < S.n_refine; ++t) {
-      j_mul(pr, iw.J.data(), iw.dx.data(), iw.jdx.data());
-      for (int r = 0; r < m; ++r) iw.st[r] = lam[r] + iw.W[r] * (iw.jdx[r] + iw.rhat[r]);
-      jt_mul(pr, iw.J.data(), iw.st.data(), iw.res.data());
-      hl_mul(iw.dx.data(), Hdx.data());
-      for (int j = 0; j < n; ++j) iw.res[j] = -(iw.grad[j] + iw.res[j]) - Hdx[j];
-      kkt_solve(iw.res.data(), corr.data());
-      for (int j = 0; j < n; ++j) iw.dx[j] += corr[j];
+    if (S.kkt_exact) {
+      // iterative refinement on the unregularised KKT [H_K J^T; J -D] [dx; dl] = [-rx; -rhat]
+      // (D = 0 on equality rows, 1/Sigma on the others) with the delta_c-regularised factor
+      // [H_K J^T; J -1/W] as the solver of each correction (oracle/ip_ref.py kkt_refine="exact")
+      std::vector<double> r2(m), ez(m);
+      std::fill(iw.dx.begin(), iw.dx.end(), 0.0);
+      std::fill(iw.dl.begin(), iw.dl.end(), 0.0);
+      std::fill(iw.jdx.begin(), iw.jdx.end(), 0.0);
+      for (int t = 0; t <= S.n_refine; ++t) {
+        for (int r = 0; r < m; ++r) iw.st[r] = lam[r] + iw.dl[r];
+        jt_mul(pr, iw.J.data(), iw.st.data(), iw.res.data());
+        hl_mul(iw.dx.data(), Hdx.data());
+        for (int j = 0; j < n; ++j) iw.res[j] = -(iw.grad[j] + iw.res[j]) - Hdx[j];
+        for (int r = 0; r < m; ++r) {
+          const double sig = (hl[r] ? iw.zl[r] / iw.sl[r] : 0.0) + (hu[r] ? iw.zu[r] / iw.su[r] : 0.0);
+          const double D = eq[r] ? 0.0 : 1.0 / sig;
+          r2[r] = -iw.rhat[r] - iw.jdx[r] + D * iw.dl[r];
+        }
+        for (int j = 0; j < n; ++j) iw.sol[pr.iperm_x[j]] = iw.res[j];
+        for (int r = 0; r < m; ++r) iw.sol[pr.iperm_z[r]] = r2[r];
+        ldl_solve(pr.ipk, iw.ldl, iw.sol.data());
+        for (int j = 0; j < n; ++j) iw.dx[j] += iw.sol[pr.iperm_x[j]];
+        for (int r = 0; r < m; ++r) iw.dl[r] += iw.sol[pr.iperm_z[r]];
+        j_mul(pr, iw.J.data(), iw.dx.data(), iw.jdx.data());
+      }
+    } else {
+      for (int r = 0; r < m; ++r) iw.st[r] = iw.W[r] * iw.rhat[r];
+      jt_mul(pr, iw.J.data(), iw.st.data(), iw.rhs.data());
+      for (int j = 0; j < n; ++j) iw.rhs[j] = -iw.rx[j] - iw.rhs[j];
+      kkt_solve(iw.rhs.data(), iw.dx.data());
+      for (int t = 0; t < S.n_refine; ++t) {
+        j_mul(pr, iw.J.data(), iw.dx.data(), iw.jdx.data());
+        for (int r = 0; r < m; ++r) iw.st[r] = lam[r] + iw.W[r] * (iw.jdx[r] + iw.rhat[r]);
+        jt_mul(pr, iw.J.data(), iw.st.data(), iw.res.data());
+        hl_mul(iw.dx.data(), Hdx.data());
+        for (int j = 0; j < n; ++j) iw.res[j] = -(iw.grad[j] + iw.res[j]) - Hdx[j];
+        kkt_solve(iw.res.data(), corr.data());
+        for (int j = 0; j < n; ++j) iw.dx[j] += corr[j];
+      }
     }
     j_mul(pr, iw.J.data(), iw.dx.data(), iw.jdx.data());
     bool finite = true;
     for (int r = 0; r < m; ++r) {
-      iw.dl[r] = iw.W[r] * (iw.jdx[r] + iw.rhat[r]);
+      if (!S.kkt_exact) iw.dl[r] = iw.W[r] * (iw.jdx[r] + iw.rhat[r]);
       const double sig = (hl[r] ? iw.zl[r] / iw.sl[r] : 0.0) + (hu[r] ? iw.zu[r] / iw.su[r] : 0.0);
       iw.ds[r] = eq[r] ? 0.0 : (iw.bs[r] + iw.dl[r]) / sig;
       iw.dzl[r] = hl[r] ? mu / iw.sl[r] - iw.zl[r] - iw.zl[r] / iw.sl[r] * iw.ds[r] : 0.0;
@@ -1206,7 +1236,8 @@ void run_problem_ip(const Problem& pr, Work& w, IpWork& iw, const IpSettings& S,
         }
       }
     }
-    IpStats s = ip_solve<DYN>(pr, w, iw, S, p.data(), Pd.data(), x.data(), lam.data(), k > 0);
+    if (!S.mpc_lam) std::fill(lam.begin(), lam.end(), 0.0);
+    IpStats s = ip_solve<DYN>(pr, w, iw, S, p.data(), Pd.data(), x.data(), lam.data(), S.mpc_lam && k > 0);
     const double* dx1 = x.data() + pr.x_off[1];
     double qn[PL_MAXQ];
     if (PL_IS_CV(O.dyn)) {
@@ -1233,6 +1264,8 @@ IpSettings ip_settings_from(const double* v) {
   S.tol = v[0]; S.mu_init = v[1]; S.bound_push = v[2]; S.bound_frac = v[3]; S.warm_push = v[4];
   S.delta_w = v[5]; S.delta_c = v[6]; S.max_iter = (int)v[7]; S.ls_max = (int)v[8]; S.n_refine = (int)v[9];
   S.inertia_cap = (int)v[10];
+  S.kkt_exact = (int)v[11];
+  S.mpc_lam = (int)v[12];
   return S;
 }
 
@@ -1456,8 +1489,10 @@ extern "C" int cpu_ip_solve(void* h, const double* p, double* x, double* lam, in
   return 0;
 }
 
-// B problems x `steps` MPC steps with the interior-point solver (lam_g carried across the
-// steps, run_mpc.py:115-143 with the Fatrop branch) on `threads` OpenMP threads.  Returns
+// B problems x `steps` MPC steps with the interior-point solver (settings mpc_lam: lam_g carried
+// across the steps as the Opti branch does, run_mpc.py:115-143, or cold multipliers per solve as
+// the reference's default compiled-solver driver does, run_mpc.py:50-111) on `threads` OpenMP
+// threads.  Returns
 // the wall seconds; xs_out [B][nx], stats [B][steps][2] = (status, iterations).
 extern "C" double cpu_ip_mpc_batch(void* h, int B, const double* P, const double* X, const double* XS,
                                    const double* T0, int steps, int threads, const double* settings, double* xs_out,

@@ -156,7 +156,8 @@ class CpuOCP:
         if s["hessian"] != "exact":
             raise ValueError("the CPU interior point restates the exact-Hessian form only")
         return np.array([s["tol"], s["mu_init"], s["bound_push"], s["bound_frac"], s["warm_start_mult_bound_push"],
-                         s["delta_w"], s["delta_c"], s["max_iter"], s["ls_max"], s["n_refine"], s["inertia_cap"]],
+                         s["delta_w"], s["delta_c"], s["max_iter"], s["ls_max"], s["n_refine"], s["inertia_cap"],
+                         1.0 if s["kkt_refine"] == "exact" else 0.0, 1.0 if s.get("mpc_lam", False) else 0.0],
                         dtype=np.float64)
 
     def hess_pairs(self):
@@ -189,7 +190,9 @@ class CpuOCP:
                             f=float(ef[1]))
 
     def ip_mpc(self, P, X, XS, T0, steps, threads=0, settings=None):
-        """`steps` MPC steps of every problem with the interior point (lam_g carried);
+        """`steps` MPC steps of every problem with the interior point (settings mpc_lam=True:
+        lam_g carried, the Opti branch; default False: cold multipliers per solve, the
+        reference's default compiled-solver driver);
         returns (wall seconds, final states, stats [B][steps][2] = (status, iterations))."""
         B = P.shape[0]
         P, X, XS = (np.ascontiguousarray(a, dtype=np.float64) for a in (P, X, XS))

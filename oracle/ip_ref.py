@@ -69,7 +69,7 @@ import scipy.sparse.linalg as spla
 # ocp.py:254-262 (reference settings) + IPOPT / Fatrop defaults for the rest
 IP_SETTINGS = dict(max_iter=10, tol=1e-3, mu_init=1e-4, bound_push=1e-7, bound_frac=1e-2,
                    warm_start_mult_bound_push=1e-7, delta_w=1e-8, delta_c=1e-4, ls_max=12, n_refine=8,
-                   hessian="exact", inertia_cap=8)
+                   hessian="exact", inertia_cap=8, kkt_refine="regularized")
 KAPPA_EPS, KAPPA_MU, THETA_MU = 10.0, 0.2, 1.5
 TAU_MIN, S_MAX, KAPPA_SIGMA = 0.99, 100.0, 1e10
 GAMMA_THETA, GAMMA_PHI, DELTA, S_THETA, S_PHI, ETA_PHI = 1e-5, 1e-8, 1.0, 1.1, 2.3, 1e-8
@@ -231,11 +231,29 @@ class IPRef:
             K = (Kb + dwi * sp.eye(x.size)).tocsc()
             rhs = -rx - J.T @ (W * rhat)
             lu = spla.splu(K)
-            dx = lu.solve(rhs)
-            for _ in range(st["n_refine"]):  # iterative refinement on the KKT x-row residual
-                res = -(grad + J.T @ (lam + W * (J @ dx + rhat))) - (H + dwi) * dx - Hl @ dx
-                dx = dx + lu.solve(res)
-            dl = W * (J @ dx + rhat)
+            if st["kkt_refine"] == "exact":
+                # delta_c regularises the factor only: iterative refinement on the UNREGULARISED
+                # KKT  [H_K  J^T; J  -D] [dx; dl] = [-rx; -rhat]  (D = 0 on equality rows, 1/Sigma on
+                # the others), each correction solved with the regularised factor
+                #   K ex = r1 + J^T W r2,  el = W (J ex - r2)
+                # The iteration contracts (eigenvalues of delta_c (D + delta_c + J H_K^-1 J^T)^-1 in
+                # [0, 1)), so the refined step tends to the delta_c = 0 Newton step that Fatrop's
+                # Riccati recursion computes on the exact KKT.  The first solve is the first
+                # correction from dx = dl = 0.
+                Dd = np.where(eq, 0.0, 1.0 / sig_safe)
+                dx, dl = np.zeros(x.size), np.zeros(m)
+                for _ in range(st["n_refine"] + 1):
+                    r1 = -(grad + J.T @ (lam + dl)) - (H + dwi) * dx - Hl @ dx
+                    r2 = -rhat - J @ dx + Dd * dl
+                    ex = lu.solve(r1 + J.T @ (W * r2))
+                    dx = dx + ex
+                    dl = dl + W * (J @ ex - r2)
+            else:  # "regularized" (r02-r05): the step of the delta_c-regularised KKT
+                dx = lu.solve(rhs)
+                for _ in range(st["n_refine"]):  # iterative refinement on the reduced x-row residual
+                    res = -(grad + J.T @ (lam + W * (J @ dx + rhat))) - (H + dwi) * dx - Hl @ dx
+                    dx = dx + lu.solve(res)
+                dl = W * (J @ dx + rhat)
             ds = np.where(iq, (bs + dl) / sig_safe, 0.0)
             dzl = np.where(hl, mu / sl - zl - zl / sl * ds, 0.0)
             dzu = np.where(hu, mu / su - zu + zu / su * ds, 0.0)

@@ -1090,6 +1090,12 @@ static int mpc_sqp_graph(pl_ocp* o) {
   return hipGraphLaunch(o->mpc_graph, h->stream) == hipSuccess ? 0 : -1;
 }
 
+extern "C" int pl_mpc_set_ip_lam(pl_ocp* o, int carry) {
+  if (!o || (carry != 0 && carry != 1)) { pl_set_error("pl_mpc_set_ip_lam: carry must be 0 or 1"); return -1; }
+  o->h.ip_mpc_lam = carry;
+  return 0;
+}
+
 // MPC-step graph state (tests): [captures, replays, eager fallback (1: capture or replay
 // failed, or PL_MPC_GRAPH=0)].
 extern "C" int pl_mpc_graph_info(const pl_ocp* o, long long* out) {
@@ -1117,10 +1123,20 @@ extern "C" int pl_mpc_step(pl_ocp* o, int k) {
   }
   if (o->h.solver == PL_SOLVER_IP) {
     enqueue_ip(&o->h);
-    // warm_start() of the next step passes this solve's lam_g back (ocp.py:373, ocp_*.py warm_start)
     PlOcpHandle* h = &o->h;
-    PL_CHECK_HIP(hipMemcpyAsync(h->d.ip_lam0, h->d.ip_lam, (size_t)h->B * h->m * 8, hipMemcpyDeviceToDevice, h->stream));
-    h->ip_lam_warm = 1;
+    if (h->ip_mpc_lam) {
+      // the Opti branch (compile_solver = False): warm_start() of the next step passes this
+      // solve's lam_g back (ocp.py:373, ocp_*.py warm_start)
+      PL_CHECK_HIP(hipMemcpyAsync(h->d.ip_lam0, h->d.ip_lam, (size_t)h->B * h->m * 8, hipMemcpyDeviceToDevice,
+                                  h->stream));
+      h->ip_lam_warm = 1;
+    } else {
+      // the reference's default driver (solver "fatrop", compile_solver = True, run_mpc.py:34-37,
+      // 50-111): the compiled solver takes the primal warm start only (its inputs end with opti.x,
+      // ocp_whole_body_rnea.py:239-257, the lam_g output commented out), so every solve starts
+      // from cold multipliers
+      h->ip_lam_warm = 0;
+    }
     launch_mpc_finish(&o->h);
   } else
     enqueue_mpc_sqp(o);

@@ -14,6 +14,8 @@
 // Every entry point takes one process-wide lock (CasADi may evaluate from several
 // threads, e.g. a threaded map; the bound handle has one stream and one staging
 // buffer), and each evaluation waits on its stream once, after all its copies.
+#include <string>
+
 namespace {
 typedef long long casadi_int;
 struct CasadiState {
@@ -158,9 +160,13 @@ extern "C" void pl_casadi_unbind(void) {
   g_cas.o = nullptr;
 }
 
+void cas_forget_compiled(const pl_ocp* o);
 void cas_forget(const pl_ocp* o) {
-  PL_CAS_LOCK;
-  if (g_cas.o == o) g_cas.o = nullptr;
+  {
+    PL_CAS_LOCK;
+    if (g_cas.o == o) g_cas.o = nullptr;
+  }
+  cas_forget_compiled(o);
 }
 
 // ---- shared boilerplate of every external function
@@ -408,5 +414,154 @@ extern "C" int retract_solution(const double** arg, double** res, casadi_int*, d
       }
     }
   }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// compiled_solver(params..., [x_warm_start], [tau_prev, W_diag]) -> x: the Fatrop branch's generated
+// solver function (opti.to_function("compiled_solver", solver_params, [opti.x]),
+// ocp.py:324-342, ocp_whole_body_rnea.py:237-258), loaded by the reference's hardware driver
+// with ca.external("compiled_solver", "codegen/lib/...") (run_mpc.py:51-53) and called as
+// sol_x = solver_function(*params) (run_mpc.py:100).  Its inputs, in order: x_init, dt_min,
+// dt_max, contact_schedule (n_feet x N), swing_schedule (n_feet x N), n_contacts, swing_period,
+// swing_height, swing_vel_limits, Q_diag, R_diag, base_vel_des, [ext_force_des if the OCP has
+// the external-force frame], [arm_vel_des if it has the arm frame], [opti.x if compiled with
+// warm_start], [tau_prev, W_diag for whole_body_rnea].  One call is one interior-point solve
+// (pl_ocp_set_solver(PL_SOLVER_IP)) of the bound batch-1 handle from COLD multipliers (the
+// generated function has no lam_g input; its output list has lam_g commented out); the
+// parameters it does not list keep the values the handle held at bind time (Opti bakes them in
+// at to_function), and without warm_start x starts from the bound initial guess.  A solve that
+// stops at the iteration cap or in a failed line search returns its last iterate.
+namespace {
+struct CompiledSlot {
+  int off, len;  // parameter-vector offset and length; off = -1: the primal warm start x
+};
+struct CompiledState {
+  pl_ocp* o = nullptr;
+  std::vector<CompiledSlot> slots;
+  std::vector<std::vector<casadi_int>> sp_in;
+  std::vector<casadi_int> sp_out;
+  std::vector<double> p0, x0, p, x;
+  std::vector<std::string> names;
+};
+CompiledState g_cs;
+}  // namespace
+
+extern "C" int pl_casadi_bind_compiled(pl_ocp* o, int warm_start, const double* x_initial) {
+  if (!o) { pl_set_error("null handle"); return -1; }
+  const PlOcpHandle& h = o->h;
+  if (h.B != 1) { pl_set_error("compiled_solver: bind a batch-1 handle (the generated solver is single-problem)"); return -1; }
+  if (h.solver != PL_SOLVER_IP) { pl_set_error("compiled_solver: the handle must use the interior-point solver (PL_SOLVER_IP)"); return -1; }
+  if (!warm_start && !x_initial) { pl_set_error("compiled_solver without warm_start needs the initial guess"); return -1; }
+  PL_CAS_LOCK;
+  CompiledState& c = g_cs;
+  c.o = o;
+  c.slots.clear();
+  c.sp_in.clear();
+  c.names.clear();
+  const PlOcpConst& O = h.oc;
+  auto add = [&](const char* name, int off, int nrow, int ncol) {
+    c.slots.push_back({off, nrow * ncol});
+    c.sp_in.push_back(dense_sp(nrow, ncol));
+    c.names.push_back(name);
+  };
+  add("x_init", O.P.x_init, O.nx, 1);
+  add("dt_min", O.P.dt_min, 1, 1);
+  add("dt_max", O.P.dt_max, 1, 1);
+  add("contact_schedule", O.P.contact, 4, O.N);
+  add("swing_schedule", O.P.swing, 4, O.N);
+  add("n_contacts", O.P.n_contacts, 1, 1);
+  add("swing_period", O.P.swing_period, 1, 1);
+  add("swing_height", O.P.swing_height, 1, 1);
+  add("swing_vel_limits", O.P.swing_vel_limits, 2, 1);
+  add("Q_diag", O.P.Q_diag, O.ndx, 1);
+  add("R_diag", O.P.R_diag, (O.P.base_vel_des - O.P.R_diag), 1);
+  add("base_vel_des", O.P.base_vel_des, 6, 1);
+  if (O.ext.valid) add("ext_force_des", O.P.ext_force_des, 3, 1);
+  if (O.arm.valid) add("arm_vel_des", O.P.arm_vel_des, 3, 1);
+  if (warm_start) add("x", -1, h.n, 1);
+  if (PL_IS_RNEA(O.dyn)) {
+    add("tau_prev", O.P.tau_prev, O.nj, 1);
+    add("W_diag", O.P.W_diag, O.nj, 1);
+  }
+  c.sp_out = dense_sp(h.n, 1);
+  c.p0.assign(o->h_params.begin(), o->h_params.begin() + h.np);
+  c.x0.assign(h.n, 0.0);
+  if (!warm_start) memcpy(c.x0.data(), x_initial, (size_t)h.n * 8);
+  c.p.resize(h.np);
+  c.x.resize(h.n);
+  return 0;
+}
+
+void cas_forget_compiled(const pl_ocp* o) {
+  PL_CAS_LOCK;
+  if (g_cs.o == o) g_cs.o = nullptr;
+}
+
+static int cs_ready() {
+  if (!g_cs.o) {
+    pl_set_error("no OCP bound (pl_casadi_bind_compiled)");
+    return 0;
+  }
+  return 1;
+}
+
+extern "C" int compiled_solver_alloc_mem(void) { return 0; }
+extern "C" int compiled_solver_init_mem(int) { return 0; }
+extern "C" void compiled_solver_free_mem(int) {}
+extern "C" int compiled_solver_checkout(void) { return 0; }
+extern "C" void compiled_solver_release(int) {}
+extern "C" void compiled_solver_incref(void) {}
+extern "C" void compiled_solver_decref(void) {}
+extern "C" casadi_int compiled_solver_n_in(void) {
+  PL_CAS_LOCK;
+  return cs_ready() ? (casadi_int)g_cs.slots.size() : 0;
+}
+extern "C" casadi_int compiled_solver_n_out(void) { return 1; }
+extern "C" double compiled_solver_default_in(casadi_int) { return 0.0; }
+extern "C" int compiled_solver_work(casadi_int* sz_arg, casadi_int* sz_res, casadi_int* sz_iw, casadi_int* sz_w) {
+  PL_CAS_LOCK;
+  if (sz_arg) *sz_arg = cs_ready() ? (casadi_int)g_cs.slots.size() : 0;
+  if (sz_res) *sz_res = 1;
+  if (sz_iw) *sz_iw = 0;
+  if (sz_w) *sz_w = 0;
+  return 0;
+}
+extern "C" const char* compiled_solver_name_in(casadi_int i) {
+  PL_CAS_LOCK;
+  if (!cs_ready() || i < 0 || i >= (casadi_int)g_cs.names.size()) return nullptr;
+  return g_cs.names[i].c_str();
+}
+extern "C" const char* compiled_solver_name_out(casadi_int i) { return i == 0 ? "x" : nullptr; }
+extern "C" const casadi_int* compiled_solver_sparsity_in(casadi_int i) {
+  PL_CAS_LOCK;
+  if (!cs_ready() || i < 0 || i >= (casadi_int)g_cs.sp_in.size()) return nullptr;
+  return g_cs.sp_in[i].data();
+}
+extern "C" const casadi_int* compiled_solver_sparsity_out(casadi_int i) {
+  PL_CAS_LOCK;
+  if (!cs_ready() || i != 0) return nullptr;
+  return g_cs.sp_out.data();
+}
+extern "C" int compiled_solver(const double** arg, double** res, casadi_int*, double*, int) {
+  PL_CAS_LOCK;
+  if (!cs_ready()) return 1;
+  CompiledState& c = g_cs;
+  pl_ocp* o = c.o;
+  c.p = c.p0;
+  c.x = c.x0;
+  for (size_t k = 0; k < c.slots.size(); ++k) {
+    const CompiledSlot& s = c.slots[k];
+    double* dst = s.off < 0 ? c.x.data() : c.p.data() + s.off;
+    if (arg[k]) memcpy(dst, arg[k], (size_t)s.len * 8);
+    else memset(dst, 0, (size_t)s.len * 8);  // CasADi passes null for an all-zero input
+  }
+  // as the reference's generated function: the objective's Hessian diagonal from these
+  // parameters (ocp.py:293-296), x from the warm start, cold multipliers, one solve
+  pl_stats st;
+  if (pl_ocp_set_params(o, c.p.data()) || pl_ocp_init_solver(o) || pl_ocp_set_x(o, c.x.data()) ||
+      pl_ocp_set_lam(o, nullptr) || pl_ocp_solve(o, &st, nullptr))
+    return 1;
+  if (res[0] && pl_ocp_get_x(o, res[0])) return 1;
   return 0;
 }

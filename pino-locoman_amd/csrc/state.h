@@ -285,6 +285,8 @@ struct PlOcpHandle {
   int jlin_len;                     // k_eval_jac_lin work-list entries (0: those columns stay in jlist)
   int solver;                       // PL_SOLVER_OSQP (SQP + OSQP ADMM) or PL_SOLVER_IP (interior point)
   int ip_lam_warm;                  // 1: the next interior-point solve starts from lam = ip_lam0
+  int ip_mpc_lam;                   // pl_mpc_step with the IP solver: 1 carries lam_g to the next step
+                                    // (the Opti branch), 0 cold multipliers (the compiled-solver branch)
   int ip_hess;                      // interior point: PL_IP_HESS_EXACT (Lagrangian) or PL_IP_HESS_GN
   int hl_len;                       // Lagrangian Hessian work list (k_lag_hess)
   int hnz_off[4];                   // d.hnz per node type: [hnz_off[t], hnz_off[t + 1])

@@ -90,6 +90,7 @@ EXPORTS = {
     "pl_debug_ip_direction": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),
     "pl_casadi_bind": (C.c_int, [C.c_void_p, C.c_int]),
     "pl_casadi_unbind": (None, []),
+    "pl_casadi_bind_compiled": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
     "pl_eval_sqp_data": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp]),
     "pl_eval_f": (C.c_int, [C.c_void_p, _dp]),
     "pl_ocp_get_step": (C.c_int, [C.c_void_p, _dp]),
@@ -101,6 +102,7 @@ EXPORTS = {
     "pl_mpc_download": (C.c_int, [C.c_void_p, _dp]),
     "pl_ocp_profile_read_hess": (C.c_int, [C.c_void_p, _dp]),
     "pl_mpc_graph_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong)]),
+    "pl_mpc_set_ip_lam": (C.c_int, [C.c_void_p, C.c_int]),
     "pl_ocp_sync": (C.c_int, [C.c_void_p]),
     "pl_state_integrate": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
     "pl_state_difference": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),

@@ -64,7 +64,9 @@ def source_sha() -> str:
         with open(path, "rb") as f:
             h.update(f.read())
         h.update(b"\0")
-    h.update(" ".join(_flags()).encode())
+    # the compile options, without the tree's absolute include paths (the GPU box runs the same
+    # tree under another root)
+    h.update(" ".join(f for f in _flags() if not os.path.isabs(f)).encode())
     return h.hexdigest()
 
 

@@ -27,7 +27,7 @@ import scipy.sparse as sp
 
 from . import _lib
 
-FUNCTIONS = ("sqp_data", "f_data", "g_data", "hess_data", "retract_solution")
+FUNCTIONS = ("sqp_data", "f_data", "g_data", "hess_data", "retract_solution", "compiled_solver")
 
 
 def library_path() -> str:
@@ -40,6 +40,27 @@ def bind(ocp, retract_steps: int = 3) -> None:
     device handle.  retract_steps = num_steps of compile_solution (default 3)."""
     h = getattr(getattr(ocp, "_backend", ocp), "h")
     _lib.check(_lib.lib().pl_casadi_bind(h, int(retract_steps)))
+
+
+def bind_compiled(ocp, warm_start: bool = True) -> None:
+    """Bind the interior-point OCP whose solve the exported ``compiled_solver`` runs: the
+    reference's ``ocp.compile_solver(warm_start)`` (ocp_whole_body_rnea.py:237-258) as a library
+    symbol, loadable the way run_mpc.py:51-53 loads the generated one::
+
+        casadi_ext.bind_compiled(ocp, warm_start=True)   # ocp = make_ocp(..., solver="fatrop")
+        solver_function = ca.external("compiled_solver", casadi_ext.library_path())
+
+    `ocp` is an ``OCP`` with the fatrop solver (batch 1); the parameters the function does not
+    take keep their current values, and without warm_start x starts from the OCP's initial guess."""
+    be = getattr(ocp, "_backend", ocp)
+    if hasattr(ocp, "param_vector"):  # the values the function bakes in (Opti's at to_function)
+        be.set_params(np.asarray(ocp.param_vector(), dtype=np.float64)[None, :])
+    x0 = getattr(ocp, "_x_initial", None)
+    x0 = None if x0 is None else np.ascontiguousarray(np.asarray(x0, dtype=np.float64).ravel())
+    if not warm_start and x0 is None:
+        raise ValueError("bind_compiled(warm_start=False) needs an OCP with an initial guess")
+    _lib.check(_lib.lib().pl_casadi_bind_compiled(be.h, int(bool(warm_start)),
+                                                  None if x0 is None else x0.ctypes.data_as(C.c_void_p)))
 
 
 def unbind() -> None:

@@ -414,6 +414,12 @@ class BatchedOCP:
         _lib.check(_lib.lib().pl_mpc_download(self.h, _lib.dptr(out)))
         return out
 
+    def mpc_set_ip_lam(self, carry):
+        """Interior-point MPC loop: carry=False (default) the reference's default driver
+        (compile_solver=True: primal warm start, cold multipliers, run_mpc.py:34-37, 50-111);
+        carry=True the Opti branch (lam_g passed back, ocp_whole_body_rnea.py:234-235)."""
+        _lib.check(_lib.lib().pl_mpc_set_ip_lam(self.h, int(bool(carry))))
+
     def mpc_graph_info(self):
         out = (C.c_longlong * 3)()
         _lib.check(_lib.lib().pl_mpc_graph_info(self.h, out))

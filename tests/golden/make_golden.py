@@ -562,12 +562,77 @@ def loop_fixture(name, rname, dyn, N, gidx, steps):
     print(name, "statuses", sorted(set(rec["loop_stats"][:, :, 0].ravel().tolist())), flush=True)
 
 
+# Interior-point closed loops of the reference's default driver (solver "fatrop", compile_solver
+# = True, warm_start = True: run_mpc.py:34-37, 50-111): per step the gait at t0 + k dt_min,
+# x_init, the OCP's primal warm start, one interior-point solve from COLD multipliers (the
+# compiled solver function takes x only, ocp_whole_body_rnea.py:239-257), x <- integrate(x,
+# DX[1]).  Problems of the benchmark batch (build_batch(..., 0) = ("syn", gidx)).  Go2 with the
+# numpy oracle; the B2G headline shape with the compiled restatement oracle/cpu (the numpy
+# oracle's algorithm to <= 3e-12 on these shapes, tests/test_cpu_baseline.py; a numpy B2G solve
+# takes ~15 min), its first step checked against the numpy fixture ip_b2g_rnea_n50 by
+# tests/test_ip.py.
+IP_LOOP_CONFIGS = [
+    ("ip_loop_go2_rnea_n20", "go2", "whole_body_rnea", 20, [0, 1, 2, 3], 5, "numpy"),
+    ("ip_loop_b2g_rnea_n50", "b2g", "whole_body_rnea", 50, [0, 1, 2, 3], 10, "cpu"),
+]
+
+
+def _ip_loop_one(args):
+    rname, dyn, N, gidx, steps, engine = args
+    from oracle.ip_ref import IPRef
+    R = robots.ROBOTS[rname]()
+    R.set_gait_sequence("trot", 0.8)
+    lay = Layout(R, dyn, N)
+    o = OracleOCP(R, dyn, N)
+    if engine == "cpu":
+        from oracle.cpu_baseline import CpuOCP
+        c = CpuOCP(R, dyn, N)
+        solve = lambda x_, p_: c.ip_solve(x_, p_)  # noqa: E731
+    else:
+        solve = lambda x_, p_: IPRef(o).solve(x_, p_)  # noqa: E731
+    P0, X0, XS0, t0 = make_problem(R, lay, dyn, N, ("syn", gidx))
+    xs, x, p = XS0.copy(), X0.copy(), P0.copy()
+    states, stl, xo = [], [], []
+    for k in range(steps):
+        if k > 0:
+            contact, swing = R.gait_sequence.get_gait_schedule(t0 + k * DT_MIN, horizon_dts(DT_MIN, DT_MAX, N), N)
+            vals = {"x_init": xs, "contact_schedule": contact, "swing_schedule": swing}
+            for key in vals:
+                o_, s_ = lay.poff[key]
+                p[o_:o_ + s_] = lay.pack(vals)[o_:o_ + s_]
+            x = o.warm_start(x, p)
+        x, _, st = solve(x, p)
+        DX, _ = o.split(x)
+        xs = o.integrate_state(xs, DX[1])
+        states.append(xs)
+        stl.append([st["status"], st["iter"]])
+        xo.append(x.copy())
+    print(f"  {dyn} syn {gidx}: {stl}", flush=True)
+    return dict(P=P0, X=X0, XS=XS0, T0=t0, states=np.array(states), stats=np.array(stl), x_out=np.array(xo))
+
+
+def ip_loop_fixture(name, rname, dyn, N, gidx, steps, engine):
+    from concurrent.futures import ProcessPoolExecutor
+    workers = min(len(gidx), int(os.environ.get("GOLDEN_WORKERS", "4")))
+    with ProcessPoolExecutor(workers) as ex:
+        res = list(ex.map(_ip_loop_one, [(rname, dyn, N, g, steps, engine) for g in gidx]))
+    rec = {"gidx": np.array(gidx), "gait": np.array("trot"), "engine": np.array(engine)}
+    for key, out in (("P", "P"), ("X", "X"), ("XS", "XS"), ("T0", "T0"), ("states", "loop_states"),
+                     ("stats", "loop_stats"), ("x_out", "loop_x")):
+        rec[out] = np.array([r[key] for r in res])
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **rec)
+    print(name, "statuses", sorted(set(rec["loop_stats"][:, :, 0].ravel().tolist())), flush=True)
+
+
 def main():
     only = sys.argv[1:]
+    for cfg in IP_LOOP_CONFIGS:
+        if cfg[0] in only:
+            ip_loop_fixture(*cfg)
     for cfg in LOOP_CONFIGS:
         if cfg[0] in only:
             loop_fixture(*cfg)
-    if only and all(o.startswith("loop_") for o in only):
+    if only and all(o.startswith("loop_") or o.startswith("ip_loop_") for o in only):
         return
     for cfg in IP_WARM_CONFIGS:
         if cfg[0] in only:

@@ -16,6 +16,9 @@ oracle itself on the same seeded inputs.  Tolerances (fp64 throughout):
 * 4-step closed MPC loop on the device: states <= 1e-7 relative (SURVEY 8c);
 * batch invariance and repeatability: bit-exact.
 """
+import json
+import os
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -23,6 +26,7 @@ import scipy.sparse as sp
 from conftest import golden, make_robot
 
 pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 CONFIGS = [("go2_rnea_n20", "go2", "whole_body_rnea", 20), ("go2_cv_n20", "go2", "centroidal_vel", 20),
            ("b2_aba_n40", "b2", "whole_body_aba", 40), ("b2g_acc_n50", "b2g", "whole_body_acc", 50),
@@ -241,6 +245,11 @@ LOOP_BENCH = [("loop_b2g_rnea_n50", "b2g", "whole_body_rnea", 50, 1024),
               ("loop_b2_aba_n40", "b2", "whole_body_aba", 40, 256)]
 
 
+# state bars looser than SURVEY 8c's 1e-7 over the 25 steps, with the reason: none yet (filled
+# from gpurun_out/loop_*_errors.json where the measured growth requires it)
+LOOP_BENCH_TOL = {}
+
+
 @pytest.mark.parametrize("name,rname,dyn,N,B", LOOP_BENCH)
 def test_device_mpc_loop_over_bench_steps_inside_batch(name, rname, dyn, N, B):
     """bench.py's loop (the BASELINE config's batch, AUTO's ADMM kernel -- k_admm at 1024,
@@ -264,21 +273,28 @@ def test_device_mpc_loop_over_bench_steps_inside_batch(name, rname, dyn, N, B):
     bo.set_x(X)
     bo.init_solver()
     bo.mpc_setup(XS, T0)
-    worst = 0.0
+    errs = np.zeros((len(G["gidx"]), steps))
+    same = np.ones((len(G["gidx"]), steps), dtype=bool)
     for k in range(steps):
         bo.mpc_step(k)
         S = bo.mpc_state()
         st = bo.mpc_stats()
         for j, g in enumerate(G["gidx"]):
-            err = _rel(S[g], G["loop_states"][j, k])
-            worst = max(worst, err)
-            assert err < 1e-7, (g, k, err)
-            assert [st["status"][g], st["admm_iters"][g], st["ls_branch"][g], st["ls_trials"][g]] == \
-                G["loop_stats"][j, k].tolist(), (g, k)
-    assert np.all(np.isfinite(bo.mpc_state()))
-    assert bo.mpc_graph_info()["replays"] >= steps - 2  # the timed shape: captured step replayed
-    print(f"{name}: {steps} steps x {len(G['gidx'])} problems, worst state error {worst:.2e}")
+            errs[j, k] = _rel(S[g], G["loop_states"][j, k])
+            same[j, k] = [st["status"][g], st["admm_iters"][g], st["ls_branch"][g], st["ls_trials"][g]] == \
+                G["loop_stats"][j, k].tolist()
+    graph = bo.mpc_graph_info()
+    finite = bool(np.all(np.isfinite(bo.mpc_state())))
     bo.close()
+    os.makedirs(os.path.join(HERE, "..", "gpurun_out"), exist_ok=True)
+    with open(os.path.join(HERE, "..", "gpurun_out", f"{name}_errors.json"), "w") as f:
+        json.dump({"state_rel_err": errs.tolist(), "outcome_exact": same.tolist(), "bar": LOOP_BENCH_TOL.get(name, 1e-7)},
+                  f)
+    print(f"{name}: {steps} steps x {len(G['gidx'])} problems, worst state error {errs.max():.2e}, "
+          f"per step {np.round(errs.max(0), 12).tolist()}")
+    assert finite and same.all(), np.argwhere(~same).tolist()
+    assert errs.max() < LOOP_BENCH_TOL.get(name, 1e-7), errs.max()
+    assert graph["replays"] >= steps - 2  # the timed shape: captured step replayed
 
 
 def test_make_ocp_surface_matches_oracle():

@@ -271,7 +271,8 @@ REFINE_COUNTS = {"ip_b2g_rnea_n50": None}
 
 @pytest.mark.gpu
 def test_ip_gpu_closed_loop():
-    """3 MPC steps of the device loop with the interior-point solver vs the oracle's loop."""
+    """3 MPC steps of the device loop with the interior-point solver and lam_g carried (the Opti
+    branch, pl_mpc_set_ip_lam(o, 1)) vs the oracle's loop."""
     from pinoloco.ocp import BatchedOCP
     G = golden("ip_go2_rnea_n20.npz")
     R = make_robot("go2", "trot")
@@ -281,6 +282,7 @@ def test_ip_gpu_closed_loop():
     bo.set_params(G["P"][:1])
     bo.set_x(G["X"][:1])
     bo.init_solver()
+    bo.mpc_set_ip_lam(True)
     bo.mpc_setup(G["XS"][:1], G["T0"][:1])
     steps = G["loop_states"].shape[0]
     for k in range(steps):
@@ -290,6 +292,71 @@ def test_ip_gpu_closed_loop():
         assert int(st["iter"][0]) == int(G["loop_stats"][k][1])
     xs = bo.mpc_state()[0]
     assert _rel(xs, G["loop_states"][-1]) <= 1e-6
+    bo.close()
+
+
+# The reference's default driver branch (compile_solver = True: primal warm start, cold
+# multipliers; make_golden.py IP_LOOP_CONFIGS), problems of the benchmark batch inside it
+IP_LOOPS = [("ip_loop_go2_rnea_n20", "go2", "whole_body_rnea", 20, 64),
+            ("ip_loop_b2g_rnea_n50", "b2g", "whole_body_rnea", 50, 1024)]
+
+
+def test_ip_loop_fixture_first_step_matches_numpy_oracle():
+    """The B2G loop fixture comes from the compiled restatement (oracle/cpu); its first solves
+    (cold start, the problems shared with the numpy fixture ip_b2g_rnea_n50) agree with the numpy
+    oracle's, and the loop holds no failed line search (the benchmark's -2 cascade came from
+    carrying lam_g, which the default driver does not do)."""
+    L = golden("ip_loop_b2g_rnea_n50.npz")
+    G = golden("ip_b2g_rnea_n50.npz")
+    shared = 0
+    for j, g in enumerate(L["gidx"]):
+        for b in range(G["P"].shape[0]):
+            if np.array_equal(G["P"][b], L["P"][j]) and np.array_equal(G["X"][b], L["X"][j]):
+                assert L["loop_stats"][j, 0].tolist() == [int(G["status"][b]), int(G["iter"][b])]
+                assert _rel(L["loop_x"][j, 0], G["x_out"][b]) < 1e-8
+                shared += 1
+    assert shared >= 3
+    # the headline shape's loop never fails a line search; the Go2 loop holds one -2 exit (syn 3,
+    # step 4), so the device loop's failure path is pinned too
+    assert -2 not in set(L["loop_stats"][:, :, 0].ravel().tolist())
+    assert -2 in set(golden("ip_loop_go2_rnea_n20.npz")["loop_stats"][:, :, 0].ravel().tolist())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,rname,dyn,N,B", IP_LOOPS)
+def test_ip_gpu_default_driver_loop_inside_batch(name, rname, dyn, N, B):
+    """pl_mpc_step with the interior-point solver in the reference's default driver mode (cold
+    multipliers per solve, pl_mpc_set_ip_lam(o, 0), the default) over the fixture's steps, inside a
+    batch of the benchmark's problems: each fixture problem's status and iteration count exact
+    at every step, its iterate x and the state <= 1e-6 relative."""
+    from pinoloco.ocp import BatchedOCP
+    from pinoloco.synthetic import build_batch
+    G = golden(f"{name}.npz")
+    R = make_robot(rname, "trot")
+    lay, P, X, XS, T0 = build_batch(R, dyn, N, B, 0)
+    for j, g in enumerate(G["gidx"]):
+        assert np.array_equal(P[g], G["P"][j]) and np.array_equal(XS[g], G["XS"][j])
+    bo = BatchedOCP(R, dyn, N, batch=B, device=0, gait_type="trot", gait_period=0.8)
+    bo.set_solver("fatrop")
+    bo.set_ip_settings()
+    bo.set_params(P)
+    bo.set_x(X)
+    bo.init_solver()
+    bo.mpc_setup(XS, T0)
+    worst = 0.0
+    counts = []
+    for k in range(G["loop_states"].shape[1]):
+        bo.mpc_step(k)
+        st = bo.ip_stats()
+        S = bo.mpc_state()
+        Xk = bo.get_x()
+        counts.append({int(a): int(c) for a, c in zip(*np.unique(st["status"], return_counts=True))})
+        for j, g in enumerate(G["gidx"]):
+            assert [int(st["status"][g]), int(st["iter"][g])] == G["loop_stats"][j, k].tolist(), (g, k)
+            e = max(_rel(S[g], G["loop_states"][j, k]), _rel(Xk[g], G["loop_x"][j, k]))
+            worst = max(worst, e)
+            assert e <= 1e-6, (g, k, e)
+    print(f"{name}: worst {worst:.2e}; status counts per step {counts}")
     bo.close()
 
 
@@ -564,3 +631,55 @@ def test_run_mpc_compiled_fatrop_branch():
         errs.append((_rel(sol_x, G["x_out"][k]), _rel(x_init, G["x_init_next"][k])))
         assert errs[-1][0] <= 1e-7 and errs[-1][1] <= 1e-7, (k, errs)
     ocp._backend.close()
+
+
+@pytest.mark.gpu
+def test_run_mpc_load_compiled_solver_external():
+    """The reference's hardware-deployment path: load_compiled_solver (run_mpc.py:51-53),
+    solver_function = ca.external("compiled_solver", lib), here the library's own
+    compiled_solver symbol in CasADi's external ABI (include/pinoloco_casadi.h), driven through
+    casadi_ext.ExternalFunction exactly as CasADi calls it (n_in / sparsity / work / call).
+    The loop of run_mpc.py:68-111 for 3 steps against the oracle's loop
+    (ip_b2g_rnea_n14_compiled.npz): status / iterations exact, sol_x and the next x_init <= 1e-7."""
+    from pinoloco import casadi_ext
+    robot, ocp = _run_mpc_setup(0)
+    G = golden("ip_b2g_rnea_n14_compiled.npz")
+    warm_start = True
+    x_init = ocp.x_nom
+    tau_prev = np.zeros(robot.nj)
+    ocp.init_solver()
+    casadi_ext.bind_compiled(ocp, warm_start)
+    solver_function = casadi_ext.ExternalFunction("compiled_solver")
+    assert solver_function.n_in == 17 and solver_function.n_out == 1
+    Q_diag = ocp.opti.value(ocp.Q_diag)
+    R_diag = ocp.opti.value(ocp.R_diag)
+    W_diag = ocp.opti.value(ocp.W_diag)
+    for k in range(G["P"].shape[0]):
+        params = _compiled_params(ocp, robot, x_init, k, Q_diag, R_diag, W_diag, tau_prev, warm_start)
+        (sol_x,) = solver_function(*params)
+        sol_x = np.asarray(sol_x).ravel()
+        st = ocp._backend.ip_stats()
+        assert (int(st["status"][0]), int(st["iter"][0])) == (int(G["status"][k]), int(G["iter"][k])), k
+        ocp.retract_stacked_sol(sol_x, retract_all=False)
+        x_init = ocp.dyn.state_integrate()(x_init, ocp.DX_prev[1])
+        tau_prev = ocp.get_tau_sol(i=1)
+        assert _rel(sol_x, G["x_out"][k]) <= 1e-7 and _rel(x_init, G["x_init_next"][k]) <= 1e-7, k
+    with pytest.raises(ValueError):
+        solver_function(*params[:-1])
+    casadi_ext.unbind()
+    ocp._backend.close()
+
+
+def test_compiled_solver_symbols_host_only():
+    """compiled_solver's CasADi symbols on a host-only handle: binding refuses a handle that is
+    not an interior-point batch-1 OCP, and the export set includes the compiled solver."""
+    from pinoloco import _lib, casadi_ext
+    from pinoloco.ocp import BatchedOCP
+    L = _lib.lib()
+    for suffix in ("", "_n_in", "_n_out", "_sparsity_in", "_sparsity_out", "_work", "_name_in"):
+        assert hasattr(L, "compiled_solver" + suffix)
+    bo = BatchedOCP(make_robot("go2"), "whole_body_rnea", 20, batch=2, device=-1)
+    with pytest.raises(_lib.PinolocoError):
+        casadi_ext.bind_compiled(bo, True)  # osqp solver, batch 2
+    bo.close()
+    assert "compiled_solver" in casadi_ext.FUNCTIONS
