@@ -282,6 +282,8 @@ def main():
     ap.add_argument("--solver", default="osqp", choices=["osqp", "fatrop"],
                     help="osqp: the headline SQP + OSQP path; fatrop: the interior-point restatement")
     ap.add_argument("--dry-run", action="store_true", help="gloo plumbing only, no GPU")
+    ap.add_argument("--admm-kernel", default="auto", choices=["auto", "sweep", "sweep2", "chain"],
+                    help="ADMM mapping (pl_ocp_set_admm_kernel); auto = the library's batch-size rule")
     ap.add_argument("--host-io-steps", type=int, default=None,
                     help="extra steps timed with the per-step D2H of [u_0, x_state] (default min(steps, 10))")
     args = ap.parse_args()
@@ -312,6 +314,8 @@ def main():
     if args.solver == "fatrop":
         bo.set_solver("fatrop")
         bo.set_ip_settings()
+    if args.admm_kernel != "auto":
+        bo.set_admm_kernel(args.admm_kernel)
     bo.set_params(P)
     bo.set_x(X)
     bo.init_solver()

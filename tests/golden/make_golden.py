@@ -512,19 +512,23 @@ def ip_warm_fixture(name, dyn, gidx):
 # 0-24) for problems of the benchmark batch (build_batch(..., 0) = ("syn", gidx)): per step the
 # gait at t0 + k dt_min, x_init, the OCP warm start, one SQP iteration, x <- integrate(x, DX[1])
 # (run_mpc.py:127-143).  tests/test_gpu.py checks these problems inside the B = 1024 / 256 batch.
+# The aba loop also stores the trajectory of the reduced-form oracle (oracle/osqp_ref.py
+# kkt="reduced_block": the GPU's algebra -- the reduced SPD system with block inverses -- in
+# numpy): whole_body_aba's closed loop amplifies the two formulations' ~1e-9 per-step difference
+# to ~1e-6 over 25 steps (tests/test_gpu.py LOOP_BENCH_TOL).
 LOOP_CONFIGS = [
     ("loop_b2g_rnea_n50", "b2g", "whole_body_rnea", 50, [0, 1, 2, 3], 25),
     ("loop_b2g_acc_n50", "b2g", "whole_body_acc", 50, [0, 1, 2, 3], 25),
-    ("loop_b2_aba_n40", "b2", "whole_body_aba", 40, [0, 1, 2, 3], 25),
+    ("loop_b2_aba_n40", "b2", "whole_body_aba", 40, [0, 1, 2, 3], 25, True),
 ]
 
 
 def _loop_one(args):
-    rname, dyn, N, gidx, steps = args
+    rname, dyn, N, gidx, steps, kkt = args
     R = robots.ROBOTS[rname]()
     R.set_gait_sequence("trot", 0.8)
     lay = Layout(R, dyn, N)
-    o = OracleOCP(R, dyn, N)
+    o = OracleOCP(R, dyn, N, kkt=kkt)
     P0, X0, XS0, t0 = make_problem(R, lay, dyn, N, ("syn", gidx))
     xs, x = XS0.copy(), X0.copy()
     states, u0s, lst = [], [], []
@@ -549,15 +553,19 @@ def _loop_one(args):
     return dict(P=P0, X=X0, XS=XS0, T0=t0, states=np.array(states), u0=np.array(u0s), stats=np.array(lst))
 
 
-def loop_fixture(name, rname, dyn, N, gidx, steps):
+def loop_fixture(name, rname, dyn, N, gidx, steps, reduced=False):
     from concurrent.futures import ProcessPoolExecutor
     workers = min(len(gidx), int(os.environ.get("GOLDEN_WORKERS", "4")))
     with ProcessPoolExecutor(workers) as ex:
-        res = list(ex.map(_loop_one, [(rname, dyn, N, g, steps) for g in gidx]))
+        res = list(ex.map(_loop_one, [(rname, dyn, N, g, steps, "quasi_definite") for g in gidx]))
+        red = list(ex.map(_loop_one, [(rname, dyn, N, g, steps, "reduced_block") for g in gidx])) if reduced else None
     rec = {"gidx": np.array(gidx), "gait": np.array("trot")}
     for key, out in (("P", "P"), ("X", "X"), ("XS", "XS"), ("T0", "T0"), ("states", "loop_states"),
                      ("u0", "loop_u0"), ("stats", "loop_stats")):
         rec[out] = np.array([r[key] for r in res])
+    if red is not None:
+        rec["loop_states_reduced"] = np.array([r["states"] for r in red])
+        rec["loop_stats_reduced"] = np.array([r["stats"] for r in red])
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **rec)
     print(name, "statuses", sorted(set(rec["loop_stats"][:, :, 0].ravel().tolist())), flush=True)
 

@@ -245,9 +245,15 @@ LOOP_BENCH = [("loop_b2g_rnea_n50", "b2g", "whole_body_rnea", 50, 1024),
               ("loop_b2_aba_n40", "b2", "whole_body_aba", 40, 256)]
 
 
-# state bars looser than SURVEY 8c's 1e-7 over the 25 steps, with the reason: none yet (filled
-# from gpurun_out/loop_*_errors.json where the measured growth requires it)
-LOOP_BENCH_TOL = {}
+# State bars looser than SURVEY 8c's 1e-7 over the 25 steps, with the reason.  whole_body_aba's
+# closed loop amplifies the per-step difference of the two linear-algebra formulations (the GPU
+# solves the reduced SPD system with block inverses, the oracle the quasi-definite KKT; one SQP
+# step differs by <= 1.4e-9 on b2_aba_n40, tests/test_reduced_oracle.py): the reduced-form oracle
+# (the GPU's algebra in numpy, stored in the fixture as loop_states_reduced) itself drifts from the
+# KKT oracle by up to 1.3e-6 by step 21 with every step's outcome exact (make_golden.py
+# LOOP_CONFIGS), and the GPU measured 9.0e-7 (profiles/r06/b/loop_b2_aba_n40_errors.json).  The GPU
+# is held to 1e-7 against the reduced-form trajectory (its own algebra) in the same test.
+LOOP_BENCH_TOL = {"loop_b2_aba_n40": 2e-6}
 
 
 @pytest.mark.parametrize("name,rname,dyn,N,B", LOOP_BENCH)
@@ -274,13 +280,17 @@ def test_device_mpc_loop_over_bench_steps_inside_batch(name, rname, dyn, N, B):
     bo.init_solver()
     bo.mpc_setup(XS, T0)
     errs = np.zeros((len(G["gidx"]), steps))
+    errs_red = np.zeros((len(G["gidx"]), steps))
     same = np.ones((len(G["gidx"]), steps), dtype=bool)
+    red = "loop_states_reduced" in G
     for k in range(steps):
         bo.mpc_step(k)
         S = bo.mpc_state()
         st = bo.mpc_stats()
         for j, g in enumerate(G["gidx"]):
             errs[j, k] = _rel(S[g], G["loop_states"][j, k])
+            if red:
+                errs_red[j, k] = _rel(S[g], G["loop_states_reduced"][j, k])
             same[j, k] = [st["status"][g], st["admm_iters"][g], st["ls_branch"][g], st["ls_trials"][g]] == \
                 G["loop_stats"][j, k].tolist()
     graph = bo.mpc_graph_info()
@@ -288,12 +298,16 @@ def test_device_mpc_loop_over_bench_steps_inside_batch(name, rname, dyn, N, B):
     bo.close()
     os.makedirs(os.path.join(HERE, "..", "gpurun_out"), exist_ok=True)
     with open(os.path.join(HERE, "..", "gpurun_out", f"{name}_errors.json"), "w") as f:
-        json.dump({"state_rel_err": errs.tolist(), "outcome_exact": same.tolist(), "bar": LOOP_BENCH_TOL.get(name, 1e-7)},
-                  f)
+        json.dump({"state_rel_err": errs.tolist(), "outcome_exact": same.tolist(), "bar": LOOP_BENCH_TOL.get(name, 1e-7),
+                   "state_rel_err_vs_reduced_form_oracle": errs_red.tolist() if red else None}, f)
     print(f"{name}: {steps} steps x {len(G['gidx'])} problems, worst state error {errs.max():.2e}, "
-          f"per step {np.round(errs.max(0), 12).tolist()}")
+          f"per step {np.round(errs.max(0), 12).tolist()}" + (f"; vs the reduced-form oracle {errs_red.max():.2e}"
+                                                                if red else ""))
     assert finite and same.all(), np.argwhere(~same).tolist()
     assert errs.max() < LOOP_BENCH_TOL.get(name, 1e-7), errs.max()
+    if red:
+        assert np.array_equal(G["loop_stats_reduced"], G["loop_stats"])
+        assert errs_red.max() < 1e-7, errs_red.max()
     assert graph["replays"] >= steps - 2  # the timed shape: captured step replayed
 
 

@@ -266,7 +266,7 @@ def test_ip_gpu_refinement_counts_and_gather_path():
 
 # linear solves per problem of the fixture's solve (first solves + refinement corrections),
 # measured on the MI355X with the current refinement rule (gpurun_out/ip_refine_counts.json)
-REFINE_COUNTS = {"ip_b2g_rnea_n50": None}
+REFINE_COUNTS = {"ip_b2g_rnea_n50": [51, 51, 51, 52, 52, 52, 51, 52]}  # profiles/r06/b/ip_refine_counts.json
 
 
 @pytest.mark.gpu
