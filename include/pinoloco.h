@@ -118,7 +118,9 @@ typedef struct {
 #define PL_PATH_NO_MPC_GRAPH    64u  /* pl_mpc_step launches eagerly (no HIP graph) */
 #define PL_PATH_ADMM_TIMING     128u /* s_memtime phase timing in the sweep / factor kernels (pl_debug_get "admm_t") */
 #define PL_PATH_IP_REFINE_GATHER 256u /* k_ip_refine's H_i dx by the per-column global gather (the nw > 192 path) */
-#define PL_PATH_ALL             511u /* pl_ocp_create rejects any other bit: callers zero the struct */
+#define PL_PATH_HESS_PAIRS      512u /* the (dq, dq) / (dq, dv) Hessian pairs by one hyper-dual sweep each (r05), not
+                                        the forward-over-reverse columns */
+#define PL_PATH_ALL             1023u /* pl_ocp_create rejects any other bit: callers zero the struct */
 
 typedef struct {
   int status;                  /* OSQP status code (1 solved, 2 inaccurate, -2 max iter, ...) */

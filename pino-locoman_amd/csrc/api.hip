@@ -8,6 +8,8 @@
 // api_build.hip; the CasADi external-function ABI is api_casadi.hip.
 #include "api_internal.h"
 
+#include <map>
+
 static thread_local char g_err[1024] = "";
 
 void pl_set_error(const char* fmt, ...) {
@@ -850,6 +852,48 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
     }
     h->hnz_off[3] = (int)hnz.size();
     if (!hnz.empty() && upload(o, &h->d.hnz, hnz)) return -2;
+    // the (dq, dq) / (dq, dv) pairs as forward-over-reverse columns (k_lag_hess_col, r06): the pair
+    // (j, k), j <= k, is written by the item (node, chain, j) with k's local coordinate in its mask
+    // (hess_tree.h col_coord).  The column sweep assumes no frame on the root and at most one frame
+    // (a foot or the external force) per chain; otherwise, without chain confinement, or with
+    // PL_PATH_HESS_PAIRS the pair kernel runs.
+    std::vector<int4> hcol;
+    {
+      bool ok = chains && !htr.empty() && !(h->debug_paths & PL_PATH_HESS_PAIRS);
+      for (int e = 0; e < O.nee && ok; ++e)
+        if ((e < O.nfeet ? O.feet[e].joint : O.ext.joint) == 1) ok = false;
+      for (int c = 0; c < Mo.nchains && ok; ++c) {
+        int nfr = 0;
+        for (int e = 0; e < O.nee; ++e) {
+          const int fj = e < O.nfeet ? O.feet[e].joint : O.ext.joint;
+          if (fj >= Mo.chain_first[c] && fj < Mo.chain_first[c] + Mo.chain_len[c]) ++nfr;
+        }
+        if (nfr > 1 || 12 + 2 * Mo.chain_len[c] > 32) ok = false;
+      }
+      const auto loc_of = [&](int ch, int k) {  // k (a state dx index) in chain ch's local coordinates
+        if (k < 6) return k;
+        if (k >= O.nv && k < O.nv + 6) return 6 + k - O.nv;
+        if (ch < 0) return -1;
+        const int first = Mo.chain_first[ch], L = Mo.chain_len[ch];
+        for (int kk = 0; kk < L; ++kk) {
+          if (Mo.idx_v[first + kk] == k) return 12 + kk;
+          if (O.nv + Mo.idx_v[first + kk] == k) return 12 + L + kk;
+        }
+        return -1;
+      };
+      std::map<long long, uint32_t> cols;  // (node, chain, j) -> mask, in work-list order
+      for (const int2& pr : htr) {
+        const int i = pr.x & 0xffff, ch = (pr.x >> 16) - 1, j = pr.y & 0xffff, k = pr.y >> 16;
+        const int lk = loc_of(ch, k);
+        if (lk < 0) { ok = false; break; }
+        cols[((long long)i << 32) | ((long long)(ch + 1) << 16) | j] |= 1u << lk;
+      }
+      if (ok)
+        for (const auto& kv : cols)
+          hcol.push_back(make_int4((int)(kv.first >> 32) | (int)(((kv.first >> 16) & 0xffff) << 16),
+                                   (int)(kv.first & 0xffff), (int)kv.second, 0));
+    }
+    h->hcol_len = (int)hcol.size();
     h->hl_len = (int)hl.size();
     h->hlin_len = (int)hlin.size();
     h->hvv_len = (int)hvv.size();
@@ -865,7 +909,7 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
       for (int k = 0; k < 3; ++k) m0.gravity[k] = 0.0;
       if (upload(o, &h->d.hlin, hlin) || (!hvv.empty() && upload(o, &h->d.hvv, hvv)) ||
           (!htr.empty() && upload(o, &h->d.htr, htr)) || (!hcone.empty() && upload(o, &h->d.hcone, hcone)) ||
-          (!htrf.empty() && upload(o, &h->d.htrf, htrf)))
+          (!htrf.empty() && upload(o, &h->d.htrf, htrf)) || (!hcol.empty() && upload(o, &h->d.hcol, hcol)))
         return -2;
       if (!h->d.model0 && (dalloc(o, &h->d.model0, 1) ||
                            hipMemcpy(h->d.model0, &m0, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess))

@@ -12,6 +12,7 @@
 // (k (k + 1) / 2 + j from the node's offset d.hoff[i]), the layout k_fnode assembles Kt_ii in.
 #include "dyn.h"
 #include "eval_common.h"
+#include "hess_tree.h"
 
 using pl::VecIn;
 
@@ -145,202 +146,7 @@ __global__ __launch_bounds__(64) void k_lag_hess_lin(PlDev d, int B, int n, int 
 // subspaces and every row block as well, and spills).  The arm rows (relative to the base,
 // dynamics/dynamics.py:86-113) keep the velocity-only tree pass, for the pairs on the base or the
 // arm's chain.  d.htr packs pairs as d.hlist; one pair per wave, one problem per lane.
-namespace {
-template <class S> __device__ void crossd(const double* a, const S* b, S* o) {  // a x b, a constant
-  o[0] = a[1] * b[2] - a[2] * b[1];
-  o[1] = a[2] * b[0] - a[0] * b[2];
-  o[2] = a[0] * b[1] - a[1] * b[0];
-}
-// out = R_j^T d for the revolute joint rotation R_j = jR Rot(axis, q_j) (rbd.h rev_rot), applied as
-// Rot^T (jR^T d) so that no hyper-dual 3x3 matrix is formed (jR constant; Rot a plane rotation for
-// the axis-aligned joints)
-template <class S, class C> __device__ void rot_t(const PlModel& M, int j, const C& s, const C& c, const S* d, S* out) {
-  S e[3];
-  pl::mattvec(M.jR[j], d, e);
-  switch (M.axis_kind[j]) {
-    case PL_AX_X:
-      out[0] = e[0]; out[1] = c * e[1] + s * e[2]; out[2] = c * e[2] - s * e[1];
-      break;
-    case PL_AX_Y:
-      out[0] = c * e[0] - s * e[2]; out[1] = e[1]; out[2] = s * e[0] + c * e[2];
-      break;
-    case PL_AX_Z:
-      out[0] = c * e[0] + s * e[1]; out[1] = c * e[1] - s * e[0]; out[2] = e[2];
-      break;
-    default: {  // Rodrigues I + s [a]x + (1 - c) [a]x^2, transposed
-      const double* a = M.axis[j];
-      const double K[9] = {0, -a[2], a[1], a[2], 0, -a[0], -a[1], a[0], 0};
-      const C oc = 1.0 - c;
-      for (int r = 0; r < 3; ++r) {
-        S t = e[r];
-        for (int q = 0; q < 3; ++q) {
-          const double kk = K[3 * q] * K[r] + K[3 * q + 1] * K[3 + r] + K[3 * q + 2] * K[6 + r];  // ([a]x^2)_qr
-          t += (s * K[3 * q + r] + oc * kk) * e[q];
-        }
-        out[r] = t;
-      }
-    }
-  }
-}
-// actInv of a motion through joint j: [R^T (m_lin - p x m_ang); R^T m_ang], p the joint placement
-template <class S, class C> __device__ void act_inv_j(const PlModel& M, int j, const C& s, const C& c, const S* m, S* out) {
-  S pxw[3];
-  crossd(M.jp[j], m + 3, pxw);
-  S d[3] = {m[0] - pxw[0], m[1] - pxw[1], m[2] - pxw[2]};
-  rot_t(M, j, s, c, d, out);
-  rot_t(M, j, s, c, m + 3, out + 3);
-}
-// f = I a + v x* I v  (body axes; inertia (m, c, Ic) constant)
-template <class S> __device__ void body_wrench(double m, const double* c, const double* Ic, const S* a, const S* v,
-                                               S* f) {
-  S t[3], h[6];
-  crossd(c, v + 3, t);
-  for (int k = 0; k < 3; ++k) h[k] = m * (v[k] - t[k]);
-  crossd(c, h, t);
-  for (int k = 0; k < 3; ++k) h[3 + k] = Ic[3 * k] * v[3] + Ic[3 * k + 1] * v[4] + Ic[3 * k + 2] * v[5] + t[k];
-  pl::motion_cross_force(v, h, f);
-  crossd(c, a + 3, t);
-  S fl[3];
-  for (int k = 0; k < 3; ++k) fl[k] = m * (a[k] - t[k]);
-  crossd(c, fl, t);
-  for (int k = 0; k < 3; ++k) {
-    f[k] += fl[k];
-    f[3 + k] += Ic[3 * k] * a[3] + Ic[3 * k + 1] * a[4] + Ic[3 * k + 2] * a[5] + t[k];
-  }
-}
-__device__ int block_row(const PlOcpConst& O, int type, int kind, int arg) {  // first row of a block, -1: none
-  int r = 0;
-  for (int bi = 0; bi < O.nblk[type]; ++bi) {
-    const PlRowBlock B = O.blk[type][bi];
-    if (B.kind == kind && (arg < 0 || B.arg == arg)) return r;
-    r += B.count;
-  }
-  return -1;
-}
-}  // namespace
-
-// The sweep's view of one node: the root pose, the state accessors and the world-axis vectors it
-// rotates into a body's axes (oR_b^T x, by a walk from the root: R0^T, then R_j^T joint by joint)
-struct TreeSweep {
-  const PlModel& M;
-  const HDual* qb;
-  const pl::RevQ<HDual, VecIn<HDual>>& qrev;
-  // two vectors in one walk (a foot's force and its velocity rows' multipliers)
-  template <class X> __device__ void to_body2(int first, int kk, const X* xw, const double* yw, HDual* ox,
-                                              HDual* oy) const {
-    HDual R0[9];
-    pl::quat_to_R(qb + 3, R0);
-    pl::mattvec(R0, xw, ox);
-    pl::mattvec(R0, yw, oy);
-    for (int k2 = 0; k2 <= kk; ++k2) {
-      const int j2 = first + k2;
-      HDual s2, c2, t[3];
-      sincos_s(qrev(M.idx_q[j2]), &s2, &c2);
-      rot_t(M, j2, s2, c2, ox, t);
-      for (int q = 0; q < 3; ++q) ox[q] = t[q];
-      rot_t(M, j2, s2, c2, oy, t);
-      for (int q = 0; q < 3; ++q) oy[q] = t[q];
-    }
-  }
-  template <class X> __device__ void to_body(int first, int kk, const X* xw, HDual* out) const {
-    HDual R0[9];
-    pl::quat_to_R(qb + 3, R0);
-    pl::mattvec(R0, xw, out);
-    for (int k2 = 0; k2 <= kk; ++k2) {
-      const int j2 = first + k2;
-      HDual s2, c2, t[3];
-      sincos_s(qrev(M.idx_q[j2]), &s2, &c2);
-      rot_t(M, j2, s2, c2, out, t);
-      for (int q = 0; q < 3; ++q) out[q] = t[q];
-    }
-  }
-};
-
-// contact forces on body j (f_b -= [fl; p x fl], fl = oR^T f_world) and its feet's velocity rows
-// (phi += (v_lin + w x p) . oR^T mu); first / kk: body j's place in its chain (first = -1: the root)
-// (fx: the contact forces; f(e, c): the external frame's, plain or seeded -- k_lag_hess_tree<true>;
-// frame ef's force and multipliers arrive already in body axes: cf, cg (cg only if has_mu))
-__device__ void foot_mu(const PlOcpConst& O, int type, int node, int e, const double* lam, const double* p,
-                        double* mu, bool* has) {  // a foot's velocity-row multipliers times coefficients
-  const int rxy = e < O.nfeet ? block_row(O, type, PL_RB_FVXY, e) : -1;
-  const int rz = e < O.nfeet ? block_row(O, type, PL_RB_FVZ, e) : -1;
-  *has = rxy >= 0 || rz >= 0;
-  const double c = e < O.nfeet ? p[O.P.contact + 4 * node + e] : 0.0;
-  mu[0] = rxy >= 0 ? c * lam[rxy] : 0.0;
-  mu[1] = rxy >= 0 ? c * lam[rxy + 1] : 0.0;
-  mu[2] = rz >= 0 ? lam[rz] : 0.0;
-}
-template <class F3>
-__device__ void body_frames(const PlOcpConst& O, const TreeSweep& T, int first, int kk, int j, int type, int node,
-                            const HDual* vj, const double* fx, const F3& f, const double* lam, const double* p,
-                            HDual* fb, HDual& phi, int ef = -1, const HDual* cf = nullptr, const HDual* cg = nullptr,
-                            bool has_mu = false) {
-  for (int e = 0; e < O.nee; ++e) {
-    const PlFrameRef& F = (e < O.nfeet) ? O.feet[e] : O.ext;
-    if (F.joint != j) continue;
-    HDual fl[3], t[3];
-    if (e == ef) {  // carried along the chain
-      for (int k = 0; k < 3; ++k) fl[k] = cf[k];
-      if (has_mu) {
-        HDual wxp[3];
-        crossd(F.p, vj + 3, wxp);  // p x w = -(w x p)
-        for (int k = 0; k < 3; ++k) phi += (vj[k] - wxp[k]) * cg[k];
-      }
-      crossd(F.p, fl, t);
-      for (int k = 0; k < 3; ++k) { fb[k] -= fl[k]; fb[3 + k] -= t[k]; }
-      continue;
-    }
-    const int rxy = e < O.nfeet ? block_row(O, type, PL_RB_FVXY, e) : -1;
-    const int rz = e < O.nfeet ? block_row(O, type, PL_RB_FVZ, e) : -1;
-    if (e >= O.nfeet) {  // the external force frame (seeded in k_lag_hess_tree<true>)
-      const decltype(f(0, 0)) fw[3] = {f(e, 0), f(e, 1), f(e, 2)};
-      T.to_body(first, kk, fw, fl);
-    } else if (rxy >= 0 || rz >= 0) {
-      const double c = p[O.P.contact + 4 * node + e];
-      const double mu[3] = {rxy >= 0 ? c * lam[rxy] : 0.0, rxy >= 0 ? c * lam[rxy + 1] : 0.0,
-                            rz >= 0 ? lam[rz] : 0.0};
-      HDual g[3], wxp[3];
-      T.to_body2(first, kk, fx + 3 * e, mu, fl, g);
-      crossd(F.p, vj + 3, wxp);  // p x w = -(w x p)
-      for (int k = 0; k < 3; ++k) phi += (vj[k] - wxp[k]) * g[k];
-    } else {
-      T.to_body(first, kk, fx + 3 * e, fl);
-    }
-    crossd(F.p, fl, t);
-    for (int k = 0; k < 3; ++k) { fb[k] -= fl[k]; fb[3 + k] -= t[k]; }
-  }
-}
-
-namespace {
-// The root pose for the state pairs: nothing downstream reads the base position (translation
-// invariance: it is set to 0), and the orientation is q0 (x) exp(w / 2), w = dq_3..5, whose
-// rotation matrix is R(q0) Exp(w) -- what integrate_ff's SE3 exponential, R -> quaternion and
-// renormalisation give (the last two are the identity on rotations: their derivatives cancel
-// analytically), without carrying them in hyper-duals.  Below the exp6 series threshold
-// (rbd.h PL_TAYLOR_PREC3) sin(t/2)/t and cos(t/2) are their series in t^2 through t^4.
-__device__ void base_pose(const double* xi, const VecIn<HDual>& dx, HDual* qb) {
-  const HDual w[3] = {dx[3], dx[4], dx[5]};
-  const HDual t2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-  HDual f, g;
-  if (val(t2) < PL_TAYLOR_PREC3 * PL_TAYLOR_PREC3) {
-    f = 0.5 - t2 * (1.0 / 48.0) + (t2 * t2) * (1.0 / 3840.0);
-    g = 1.0 - t2 * 0.125 + (t2 * t2) * (1.0 / 384.0);
-  } else {
-    const HDual th = sqrt_s(t2);
-    HDual sh, ch;
-    sincos_s(th * 0.5, &sh, &ch);
-    f = sh / th;
-    g = ch;
-  }
-  const HDual u[3] = {f * w[0], f * w[1], f * w[2]};  // exp(w / 2) = [u; g]
-  const double* q0 = xi + 3;                           // [x y z w]
-  HDual cr[3];
-  crossd(q0, u, cr);
-  for (int k = 0; k < 3; ++k) qb[3 + k] = q0[3] * u[k] + q0[k] * g + cr[k];
-  qb[6] = q0[3] * g - (q0[0] * u[0] + q0[1] * u[1] + q0[2] * u[2]);
-  for (int k = 0; k < 3; ++k) qb[k] = HDual(0.0);
-}
-}  // namespace
+using namespace hess;
 
 // whole_body_rnea / whole_body_acc, the (dv, dv) block: the only rows with curvature in v are the RNEA rows,
 // and at a = 0, f = 0 without gravity the RNEA torque is the bias term C(q, v) v, a quadratic form
@@ -421,116 +227,37 @@ __global__ __launch_bounds__(64) void k_lag_hess_tree(PlDev d, int B, int n, int
   const int qa = blockIdx.y * 64 + threadIdx.x;  // the active problems, compacted (k_ip_compact)
   if (qa >= d.ip_act[B]) return;
   const int b = d.ip_act[qa];
-  const PlOcpConst& O = *d.oc;
-  const PlModel& M = *d.model;
   const int2 w = (SF ? d.htrf : d.htr)[blockIdx.x];
   const int wx = __builtin_amdgcn_readfirstlane(w.x);
   const int i = wx & 0xffff, only_ch = (wx >> 16) - 1;
   const int jk = __builtin_amdgcn_readfirstlane(w.y);
   const int j = jk & 0xffff, k = jk >> 16;
   const PlNode nd = d.nodes[i];
-  const double* x = d.x + (size_t)b * n + nd.x_off;
-  const double* p = d.p + (size_t)b * np;
-  const double* lam = d.ip_lam + (size_t)b * m + nd.row_off;
-  double* H = d.Hlag + (size_t)b * hl_stride + d.hoff[i] + k * (k + 1) / 2 + j;
-  if (j < 3) {  // the RNEA and the frame velocities do not read the base position (rows.h seed_pos)
-    *H = 0.0;
-    return;
-  }
-  const double* xi = p + O.P.x_init;
-  const int nv = O.nv, ndx = O.ndx, type = pl::node_type(O, i);
-  const VecIn<HDual> dx{x, nullptr, 0.0, j, k};
-  HDual qb[7];
-  base_pose(xi, dx, qb);
-  const pl::RevQ<HDual, VecIn<HDual>> qrev{xi, dx};
-  const pl::VelAcc<HDual, VecIn<HDual>> vel{xi + O.nq, pl::sub_in(dx, nv)};
-  const double* a = x + ndx;           // u = [a | f | tau_j]: constants for a state pair
-  const double* fx = x + ndx + O.na;
-  const int fk = k - ndx - O.na;  // SF: the seeded force component
-  const auto f = [&](int e, int c) {
-    if constexpr (SF) return HDual(fx[3 * e + c], 0.0, 3 * e + c == fk ? 1.0 : 0.0, 0.0);
-    else return fx[3 * e + c];
-  };
-  const int rb = block_row(O, type, PL_RB_RNEA_BASE, -1), rt = block_row(O, type, PL_RB_TAU_EQ, -1);
-  HDual phi(0.0);
-  // the sweep's carried state is v, a and L of the current body; the root's pose and motion are
-  // recomputed per chain from q_b, and a body's world rotation (its frames) by a walk from the root
-  const double mg[3] = {-M.gravity[0], -M.gravity[1], -M.gravity[2]};
-  const TreeSweep T{M, qb, qrev};
-  if (only_ch < 0 && rb >= 0) {  // the root body's own term (base coordinates only)
-    HDual v1[6], a1[6], f1[6];
-    for (int c = 0; c < 6; ++c) v1[c] = vel[c];
-    T.to_body(0, -1, mg, a1);
-    for (int c = 0; c < 3; ++c) { a1[c] = a1[c] + a[c]; a1[3 + c] = HDual(a[3 + c]); }
-    body_wrench(M.mass[1], M.lever[1], M.Ic[1], a1, v1, f1);
-    body_frames(O, T, 0, -1, 1, type, i, v1, fx, f, lam, p, f1, phi);
-    for (int c = 0; c < 6; ++c) phi += lam[rb + c] * f1[c];
-  }
-  for (int ch = 0; ch < M.nchains; ++ch) {
-    if (only_ch >= 0 && ch != only_ch) continue;
-    const int first = M.chain_first[ch], L = M.chain_len[ch];
-    // the chain's first frame (a foot, or the external force frame): its world force and
-    // velocity-row multipliers are rotated into body axes joint by joint with the sweep's own
-    // rotations (cf, cg) instead of a walk from the root at the frame
-    int ef = -1, ej = -1;
-    for (int e = 0; e < O.nee && ef < 0; ++e) {
-      const int fj = e < O.nfeet ? O.feet[e].joint : O.ext.joint;
-      if (fj >= first && fj < first + L) { ef = e; ej = fj; }
-    }
-    HDual pv[6], pa[6], pL[6], cf[3], cg[3];
-    bool has_mu = false;
-    {
-      HDual R0[9];
-      pl::quat_to_R(qb + 3, R0);
-      pl::mattvec(R0, mg, pa);
-      if (ef >= 0) {
-        const decltype(f(0, 0)) fw[3] = {f(ef, 0), f(ef, 1), f(ef, 2)};
-        pl::mattvec(R0, fw, cf);
-        double mu[3];
-        foot_mu(O, type, i, ef, lam, p, mu, &has_mu);
-        if (has_mu) pl::mattvec(R0, mu, cg);
-      }
-    }
-    for (int c = 0; c < 3; ++c) { pa[c] = pa[c] + a[c]; pa[3 + c] = HDual(a[3 + c]); }
-    for (int c = 0; c < 6; ++c) { pv[c] = vel[c]; pL[c] = HDual(rb >= 0 ? lam[rb + c] : 0.0); }
-    for (int kk = 0; kk < L; ++kk) {
-      const int jt = first + kk;
-      HDual s, c;
-      sincos_s(qrev(M.idx_q[jt]), &s, &c);
-      if (ef >= 0 && jt <= ej) {
-        HDual t3[3];
-        rot_t(M, jt, s, c, cf, t3);
-        for (int q = 0; q < 3; ++q) cf[q] = t3[q];
-        if (has_mu) {
-          rot_t(M, jt, s, c, cg, t3);
-          for (int q = 0; q < 3; ++q) cg[q] = t3[q];
-        }
-      }
-      const double* ax = M.axis[jt];
-      const int iv = M.idx_v[jt];
-      const HDual qd = vel[iv];
-      HDual vj[6], aj[6], t[3];
-      act_inv_j(M, jt, s, c, pv, vj);
-      for (int q = 0; q < 3; ++q) vj[3 + q] += ax[q] * qd;
-      act_inv_j(M, jt, s, c, pa, aj);
-      // + S qdd + v x vJ, vJ = [0; ax qd]:  [v_lin x ax; w x ax] qd
-      crossd(ax, vj, t);
-      for (int q = 0; q < 3; ++q) aj[q] -= t[q] * qd;
-      crossd(ax, vj + 3, t);
-      for (int q = 0; q < 3; ++q) aj[3 + q] += ax[q] * a[iv] - t[q] * qd;
-      for (int q = 0; q < 6; ++q) { pv[q] = vj[q]; pa[q] = aj[q]; }
-      act_inv_j(M, jt, s, c, pL, aj);  // L_j (aj: scratch)
-      const double lj = rt >= 0 ? lam[rt + iv - 6] : 0.0;
-      for (int q = 0; q < 3; ++q) aj[3 + q] += ax[q] * lj;
-      for (int q = 0; q < 6; ++q) pL[q] = aj[q];
-      HDual fj[6];
-      body_wrench(M.mass[jt], M.lever[jt], M.Ic[jt], pa, pv, fj);
-      body_frames(O, T, first, kk, jt, type, i, pv, fx, f, lam, p, fj, phi, ef, cf, cg, has_mu);
-      for (int q = 0; q < 6; ++q) phi += pL[q] * fj[q];
-    }
-  }
-  double acc = phi.c;
-  *H = acc;
+  d.Hlag[(size_t)b * hl_stride + d.hoff[i] + k * (k + 1) / 2 + j] =
+      tree_pair<SF>(*d.model, *d.oc, i, only_ch, j, k, d.x + (size_t)b * n + nd.x_off, d.p + (size_t)b * np,
+                    d.ip_lam + (size_t)b * m + nd.row_off);
+}
+
+// r06: the (dq, dq) and (dq, dv) pairs by forward-over-reverse columns (hess_tree.h tree_col): one work
+// item per (node, chain, dq column j) with the mask of its pairs' other coordinates (api.hip
+// set_solver groups d.htr that way: every pair is written by the item of its smaller index j), one item
+// per wave, one problem per lane.  PL_PATH_HESS_PAIRS keeps k_lag_hess_tree<false> per pair.
+__global__ __launch_bounds__(64) void k_lag_hess_col(PlDev d, int B, int n, int m, int np, long long hl_stride) {
+  const int qa = blockIdx.y * 64 + threadIdx.x;
+  if (qa >= d.ip_act[B]) return;
+  const int b = d.ip_act[qa];
+  const int4 w = d.hcol[blockIdx.x];
+  const int wx = __builtin_amdgcn_readfirstlane(w.x);
+  const int i = wx & 0xffff, only_ch = (wx >> 16) - 1;
+  const int j = __builtin_amdgcn_readfirstlane(w.y);
+  const uint32_t mask = (uint32_t)__builtin_amdgcn_readfirstlane(w.z);
+  const PlNode nd = d.nodes[i];
+  double* H = d.Hlag + (size_t)b * hl_stride + d.hoff[i];
+  tree_col(*d.model, *d.oc, i, only_ch, j, mask, d.x + (size_t)b * n + nd.x_off, d.p + (size_t)b * np,
+           d.ip_lam + (size_t)b * m + nd.row_off, [&](int k, double v) {
+             const int hi = k > j ? k : j, lo = k > j ? j : k;
+             H[hi * (hi + 1) / 2 + lo] = v;
+           });
 }
 
 
@@ -689,7 +416,10 @@ void launch_lag_hess(PlOcpHandle* h) {
     hipLaunchKernelGGL(k_lag_hess_vv, dim3(h->hvv_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,
                        h->m, h->np, h->hl_stride, make_int3(h->hl_rb_base[0], h->hl_rb_base[1], h->hl_rb_base[2]),
                        make_int3(h->hl_rb_tau[0], h->hl_rb_tau[1], h->hl_rb_tau[2]));
-  if (h->htr_len > 0)
+  if (h->hcol_len > 0)
+    hipLaunchKernelGGL(k_lag_hess_col, dim3(h->hcol_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,
+                       h->m, h->np, h->hl_stride);
+  else if (h->htr_len > 0)
     hipLaunchKernelGGL(k_lag_hess_tree<false>, dim3(h->htr_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B,
                        h->n, h->m, h->np, h->hl_stride);
   if (h->htr_len > 0 && h->oc.arm.valid)

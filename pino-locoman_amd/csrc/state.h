@@ -232,6 +232,8 @@ struct PlDev {
   int2* hcone;       // whole_body_rnea / whole_body_acc: (node, foot-force column) of the cone curvature (k_lag_hess_cone)
   int2* htrf;        // the (dq, external force) pairs (k_lag_hess_tree<true>)
   int2* htr;         // whole_body_rnea / whole_body_acc: the (dq, dq) and (dq, dv) pairs (k_lag_hess_tree)
+  int4* hcol;        // the same pairs as forward-over-reverse columns (k_lag_hess_col): (node | (chain + 1) << 16,
+                     // column j, mask of the other coordinates (hess_tree.h col_coord), 0)
   int2* hvv;         // whole_body_rnea / whole_body_acc: the (dv, dv) pairs, packed as hlist (k_lag_hess_vv)
   int2* hlin;        // whole_body_rnea: (node, dq column k) of the linear-column Hessian blocks (k_lag_hess_lin)
   PlModel* model0;   // the model with zero gravity (M(q) lambda by an RNEA pass at v = 0)
@@ -293,6 +295,7 @@ struct PlOcpHandle {
   int hcone_len;                    // k_lag_hess_cone work list
   int htrf_len;                     // k_lag_hess_tree<true> work list
   int htr_len;                      // k_lag_hess_tree work list
+  int hcol_len;                     // k_lag_hess_col work list (0: the pair kernel runs)
   int hvv_len;                      // k_lag_hess_vv work list
   int hlin_len;                     // k_lag_hess_lin work list (0: every pair by hyper-dual passes)
   int hl_rb_base[3], hl_rb_tau[3];  // per node type: first row of the RNEA base / joint-torque rows (-1: none)

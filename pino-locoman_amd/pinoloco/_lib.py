@@ -41,7 +41,8 @@ class OcpDesc(C.Structure):
 # pl_ocp_desc.debug_paths bits (include/pinoloco.h PL_PATH_*): the earlier builds' paths the
 # regression tests compare with, and the phase-timing instrumentation; 0 in production
 PATHS = {"jac_dual_all": 1, "jac_const_every": 2, "hess_full_tree": 4, "hess_dual_all": 8, "fchain_list": 16,
-         "ruiz_per_pass": 32, "no_mpc_graph": 64, "admm_timing": 128, "ip_refine_gather": 256}
+         "ruiz_per_pass": 32, "no_mpc_graph": 64, "admm_timing": 128, "ip_refine_gather": 256,
+         "hess_pairs": 512}
 
 
 class Stats(C.Structure):

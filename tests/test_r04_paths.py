@@ -65,7 +65,9 @@ def test_hessian_rewrites_match_full_pairs(name, rname, dyn, N):
     G = golden(f"{name}.npz")
     gait = str(G["gait"])
     H = {}
-    for tag, paths in (("new", ()), ("old", ("hess_full_tree", "hess_dual_all"))):
+    # new: the r06 forward-over-reverse columns (k_lag_hess_col); pairs: the r05 hyper-dual pair
+    # sweeps (PL_PATH_HESS_PAIRS); old: every pair in hyper-dual node rows over the whole tree (r04)
+    for tag, paths in (("new", ()), ("pairs", ("hess_pairs",)), ("old", ("hess_full_tree", "hess_dual_all"))):
         ib = bool(int(G["include_base"])) if "include_base" in G else True
         R = make_robot(rname, gait)
         bo = BatchedOCP(R, dyn, N, batch=1, device=0, gait_type=gait, include_base=ib, debug_paths=paths)
@@ -79,6 +81,7 @@ def test_hessian_rewrites_match_full_pairs(name, rname, dyn, N):
         bo.close()
     d = abs(H["new"] - H["old"]).max()
     assert d <= 1e-12 * abs(H["old"]).max()
+    assert abs(H["new"] - H["pairs"]).max() <= 1e-13 * abs(H["pairs"]).max()
 
 
 @pytest.mark.parametrize("name,rname,dyn,N", [("b2_aba_n40", "b2", "whole_body_aba", 40),
