@@ -74,8 +74,8 @@ def admm_bytes_per_problem_iter(sz, node_table, padded=False, kernel="sweep", nd
 
 
 HESS_FLOPS_FILE = os.path.join(HERE, "profiles", "traffic", "hess_flops.json")
-HESS_SOURCES = ("pino-locoman_amd/csrc/k_hess.hip", "pino-locoman_amd/csrc/rows.h", "pino-locoman_amd/csrc/rbd.h",
-                "pino-locoman_amd/csrc/ad.h", "pino-locoman_amd/csrc/targets.h")
+HESS_SOURCES = ("pino-locoman_amd/csrc/k_hess.hip", "pino-locoman_amd/csrc/hess_tree.h", "pino-locoman_amd/csrc/rows.h",
+                "pino-locoman_amd/csrc/rbd.h", "pino-locoman_amd/csrc/ad.h", "pino-locoman_amd/csrc/targets.h")
 FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 vector (MI355X_MICROARCH.md)
 
 
@@ -469,8 +469,8 @@ def main():
             ach = flops / (h_avg * 1e-3) / 1e12 if (hf and h_avg > 0) else None
             out["admm_roofline"] = out["roofline"]
             out["roofline"] = {"bound": "fp64_valu",
-                               "kernel": "Lagrangian Hessian (k_lag_hess_tree + _vv + _lin + _cone; k_lag_hess_pb "
-                                         "off the rnea family)",
+                               "kernel": "Lagrangian Hessian (k_lag_hess_col + _arm + _lin + _vv + _tree<true> + _cone; "
+                                         "k_lag_hess_pb off the rnea family)",
                                "mapping": "sweep", "achieved": ach,
                                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                                "frac": ach / FP64_PEAK_TFLOPS if ach is not None else None, "traffic": None,
