@@ -888,10 +888,15 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
         if (lk < 0) { ok = false; break; }
         cols[((long long)i << 32) | ((long long)(ch + 1) << 16) | j] |= 1u << lk;
       }
+      h->hcol_nbase = 0;
       if (ok)
-        for (const auto& kv : cols)
-          hcol.push_back(make_int4((int)(kv.first >> 32) | (int)(((kv.first >> 16) & 0xffff) << 16),
-                                   (int)(kv.first & 0xffff), (int)kv.second, 0));
+        for (int pass = 0; pass < 2; ++pass)  // the whole-tree base columns first (k_lag_hess_col<true>)
+          for (const auto& kv : cols) {
+            const int chp = (int)((kv.first >> 16) & 0xffff);
+            if ((chp == 0) != (pass == 0)) continue;
+            hcol.push_back(make_int4((int)(kv.first >> 32) | (chp << 16), (int)(kv.first & 0xffff), (int)kv.second, 0));
+            if (pass == 0) ++h->hcol_nbase;
+          }
     }
     h->hcol_len = (int)hcol.size();
     h->hl_len = (int)hl.size();

@@ -400,7 +400,10 @@ template <class S> PL_HD S ang_adj(const double* ax, const S* y, const S* yb) {
 // d^2 phi / dx_j dx_k for every coordinate k of the chain at once.  The base rotation's adjoint
 // goes through R0: d phi / dw_k = Rbar0 : dR0 / dw_k with dR0 / dw_k and d^2 R0 / dw_j dw_k from
 // a hyper-dual evaluation of the root pose.
-template <class W>
+// WHOLE: the whole-tree base columns (only_ch < 0: the root term, every chain and the base rotation's
+// adjoint); otherwise one chain, whose columns never write a base-rotation entry (the register
+// budget of the chain items then holds no R0 adjoint).
+template <bool WHOLE, class W>
 PL_HD void tree_col(const PlModel& M, const PlOcpConst& O, int i, int only_ch, int j, uint32_t mask, const double* x,
                     const double* p, const double* lam, W&& write) {
   const auto kidx = [&](int loc) { return col_coord(M, O, only_ch, loc); };
@@ -424,10 +427,10 @@ PL_HD void tree_col(const PlModel& M, const PlOcpConst& O, int i, int only_ch, i
   const double* fx = x + ndx + O.na;
   const int rb = block_row(O, type, PL_RB_RNEA_BASE, -1), rt = block_row(O, type, PL_RB_TAU_EQ, -1);
   const double mg[3] = {-M.gravity[0], -M.gravity[1], -M.gravity[2]};
-  Dual R0b[9], v0b[6];  // adjoints of R0 and of the base velocity
-  for (int q = 0; q < 9; ++q) R0b[q] = Dual(0.0);
+  Dual R0b[WHOLE ? 9 : 1], v0b[6];  // adjoints of R0 (whole-tree columns) and of the base velocity
+  for (int q = 0; q < (WHOLE ? 9 : 1); ++q) R0b[q] = Dual(0.0);
   for (int q = 0; q < 6; ++q) v0b[q] = Dual(0.0);
-  if (only_ch < 0 && rb >= 0) {  // the root body's own term: phi += lam_b . body_wrench(a1, v1)
+  if (WHOLE && rb >= 0) {  // the root body's own term: phi += lam_b . body_wrench(a1, v1)
     Dual v1[6], a1b[6], v1b[6], fb[6];
     for (int c = 0; c < 6; ++c) { v1[c] = vel[c]; a1b[c] = Dual(0.0); v1b[c] = Dual(0.0); fb[c] = Dual(lam[rb + c]); }
     body_wrench_adj(M.mass[1], M.lever[1], M.Ic[1], v1, fb, a1b, v1b);
@@ -435,8 +438,7 @@ PL_HD void tree_col(const PlModel& M, const PlOcpConst& O, int i, int only_ch, i
     for (int r = 0; r < 3; ++r)  // a1_lin = R0^T mg + a
       for (int c = 0; c < 3; ++c) R0b[3 * r + c] += mg[r] * a1b[c];
   }
-  for (int ch = 0; ch < M.nchains; ++ch) {
-    if (only_ch >= 0 && ch != only_ch) continue;
+  for (int ch = WHOLE ? 0 : only_ch; ch < (WHOLE ? M.nchains : only_ch + 1); ++ch) {
     const int first = M.chain_first[ch], L = M.chain_len[ch];
     int ef = -1, ej = -1;
     for (int e = 0; e < O.nee && ef < 0; ++e) {
@@ -566,18 +568,20 @@ PL_HD void tree_col(const PlModel& M, const PlOcpConst& O, int i, int only_ch, i
         rot_j(M, jt, s, c, cgb, t);
         for (int q = 0; q < 3; ++q) cgb[q] = t[q];
       }
-      if (only_ch >= 0) {
+      if (!WHOLE) {
         if (mask >> (12 + kk) & 1u) write(iv, thb.d);            // dq of joint jt
         if (mask >> (12 + L + kk) & 1u) write(nv + iv, qdb.d);   // dv of joint jt
       }
     }
     // the chain's root state: v_0 = vel (base), a_0 = R0^T mg + a, cf_0 = R0^T f, cg_0 = R0^T mu
     for (int q = 0; q < 6; ++q) v0b[q] += vb[q];
-    for (int r = 0; r < 3; ++r)
-      for (int c = 0; c < 3; ++c) R0b[3 * r + c] += mg[r] * ab[c] + fw[r] * cfb[c] + mu[r] * cgb[c];
+    if constexpr (WHOLE)
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) R0b[3 * r + c] += mg[r] * ab[c] + fw[r] * cfb[c] + mu[r] * cgb[c];
   }
   for (int c = 0; c < 6; ++c)
     if (mask >> (6 + c) & 1u) write(nv + c, v0b[c].d);
+  if constexpr (!WHOLE) return;
   for (int k = 3; k < 6; ++k) {  // the base rotation (whole-tree columns)
     if (!(mask >> k & 1u)) continue;
     const VecIn<HDual> hx{x, nullptr, 0.0, j, k};

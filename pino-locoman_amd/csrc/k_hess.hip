@@ -242,18 +242,20 @@ __global__ __launch_bounds__(64) void k_lag_hess_tree(PlDev d, int B, int n, int
 // item per (node, chain, dq column j) with the mask of its pairs' other coordinates (api.hip
 // set_solver groups d.htr that way: every pair is written by the item of its smaller index j), one item
 // per wave, one problem per lane.  PL_PATH_HESS_PAIRS keeps k_lag_hess_tree<false> per pair.
-__global__ __launch_bounds__(64) void k_lag_hess_col(PlDev d, int B, int n, int m, int np, long long hl_stride) {
+template <bool WHOLE>
+__global__ __launch_bounds__(64) void k_lag_hess_col(PlDev d, int B, int n, int m, int np, long long hl_stride,
+                                                     int item0) {
   const int qa = blockIdx.y * 64 + threadIdx.x;
   if (qa >= d.ip_act[B]) return;
   const int b = d.ip_act[qa];
-  const int4 w = d.hcol[blockIdx.x];
+  const int4 w = d.hcol[item0 + blockIdx.x];
   const int wx = __builtin_amdgcn_readfirstlane(w.x);
   const int i = wx & 0xffff, only_ch = (wx >> 16) - 1;
   const int j = __builtin_amdgcn_readfirstlane(w.y);
   const uint32_t mask = (uint32_t)__builtin_amdgcn_readfirstlane(w.z);
   const PlNode nd = d.nodes[i];
   double* H = d.Hlag + (size_t)b * hl_stride + d.hoff[i];
-  tree_col(*d.model, *d.oc, i, only_ch, j, mask, d.x + (size_t)b * n + nd.x_off, d.p + (size_t)b * np,
+  tree_col<WHOLE>(*d.model, *d.oc, i, only_ch, j, mask, d.x + (size_t)b * n + nd.x_off, d.p + (size_t)b * np,
            d.ip_lam + (size_t)b * m + nd.row_off, [&](int k, double v) {
              const int hi = k > j ? k : j, lo = k > j ? j : k;
              H[hi * (hi + 1) / 2 + lo] = v;
@@ -416,10 +418,14 @@ void launch_lag_hess(PlOcpHandle* h) {
     hipLaunchKernelGGL(k_lag_hess_vv, dim3(h->hvv_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,
                        h->m, h->np, h->hl_stride, make_int3(h->hl_rb_base[0], h->hl_rb_base[1], h->hl_rb_base[2]),
                        make_int3(h->hl_rb_tau[0], h->hl_rb_tau[1], h->hl_rb_tau[2]));
-  if (h->hcol_len > 0)
-    hipLaunchKernelGGL(k_lag_hess_col, dim3(h->hcol_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,
-                       h->m, h->np, h->hl_stride);
-  else if (h->htr_len > 0)
+  if (h->hcol_len > 0) {  // the whole-tree base columns first, then the chain columns
+    if (h->hcol_nbase > 0)
+      hipLaunchKernelGGL(k_lag_hess_col<true>, dim3(h->hcol_nbase, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d,
+                         h->B, h->n, h->m, h->np, h->hl_stride, 0);
+    if (h->hcol_len > h->hcol_nbase)
+      hipLaunchKernelGGL(k_lag_hess_col<false>, dim3(h->hcol_len - h->hcol_nbase, (h->B + 63) / 64), dim3(64), 0,
+                         h->stream, h->d, h->B, h->n, h->m, h->np, h->hl_stride, h->hcol_nbase);
+  } else if (h->htr_len > 0)
     hipLaunchKernelGGL(k_lag_hess_tree<false>, dim3(h->htr_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B,
                        h->n, h->m, h->np, h->hl_stride);
   if (h->htr_len > 0 && h->oc.arm.valid)

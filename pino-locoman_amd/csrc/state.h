@@ -296,6 +296,7 @@ struct PlOcpHandle {
   int htrf_len;                     // k_lag_hess_tree<true> work list
   int htr_len;                      // k_lag_hess_tree work list
   int hcol_len;                     // k_lag_hess_col work list (0: the pair kernel runs)
+  int hcol_nbase;                   // its first hcol_nbase items are the whole-tree base columns
   int hvv_len;                      // k_lag_hess_vv work list
   int hlin_len;                     // k_lag_hess_lin work list (0: every pair by hyper-dual passes)
   int hl_rb_base[3], hl_rb_tau[3];  // per node type: first row of the RNEA base / joint-torque rows (-1: none)

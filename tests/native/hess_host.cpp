@@ -18,7 +18,8 @@ extern "C" void th_hess_col(const void* model, const void* oc, int i, int only_c
   PlModel M; PlOcpConst O;
   memcpy(&M, model, sizeof(M));
   memcpy(&O, oc, sizeof(O));
-  hess::tree_col(M, O, i, only_ch, j, mask, x, p, lam, [&](int k, double v) { out[k] = v; });
+  if (only_ch < 0) hess::tree_col<true>(M, O, i, only_ch, j, mask, x, p, lam, [&](int k, double v) { out[k] = v; });
+  else hess::tree_col<false>(M, O, i, only_ch, j, mask, x, p, lam, [&](int k, double v) { out[k] = v; });
 }
 
 extern "C" int th_col_coord(const void* model, const void* oc, int only_ch, int loc) {

@@ -83,7 +83,12 @@ def test_columns_match_pairs(harness, rname, dyn, N, nodes):
                 nloc = 12 if ch < 0 else 12 + 2 * H.th_chain_len(mb, ch)
                 coords = [H.th_col_coord(mb, ob, ch, loc) for loc in range(nloc)]
                 for j in [c for c in coords if c < bo.layout.ndx // 2]:  # the dq columns (htr pairs: j < nv)
-                    locs = [loc for loc, k in enumerate(coords) if k >= j]
+                    # the pairs a work item of this kind writes (api.hip set_solver): the whole-tree items
+                    # the base pairs; a chain item with a base-rotation column j its chain's coordinates,
+                    # with a chain column also the base velocities (the base-base pairs are whole-tree)
+                    jchain = ch >= 0 and coords.index(j) >= 12
+                    locs = [loc for loc, k in enumerate(coords) if k >= j and
+                            (ch < 0 or loc >= 12 or (jchain and 6 <= loc < 12))]
                     mask = sum(1 << loc for loc in locs)
                     out = np.full(bo.layout.ndx, np.nan)
                     H.th_hess_col(mb, ob, i, ch, j, mask, _d(xi), _d(p), _d(lam), _d(out))
