@@ -899,6 +899,20 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
           }
     }
     h->hcol_len = (int)hcol.size();
+    // k_lag_hess_arm's pairs: those on the base or the arm's chain (the others have no arm-row curvature;
+    // until r05 their waves ran and exited)
+    std::vector<int2> harm;
+    {
+      int arm_ch = -1;
+      for (int c = 0; c < Mo.nchains; ++c)
+        if (O.arm.valid && O.arm.joint >= Mo.chain_first[c] && O.arm.joint < Mo.chain_first[c] + Mo.chain_len[c]) arm_ch = c;
+      if (arm_ch >= 0)
+        for (const int2& pr : htr) {
+          const int ch = (pr.x >> 16) - 1;
+          if (ch < 0 || ch == arm_ch) harm.push_back(pr);
+        }
+    }
+    h->harm_len = (int)harm.size();
     h->hl_len = (int)hl.size();
     h->hlin_len = (int)hlin.size();
     h->hvv_len = (int)hvv.size();
@@ -914,7 +928,8 @@ extern "C" int pl_ocp_set_solver(pl_ocp* o, int solver) {
       for (int k = 0; k < 3; ++k) m0.gravity[k] = 0.0;
       if (upload(o, &h->d.hlin, hlin) || (!hvv.empty() && upload(o, &h->d.hvv, hvv)) ||
           (!htr.empty() && upload(o, &h->d.htr, htr)) || (!hcone.empty() && upload(o, &h->d.hcone, hcone)) ||
-          (!htrf.empty() && upload(o, &h->d.htrf, htrf)) || (!hcol.empty() && upload(o, &h->d.hcol, hcol)))
+          (!htrf.empty() && upload(o, &h->d.htrf, htrf)) || (!hcol.empty() && upload(o, &h->d.hcol, hcol)) ||
+          (!harm.empty() && upload(o, &h->d.harm, harm)))
         return -2;
       if (!h->d.model0 && (dalloc(o, &h->d.model0, 1) ||
                            hipMemcpy(h->d.model0, &m0, sizeof(PlModel), hipMemcpyHostToDevice) != hipSuccess))

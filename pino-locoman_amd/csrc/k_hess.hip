@@ -272,7 +272,7 @@ __global__ __launch_bounds__(64) void k_lag_hess_arm(PlDev d, int B, int n, int 
   const int b = d.ip_act[qa];
   const PlOcpConst& O = *d.oc;
   const PlModel& M = *d.model;
-  const int2 w = d.htr[blockIdx.x];
+  const int2 w = d.harm[blockIdx.x];  // the pairs on the base or the arm's chain (r06; d.htr until r05)
   const int wx = __builtin_amdgcn_readfirstlane(w.x);
   const int i = wx & 0xffff, only_ch = (wx >> 16) - 1;
   const int jk = __builtin_amdgcn_readfirstlane(w.y);
@@ -428,8 +428,8 @@ void launch_lag_hess(PlOcpHandle* h) {
   } else if (h->htr_len > 0)
     hipLaunchKernelGGL(k_lag_hess_tree<false>, dim3(h->htr_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B,
                        h->n, h->m, h->np, h->hl_stride);
-  if (h->htr_len > 0 && h->oc.arm.valid)
-    hipLaunchKernelGGL(k_lag_hess_arm, dim3(h->htr_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,
+  if (h->harm_len > 0 && h->oc.arm.valid)
+    hipLaunchKernelGGL(k_lag_hess_arm, dim3(h->harm_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B, h->n,
                        h->m, h->np, h->hl_stride);
   if (h->htrf_len > 0)
     hipLaunchKernelGGL(k_lag_hess_tree<true>, dim3(h->htrf_len, (h->B + 63) / 64), dim3(64), 0, h->stream, h->d, h->B,

@@ -232,6 +232,7 @@ struct PlDev {
   int2* hcone;       // whole_body_rnea / whole_body_acc: (node, foot-force column) of the cone curvature (k_lag_hess_cone)
   int2* htrf;        // the (dq, external force) pairs (k_lag_hess_tree<true>)
   int2* htr;         // whole_body_rnea / whole_body_acc: the (dq, dq) and (dq, dv) pairs (k_lag_hess_tree)
+  int2* harm;        // the pairs of d.htr on the base or the arm's chain (k_lag_hess_arm)
   int4* hcol;        // the same pairs as forward-over-reverse columns (k_lag_hess_col): (node | (chain + 1) << 16,
                      // column j, mask of the other coordinates (hess_tree.h col_coord), 0)
   int2* hvv;         // whole_body_rnea / whole_body_acc: the (dv, dv) pairs, packed as hlist (k_lag_hess_vv)
@@ -296,6 +297,7 @@ struct PlOcpHandle {
   int htrf_len;                     // k_lag_hess_tree<true> work list
   int htr_len;                      // k_lag_hess_tree work list
   int hcol_len;                     // k_lag_hess_col work list (0: the pair kernel runs)
+  int harm_len;                     // k_lag_hess_arm work list
   int hcol_nbase;                   // its first hcol_nbase items are the whole-tree base columns
   int hvv_len;                      // k_lag_hess_vv work list
   int hlin_len;                     // k_lag_hess_lin work list (0: every pair by hyper-dual passes)
