@@ -284,6 +284,8 @@ def main():
     ap.add_argument("--dry-run", action="store_true", help="gloo plumbing only, no GPU")
     ap.add_argument("--admm-kernel", default="auto", choices=["auto", "sweep", "sweep2", "chain"],
                     help="ADMM mapping (pl_ocp_set_admm_kernel); auto = the library's batch-size rule")
+    ap.add_argument("--debug-paths", default="",
+                    help="comma list of pl_ocp_desc.debug_paths names (earlier kernel paths, A/B runs only)")
     ap.add_argument("--host-io-steps", type=int, default=None,
                     help="extra steps timed with the per-step D2H of [u_0, x_state] (default min(steps, 10))")
     args = ap.parse_args()
@@ -310,7 +312,9 @@ def main():
     B = args.batch
     first, _ = shard(B * world, world, rank)
     lay, P, X, XS, T0 = build_batch(R, args.dynamics, args.nodes, B, first)
-    bo = BatchedOCP(R, args.dynamics, args.nodes, batch=B, device=local_rank, gait_type="trot", gait_period=0.8)
+    paths = tuple(p for p in args.debug_paths.split(",") if p)
+    bo = BatchedOCP(R, args.dynamics, args.nodes, batch=B, device=local_rank, gait_type="trot", gait_period=0.8,
+                    debug_paths=paths)
     if args.solver == "fatrop":
         bo.set_solver("fatrop")
         bo.set_ip_settings()
@@ -436,8 +440,9 @@ def main():
                        "dynamics": args.dynamics,
                        "solver": ("osqp-sqp (1 SQP iteration, max_iter 100)" if args.solver == "osqp" else
                                   "fatrop-equivalent interior point (max_iter 10, tol 1e-3, mu_init 1e-4)"),
-                       "parallelism": f"batch-sharded dp{world}"},
-            "roofline": {"bound": "hbm", "kernel": kname, "byte_model": kernel, "achieved": achieved,
+                       "parallelism": f"batch-sharded dp{world}", **({"debug_paths": list(paths)} if paths else {})},
+            "roofline": {"bound": "hbm", "kernel": kname, "byte_model": kernel, "workgroups_per_problem": bo.admm_groups(),
+                         "achieved": achieved,
                          "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": per_launch_bytes,

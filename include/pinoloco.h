@@ -120,7 +120,9 @@ typedef struct {
 #define PL_PATH_IP_REFINE_GATHER 256u /* k_ip_refine's H_i dx by the per-column global gather (the nw > 192 path) */
 #define PL_PATH_HESS_PAIRS      512u /* the (dq, dq) / (dq, dv) Hessian pairs by one hyper-dual sweep each (r05), not
                                         the forward-over-reverse columns */
-#define PL_PATH_ALL             1023u /* pl_ocp_create rejects any other bit: callers zero the struct */
+#define PL_PATH_RC_ONE_GROUP    1024u /* the chain ADMM kernel on one workgroup per problem (r05), not the
+                                         multi-workgroup node phases */
+#define PL_PATH_ALL             2047u /* pl_ocp_create rejects any other bit: callers zero the struct */
 
 typedef struct {
   int status;                  /* OSQP status code (1 solved, 2 inaccurate, -2 max iter, ...) */
@@ -326,6 +328,10 @@ int pl_dyn_eval(pl_dyn* d, int fn, int batch, int frame, int flags, const double
 #define PL_ADMM_CHAIN 3
 int pl_ocp_set_admm_kernel(pl_ocp* o, int kind);
 int pl_ocp_get_admm_kernel(const pl_ocp* o);
+/* Workgroups per problem of the next ADMM launch: 1 for the sweep kernels; for the chain kernel
+ * ceil((N + 1) / 8) while the batch's workgroups fit one per CU, else fewer (1 under
+ * PL_PATH_RC_ONE_GROUP). */
+int pl_ocp_get_admm_groups(const pl_ocp* o);
 
 /* Timing of the dominant kernel (ADMM sweeps) with HIP events on the handle's
  * stream: pl_ocp_profile(o, 1) clears and starts, pl_ocp_profile_read returns

@@ -120,7 +120,8 @@ extern "C" void pl_model_destroy(pl_model* m) { delete m; }
 // ADMM kernel selection (the three give the same iterates to round-off):
 //   sweep   k_admm: one wave per problem, node-by-node block sweeps (HBM-bound at B >= 1024)
 //   sweep2  k_admm2: two waves per problem
-//   chain   k_admm_rc: reduced chain, one workgroup of 8 waves per problem (small batches)
+//   chain   k_admm_rc: reduced chain, 8 waves per problem (small batches); up to ceil((N + 1) / 8)
+//           workgroups per problem while the batch's workgroups fit one per CU (rc_groups)
 // AUTO: chain up to PL_ADMM_CHAIN_MAX_B problems when supported, else sweep2 up to 512
 // problems (idle SIMDs below 4 x 256), else sweep.  The chain
 // buffers are allocated on first selection.
@@ -134,7 +135,9 @@ int admm_select(pl_ocp* o, int kind) {
   if (kind == PL_ADMM_SWEEP2 && !admm2_supported(&h)) { pl_set_error("sweep2 ADMM kernel does not support this OCP"); return -1; }
   if (kind == PL_ADMM_CHAIN && !admm_rc_supported(&h)) { pl_set_error("chain ADMM kernel does not support this OCP"); return -1; }
   if (kind == PL_ADMM_CHAIN && o->on_device && !h.d.CH) {
-    if (dalloc(o, &h.d.CH, (size_t)h.B * h.ch_stride) || dalloc(o, &h.d.chv, (size_t)h.B * h.chv_stride)) return -2;
+    if (dalloc(o, &h.d.CH, (size_t)h.B * h.ch_stride) || dalloc(o, &h.d.chv, (size_t)h.B * h.chv_stride) ||
+        dalloc(o, &h.d.rcsync, (size_t)h.B * PL_RC_SYNC))
+      return -2;
   }
   h.admm_rc = kind == PL_ADMM_CHAIN ? 1 : 0;
   h.admm_waves = kind == PL_ADMM_SWEEP2 ? 2 : 1;
@@ -270,6 +273,8 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
     delete o;
     return -2;
   }
+  if (hipDeviceGetAttribute(&h.num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || h.num_cu <= 0)
+    h.num_cu = 1;  // unknown: k_admm_rc then runs one workgroup per problem
   if (hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking) != hipSuccess) {
     pl_set_error("hipStreamCreate failed");
     delete o;
@@ -570,6 +575,11 @@ extern "C" int pl_ocp_set_admm_kernel(pl_ocp* o, int kind) {
 extern "C" int pl_ocp_get_admm_kernel(const pl_ocp* o) {
   if (!o) { pl_set_error("null handle"); return -1; }
   return o->h.admm_rc ? PL_ADMM_CHAIN : (o->h.admm_waves == 2 ? PL_ADMM_SWEEP2 : PL_ADMM_SWEEP);
+}
+
+extern "C" int pl_ocp_get_admm_groups(const pl_ocp* o) {
+  if (!o) { pl_set_error("null handle"); return -1; }
+  return o->h.admm_rc ? rc_groups(&o->h) : 1;
 }
 
 extern "C" int pl_ocp_set_sqp_iters(pl_ocp* o, int sqp_iters) {

@@ -31,9 +31,27 @@
 // Determinism: fixed node -> wave assignment, fixed per-lane summation orders and LDS f64
 // adds applied in instruction order, so a problem gives the same bits in any batch that
 // selects this kernel (the sweep kernels sum in other orders: results agree to round-off).
+//
+// Several workgroups per problem (r06, rc_groups).  The node-parallel phases P / P3 spread
+// over G workgroups of W waves (node i on wave i mod (G W)), so the 21 Go2 nodes of config 2
+// run in one round instead of three; the chains stay on workgroup 0.  The phases hand off
+// through global memory inside the launch (MI355X_MICROARCH.md, inter-workgroup visibility):
+//   fan-in   every workgroup g > 0, after its nodes: each wave s_waitcnt vmcnt(0), workgroup
+//            barrier, one agent-scope atomic add to the problem's count; workgroup 0 polls it;
+//   fan-out  workgroup 0, after the chains: the same drain, then one agent-scope store of the
+//            iteration's epoch, which the others poll.
+// Every handed-off value (c'_i, h'_i, a2_i from the nodes; delta_i, e_i from the chains; the
+// last iteration's rhs) is stored write-through (sc1) and loaded sc1 (st_sc1 / ld_sc1: L2,
+// never a stale L1 line), so no fence is needed.  Every poll is bounded: a workgroup that gives
+// up writes a code into the problem's give-up word, poisons x (NaN) and exits, and a waiting
+// workgroup that sees the word exits too.  All B G workgroups are resident together: rc_groups
+// keeps B G <= the CU count (the kernel's LDS allows one workgroup per CU).  G = 1 is the r05
+// kernel (PL_PATH_RC_ONE_GROUP); the node arithmetic does not depend on G, so the iterates are
+// bit-identical for any G.
 #include <algorithm>
 
 #include "admm_common.h"
+#include "pinoloco.h"  // PL_PATH_RC_ONE_GROUP
 #include "state.h"
 
 namespace {
@@ -44,6 +62,41 @@ struct RcLds {
   int prog_dbl, chn, per_wave;  // programs | chain buffers [2][64] | per-wave regions
   int v, y, acc, trow, tcpl, bc, asb, asb_cap;
 };
+
+// Handed-off values: write-through stores / L1-bypassing loads (buffer_{store,load}_dwordx2 sc1).
+// Buffer ops, not relaxed atomics: the LDS-only barriers of the chains carry an acquire fence, and
+// an acquire after an atomic load makes the compiler wait vmcnt(0), draining the chain-block
+// prefetch every step.
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+constexpr int RC_SC1 = 16;  // cache-policy bits of the buffer ops: sc1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rc_rsrc(const double* base, int count) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0, count * 8, 0x00020000);
+}
+__device__ __forceinline__ double ld_sc1(__amdgpu_buffer_rsrc_t r, int idx) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, idx * 8, 0, RC_SC1));
+}
+__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, int idx, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, idx * 8, 0, RC_SC1);
+}
+
+// hand-off words of one problem (d.rcsync, zeroed before every launch)
+enum { RC_ARRIVE = 0, RC_EPOCH = 1, RC_GIVEUP = 2 };
+constexpr unsigned RC_SPIN_MAX = 1u << 21;  // polls (s_sleep 2 each) before a workgroup gives up
+
+// One wave polls *w >= target (relaxed sc1 loads); false when the give-up word is set or after
+// RC_SPIN_MAX polls (then it sets the word to `code`).
+__device__ __forceinline__ bool rc_poll(unsigned* sy, int word, unsigned target, unsigned code) {
+  for (unsigned s = 0;; ++s) {
+    if (__hip_atomic_load((gu32*)(sy + word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+    if (__hip_atomic_load((gu32*)(sy + RC_GIVEUP), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
+    if (s >= RC_SPIN_MAX) {
+      __hip_atomic_store((gu32*)(sy + RC_GIVEUP), code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
 
 struct Sb {
   double2 s[KM][8];
@@ -64,6 +117,15 @@ struct RcChain {
   static constexpr int SG = X / NS;
   static constexpr int PD = (W >= 8 ? 72 : 144) / SG < 2 ? 2 : ((W >= 8 ? 72 : 144) / SG > 10 ? 10 : (W >= 8 ? 72 : 144) / SG);
 };
+
+// An explicit copy out of a prefetch slot before its refill is issued: otherwise the compiler may
+// load the refill into other registers and move it into the slot at the loop latch, which waits
+// vmcnt(0) on the refill and drains the prefetch every chain step.
+__device__ __forceinline__ double slot_copy(double x) {
+  double y;
+  asm volatile("v_mov_b64 %0, %1" : "=v"(y) : "v"(x));
+  return y;
+}
 
 // Workgroup barrier that orders LDS only (lgkmcnt(0) + s_barrier): __syncthreads() would also
 // wait vmcnt(0) and drain the chain blocks kept in flight across the steps.
@@ -136,11 +198,11 @@ __global__ __launch_bounds__(256) void k_fred(PlDev d, int N, int nnz, int ndx, 
 template <int W, int X>
 __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, int m, int nnz, int S_stride,
                                                        int cpl_stride, long long ch_stride, int chv_stride, RcLds lm,
-                                                       int niter, int check, double sigma, double alpha) {
+                                                       int niter, int check, double sigma, double alpha, int G) {
   extern __shared__ double lds[];
-  const int b = blockIdx.x;
+  const int b = blockIdx.x / G, g = blockIdx.x - b * G;  // problem, workgroup of the problem
   PlProbInfo* info = d.info + b;
-  if (info->done) return;  // the whole workgroup (one problem)
+  if (info->done) return;  // every workgroup of the problem
   {
     const uint4* src = reinterpret_cast<const uint4*>(d.aprog);
     uint4* dst = reinterpret_cast<uint4*>(lds);
@@ -152,7 +214,9 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint16_t* PG = reinterpret_cast<const uint16_t*>(lds);
-  double* Wr = lds + lm.prog_dbl + 128 + wv * lm.per_wave;
+  double* Wr = lds + lm.prog_dbl + 130 + wv * lm.per_wave;
+  int* okw = reinterpret_cast<int*>(lds + lm.prog_dbl + 128);  // a poll's outcome, for the whole workgroup
+  unsigned* sy = d.rcsync + (size_t)b * PL_RC_SYNC;
   double* v = Wr + lm.v;        // mat-vec input, zero padded to 4 T
   double* y = Wr + lm.y;        // mat-vec output [0, nw) | e_{i+1} [nw, nw + ndx)
   double* acc = Wr + lm.acc;    // LDS f64-add accumulators (mat-vec, row sums, column sums)
@@ -184,6 +248,10 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   double* A2 = DL + 3 * L;
   double* CP = DL + 4 * L;
   double* HP = DL + 5 * L;
+  // the handed-off vectors through buffer descriptors (uniform: kernel arguments + blockIdx)
+  const __amdgpu_buffer_rsrc_t rchv = rc_rsrc(DL, 6 * L), rrhs = rc_rsrc(rhs, n);
+  constexpr int oDL = 0;
+  const int oEE = 2 * L, oA2 = 3 * L, oCP = 4 * L, oHP = 5 * L;
   typedef const __attribute__((address_space(4))) PlAdmmNode* CNode;
   const CNode an = (CNode)d.anodes;
   constexpr int X2 = X * X;
@@ -283,10 +351,10 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
           const uint32_t w = xc[qq];
           c += A(w & 0xffff) * tcpl[w >> 16];
         }
-        CP[i * ndx + lane] = c;
+        st_sc1(rchv, oCP + i * ndx + lane, c);
       }
     }
-    if (lane < ndx) HP[i * ndx + lane] = y[lane];
+    if (lane < ndx) st_sc1(rchv, oHP + i * ndx + lane, y[lane]);
     wsync();
   };
 
@@ -324,8 +392,8 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
         lu[mm] = us[r];
       }
     }
-    const double dl = mode ? DL[i * ndx + rr] : 0.0;
-    const double ee = (mode && !term) ? EE[(i + 1) * ndx + rr] : 0.0;
+    const double dl = mode ? ld_sc1(rchv, oDL + i * ndx + rr) : 0.0;
+    const double ee = (mode && !term) ? ld_sc1(rchv, oEE + (i + 1) * ndx + rr) : 0.0;
     const int na = min(ne, cap);
     const int sh = (int)(((size_t)Ai >> 3) & 1);  // 16-byte alignment of the DMA source
     {
@@ -347,7 +415,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
         if (c < nw) v[c] = rh[mm];
         else if (c < T4) v[c] = 0.0;
       }
-      if (lane < ndx) A2[(i + 1) * ndx + lane] = 0.0;
+      if (lane < ndx) st_sc1(rchv, oA2 + (i + 1) * ndx + lane, 0.0);
       wsync();
       matvec(i, R, true);
       coupling_out(i, A);
@@ -471,11 +539,12 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
         rn[mm] = sigma * xnew - qo[mm] + (term ? 0.0 : acc[c]);
         gst(xa, x_off + c, xnew);
         if (store_delta) gst(dxs, x_off + c, xnew - xo[mm]);
-        gst(rhs, x_off + c, rn[mm]);
+        if (mode == 2) st_sc1(rrhs, x_off + c, rn[mm]);  // read by workgroup 0's closing pass
+        else gst(rhs, x_off + c, rn[mm]);
       }
     }
     if (!term) {
-      if (lane < ndx) A2[(i + 1) * ndx + lane] = acc[nw + lane];
+      if (lane < ndx) st_sc1(rchv, oA2 + (i + 1) * ndx + lane, acc[nw + lane]);
 #pragma unroll
       for (int mm = 0; mm < MR; ++mm) {
         const int r = lane + 64 * mm;
@@ -495,7 +564,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
       else if (c < T4) v[c] = 0.0;
     }
     wsync();
-    matvec(i, R, false);  // y = g_i = S_i rhs'_i (the block again, from L2: registers are not kept across)
+    matvec(i, R, an[i].nunit <= KM);  // y = g_i = S_i rhs'_i: the block is still in R unless it took several passes
     coupling_out(i, A);
   };
 
@@ -536,8 +605,8 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
       const double2* pp = reinterpret_cast<const double2*>(CH + (size_t)ig * 3 * X2);
 #pragma unroll
       for (int k = 0; k < SG / 2; ++k) rg[s][k] = gld(pp, boff + k);
-      u1[s] = gld(DL + ig * X, o1);        // c'_i (F rows) / h'_i (G rows)
-      u2[s] = gld(DL + (ig + 1) * X, o2);  // a2_i
+      u1[s] = ld_sc1(rchv, ig * X + o1);        // c'_i (F rows) / h'_i (G rows)
+      u2[s] = ld_sc1(rchv, (ig + 1) * X + o2);  // a2_i
     };
     int z0;  // an opaque 0: keeps the prologue's (iteration-invariant) addresses out of registers across phases
     asm volatile("s_mov_b32 %0, 0" : "=s"(z0));
@@ -545,7 +614,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
     for (int s = 0; s < PD; ++s) fetch(s, s + z0);
     if (wv == 0) {
       cbuf[lane] = 0.0;  // delta_0
-      if (lane < X) DL[lane] = 0.0;
+      if (lane < X) st_sc1(rchv, oDL + lane, 0.0);
     }
     lds_barrier();
     for (int i0 = 0; i0 <= N; i0 += PD) {
@@ -561,7 +630,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
             if (k & 1) p1 += rg[s][k].x * t.x + rg[s][k].y * t.y;
             else p0 += rg[s][k].x * t.x + rg[s][k].y * t.y;
           }
-          const double v1 = u1[s], v2 = u2[s];
+          const double v1 = slot_copy(u1[s]), v2 = slot_copy(u2[s]);
           __builtin_amdgcn_sched_barrier(0);  // the slot is consumed before its refill is issued (one register set)
           fetch(s, i + PD);
           const double sum = reduce_row(p0 + p1);
@@ -570,7 +639,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
               if (i < N) {
                 const double de = (v1 - sum) - v2;
                 cbuf[((i + 1) & 1) * 64 + crow] = de;
-                DL[(i + 1) * X + crow] = de;
+                st_sc1(rchv, oDL + (i + 1) * X + crow, de);
               }
             } else {
               WD[i * X + crow] = v1 - sum;
@@ -600,7 +669,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
     if (cF && cs == 0 && cvalid) {
       const double e = WD[N * X + crow];
       cbuf[(N & 1) * 64 + crow] = e;
-      EE[N * X + crow] = e;
+      st_sc1(rchv, oEE + N * X + crow, e);
     }
     lds_barrier();
     for (int j0 = 0; j0 < N - 1; j0 += PD) {
@@ -616,14 +685,14 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
             if (k & 1) p1 += rg[s][k].x * t.x + rg[s][k].y * t.y;
             else p0 += rg[s][k].x * t.x + rg[s][k].y * t.y;
           }
-          const double v1 = u1[s];
+          const double v1 = slot_copy(u1[s]);
           __builtin_amdgcn_sched_barrier(0);
           fetch(s, i - PD);
           const double sum = reduce_row(p0 + p1);
           if (cF && cs == 0 && cvalid) {
             const double e = v1 - sum;
             cbuf[(i & 1) * 64 + crow] = e;
-            EE[i * X + crow] = e;
+            st_sc1(rchv, oEE + i * X + crow, e);
           }
           lds_barrier();
         }
@@ -631,9 +700,9 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
     }
   };
 
-  // optional phase timing (PL_ADMM_TIMING=1: s_memtime on wave 0, cycles into d.dbg[b][0..5]):
-  // P, C1, P2, C2, P3, barrier waits
-  const bool tim = d.dbg != nullptr;
+  // optional phase timing (PL_ADMM_TIMING=1: s_memtime on wave 0 of workgroup 0, cycles into
+  // d.dbg[b][0..5]): P, C1, P2, C2, P3, barrier / hand-off waits
+  const bool tim = d.dbg != nullptr && g == 0;
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tl = 0;
   auto T = [&](int slot) __attribute__((always_inline)) {
     if (tim) {
@@ -642,36 +711,83 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
       tl = now;
     }
   };
+  // ---- hand-offs between the node phases (all workgroups) and the chains (workgroup 0).
+  // Returns false on every wave of the workgroup when a poll gave up.
+  auto drain = [&]() __attribute__((always_inline)) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have reached L2
+    __syncthreads();
+  };
+  auto poll_all = [&](int word, unsigned target, unsigned code) __attribute__((always_inline)) {
+    if (wv == 0) {
+      const bool ok = rc_poll(sy, word, target, code);
+      if (lane == 0) *okw = ok ? 1 : 0;
+    }
+    __syncthreads();
+    return *okw != 0;
+  };
+  auto give_up = [&]() __attribute__((always_inline)) {  // poison the problem's x: its solve reports NaN
+    if (threadIdx.x == 0) xa[0] = __builtin_nan("");
+  };
+  // fan-in e (e = 1: the first P, e = it + 2: iteration it's P3): false if workgroup 0 gave up
+  auto fan_in = [&](unsigned e) __attribute__((always_inline)) {
+    if (G == 1) {
+      __syncthreads();
+      return true;
+    }
+    drain();
+    if (g != 0) {
+      if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32*)(sy + RC_ARRIVE), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    }
+    return poll_all(RC_ARRIVE, (unsigned)(G - 1) * e, 0x100u + e);
+  };
+  // fan-out of iteration it's chains (workgroup 0 publishes, the others wait)
+  auto fan_out = [&](int it) __attribute__((always_inline)) {
+    if (G == 1) {
+      __syncthreads();
+      return true;
+    }
+    if (g == 0) {
+      drain();
+      if (threadIdx.x == 0) __hip_atomic_store((gu32*)(sy + RC_EPOCH), (unsigned)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    }
+    return poll_all(RC_EPOCH, (unsigned)(it + 1), 0x10000u + (unsigned)it);
+  };
+  const int i0 = g * W + wv, istep = G * W;  // this wave's nodes
   T(-1);
-  if (wv == 0 && lane < ndx) A2[lane] = 0.0;  // a2_{-1}
-  for (int i = wv; i <= N; i += W) pnode(i, 0, false);
+  if (g == 0 && wv == 0 && lane < ndx) st_sc1(rchv, oA2 + lane, 0.0);  // a2_{-1}
+  for (int i = i0; i <= N; i += istep) pnode(i, 0, false);
   T(0);
-  __syncthreads();
+  if (!fan_in(1)) { give_up(); return; }
   T(5);
   for (int it = 0; it < niter; ++it) {
-    chain_fwd();  // C1 (+ w_i[dx], formerly P2)
-    T(1);
-    __syncthreads();
-    T(5);
-    chain_bwd();  // C2
-    T(3);
-    __syncthreads();
+    if (g == 0) {
+      chain_fwd();  // C1 (+ w_i[dx], formerly P2)
+      T(1);
+      __syncthreads();
+      T(5);
+      chain_bwd();  // C2
+      T(3);
+    }
+    if (!fan_out(it)) { give_up(); return; }
     T(5);
     const bool lastit = it == niter - 1;
-    for (int i = wv; i <= N; i += W) pnode(i, lastit ? 2 : 1, check && lastit);
+    for (int i = i0; i <= N; i += istep) pnode(i, lastit ? 2 : 1, check && lastit);
     T(4);
-    __syncthreads();
+    if (!fan_in((unsigned)it + 2)) { give_up(); return; }
     T(5);
   }
+  if (g != 0) return;
   if (tim && wv == 0 && lane == 0) {
     for (int k = 0; k < 6; ++k) d.dbg[(size_t)b * 16 + k] += (double)tacc[k];
     d.dbg[(size_t)b * 16 + 6] += niter;
   }
-  // the complete rhs for the next launch / kernel: rhs_i[dx] += a2_{i-1}
+  // the complete rhs for the next launch / kernel: rhs_i[dx] += a2_{i-1} (workgroup 0, all nodes)
   for (int i = wv; i <= N; i += W) {
     if (i >= 1 && lane < ndx) {
       const int c = an[i].x_off + lane;
-      rhs[c] = rhs[c] + A2[i * ndx + lane];
+      rhs[c] = ld_sc1(rrhs, c) + ld_sc1(rchv, oA2 + i * ndx + lane);
     }
   }
   if (wv == 0 && lane == 0) {
@@ -693,7 +809,7 @@ RcCfg rc_config(const PlOcpHandle* h, int w) {
   RcLds& lm = c.lm;
   auto up2 = [](int x) { return (x + 1) & ~1; };
   lm.prog_dbl = up2((h->aprog_len + 3) / 4);
-  lm.chn = lm.prog_dbl;
+  lm.chn = lm.prog_dbl;  // then [2][64] chain buffers and the 2-double poll word
   const int T = h->ntile_max;
   int o = 0;
   lm.v = o;
@@ -711,11 +827,11 @@ RcCfg rc_config(const PlOcpHandle* h, int w) {
   lm.asb = o;
   c.w = w;
   const int budget = 160 * 1024 / 8;
-  int cap = ((budget - lm.prog_dbl - 128) / w - o - 2) & ~1;
+  int cap = ((budget - lm.prog_dbl - 130) / w - o - 2) & ~1;
   cap = std::max(0, std::min(up2(std::max(h->nent_max, 1)), cap));
   lm.asb_cap = cap;
   lm.per_wave = o + cap + 2;  // + the 16-byte alignment shift of the A staging DMA
-  c.lds = (size_t)(lm.prog_dbl + 128 + w * lm.per_wave) * sizeof(double);
+  c.lds = (size_t)(lm.prog_dbl + 130 + w * lm.per_wave) * sizeof(double);
   return c;
 }
 
@@ -726,14 +842,27 @@ void launch_rc_t(PlOcpHandle* h, int niter, int check, const RcCfg& c) {
     hipFuncSetAttribute((const void*)k_admm_rc<W, X>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((k_admm_rc<W, X>), dim3(h->B), dim3(64 * W), c.lds, h->stream, h->d, h->N, h->n, h->m, h->nnz,
+  const int G = rc_groups(h);
+  if (G > 1) (void)hipMemsetAsync(h->d.rcsync, 0, (size_t)h->B * PL_RC_SYNC * sizeof(unsigned), h->stream);
+  hipLaunchKernelGGL((k_admm_rc<W, X>), dim3(h->B * G), dim3(64 * W), c.lds, h->stream, h->d, h->N, h->n, h->m, h->nnz,
                      h->S_stride, std::max(h->ncpl_max, 1), h->ch_stride, h->chv_stride, c.lm, niter, check,
-                     h->set.sigma, h->set.alpha);
+                     h->set.sigma, h->set.alpha, G);
 }
 
 }  // namespace
 
 long long rc_ch_stride(int N, int ndx) { return (long long)(N + 1) * 3 * ndx * ndx; }
+
+// Workgroups per problem of k_admm_rc: enough for one round of node phases, as long as the
+// batch's workgroups are all resident at once (one per CU: the kernel's LDS), which the
+// in-launch hand-offs require.
+int rc_groups(const PlOcpHandle* h) {
+  if ((h->debug_paths & PL_PATH_RC_ONE_GROUP) || !h->d.rcsync) return 1;
+  const int W = h->rc_waves;
+  int G = (h->N + W) / W;  // ceil((N + 1) / W)
+  while (G > 1 && (long long)h->B * G > h->num_cu) --G;
+  return std::max(G, 1);
+}
 int rc_chv_stride(int N, int ndx) { return 6 * (N + 2) * ndx; }
 
 bool admm_rc_supported(const PlOcpHandle* h) {

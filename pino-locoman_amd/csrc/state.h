@@ -76,6 +76,7 @@ struct PlNode {
 #define PL_ADMM_MR 3        // rows per lane: nrow <= 192
 #define PL_ADMM_ASR_MAX 32  // A values per lane staged through registers (entries past 64 x ASR: global)
 #define PL_ACPL (64 * (PL_ADMM_CWM + PL_ADMM_XCM))  // coupling A values per node (d.Acpl)
+#define PL_RC_SYNC 32       // k_admm_rc hand-off words per problem (one 128-byte line)
 struct PlAdmmNode {
   int nw, nrow, ncol, ncpl, nent, nunit, ntile, ntl;  // nunit = K slots, ntile = T, ntl = tiles
   unsigned kmagic;  // ceil(2^32 / K): t / K == umulhi(t, kmagic) for the tile counts used
@@ -178,6 +179,8 @@ struct PlDev {
   double* FS;            // factor scratch [B][fs_stride]: A', G, C^-1 per node
   double* CH;            // reduced-chain blocks [B][ch_stride]: per node F_i^T | F_i | G_i (k_fred, k_admm_rc.hip)
   double* chv;           // reduced-chain vectors [B][chv_stride] (k_admm_rc)
+  unsigned* rcsync;      // k_admm_rc hand-off words [B][PL_RC_SYNC]: fan-in count, fan-out epoch, give-up
+                         // code (zeroed before every launch)
   uint32_t* ttab;        // lane-tile tables [64][PL_ADMM_KM] per distinct (T, K): (I << 24) | (J << 16) | cidx
   int2* jlist;           // k_eval_jac work list: (node, local column), tree-pass columns first (whole waves)
   int2* jlin;            // k_eval_jac_lin work list (rnea: the a / f columns, -1 padded to whole waves)
@@ -279,7 +282,8 @@ struct PlOcpHandle {
   int ruiz_fused;                   // 1: all equilibration passes in k_ruiz_fused (PL_PATH_RUIZ_PER_PASS: per-pass kernels)
   unsigned debug_paths;             // pl_ocp_desc.debug_paths (PL_PATH_*), 0 in production
   int admm_rc;                      // 1: reduced-chain ADMM (k_admm_rc.hip) instead of the sweeps
-  int rc_waves;                     // waves per problem of k_admm_rc (4 or 8)
+  int rc_waves;                     // waves per workgroup of k_admm_rc (4 or 8)
+  int num_cu;                       // compute units of the device (k_admm_rc's co-residency bound)
   long long ch_stride;              // doubles of chain blocks per problem
   int chv_stride;                   // doubles of chain vectors per problem
   int jl_len;                       // k_eval_jac work-list entries (a multiple of 64 before the cheap part)
@@ -362,6 +366,7 @@ void launch_fred(PlOcpHandle* h);
 void launch_acpl(PlOcpHandle* h);
 long long rc_ch_stride(int N, int ndx);
 int rc_chv_stride(int N, int ndx);
+int rc_groups(const PlOcpHandle* h);
 void launch_check(PlOcpHandle* h, int it, int final_check);
 void launch_unscale(PlOcpHandle* h);
 void launch_line_search(PlOcpHandle* h);

@@ -42,7 +42,7 @@ class OcpDesc(C.Structure):
 # regression tests compare with, and the phase-timing instrumentation; 0 in production
 PATHS = {"jac_dual_all": 1, "jac_const_every": 2, "hess_full_tree": 4, "hess_dual_all": 8, "fchain_list": 16,
          "ruiz_per_pass": 32, "no_mpc_graph": 64, "admm_timing": 128, "ip_refine_gather": 256,
-         "hess_pairs": 512}
+         "hess_pairs": 512, "rc_one_group": 1024}
 
 
 class Stats(C.Structure):
@@ -84,6 +84,7 @@ EXPORTS = {
     "pl_ocp_set_solver": (C.c_int, [C.c_void_p, C.c_int]),
     "pl_ocp_set_admm_kernel": (C.c_int, [C.c_void_p, C.c_int]),
     "pl_ocp_get_admm_kernel": (C.c_int, [C.c_void_p]),
+    "pl_ocp_get_admm_groups": (C.c_int, [C.c_void_p]),
     "pl_ocp_set_ip_settings": (C.c_int, [C.c_void_p, C.POINTER(IpSettings)]),
     "pl_ocp_ip_stats": (C.c_int, [C.c_void_p, C.POINTER(IpStats)]),
     "pl_ocp_get_lam": (C.c_int, [C.c_void_p, _dp]),

@@ -280,6 +280,11 @@ class BatchedOCP:
         code = _lib.lib().pl_ocp_get_admm_kernel(self.h)
         return {v: k for k, v in self.ADMM_KERNELS.items()}[code]
 
+    def admm_groups(self):
+        """Workgroups per problem of the next ADMM launch (k_admm_rc spreads its node phases
+        over several; the sweep kernels use 1)."""
+        return _lib.lib().pl_ocp_get_admm_groups(self.h)
+
     def set_solver(self, solver):
         """"osqp" (SQP + OSQP, ocp.py:265-313 / 375-422) or "fatrop" (the interior-point
         restatement of the Fatrop branch, ocp.py:248-263 / 360-373)."""

@@ -147,7 +147,7 @@ def test_debug_paths_outside_mask_rejected(monkeypatch):
         BatchedOCP(R, "whole_body_rnea", 10, batch=1, device=-1, debug_paths=("undefined_bit",))
     bo = BatchedOCP(R, "whole_body_rnea", 10, batch=1, device=-1, debug_paths=tuple(k for k in _lib.PATHS
                                                                                    if k != "undefined_bit"))
-    assert bo.sizes()["debug_paths"] == 1023
+    assert bo.sizes()["debug_paths"] == 2047
     bo.close()
 
 

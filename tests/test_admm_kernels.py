@@ -137,3 +137,29 @@ def test_chain_interior_point_agrees_with_sweep():
     assert np.array_equal(ss["iter"], sc["iter"]) and np.array_equal(ss["status"], sc["status"])
     for b in range(xs.shape[0]):
         assert _rel(xc[b], xs[b]) < 1e-6, b
+
+
+@pytest.mark.parametrize("rname,dyn,N,B,groups", [("go2", "whole_body_rnea", 20, 1, 3),
+                                                  ("b2g", "whole_body_rnea", 50, 6, 7)])
+def test_chain_groups_bit_identical(rname, dyn, N, B, groups):
+    """k_admm_rc spreads its node phases over ceil((N + 1) / 8) workgroups per problem (r06,
+    in-launch hand-offs); the node arithmetic is the same, so the iterates are bit-identical to
+    the one-workgroup kernel (PL_PATH_RC_ONE_GROUP) over whole solves and MPC steps."""
+    from pinoloco.ocp import BatchedOCP
+    from pinoloco.synthetic import build_batch
+    R = make_robot(rname)
+    lay, P, X, XS, T0 = build_batch(R, dyn, N, B, 0)
+    out = []
+    for paths, want in (((), groups), (("rc_one_group",), 1)):
+        bo = BatchedOCP(R, dyn, N, batch=B, device=0, debug_paths=paths)
+        bo.set_admm_kernel("chain")
+        assert bo.admm_groups() == want
+        bo.set_params(P)
+        bo.set_x(X)
+        bo.init_solver()
+        st = bo.solve()
+        out.append((bo.get_x(), st["admm_iters"], st["status"]))
+        bo.close()
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])
+    assert np.all(np.isfinite(out[0][0]))

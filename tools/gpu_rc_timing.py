@@ -1,6 +1,6 @@
 """Phase timing of the reduced-chain ADMM kernel (k_admm_rc, s_memtime on wave 0).
 
-Run on the GPU box:  python tools/gpu_rc_timing.py robot dynamics N B
+Run on the GPU box:  python tools/gpu_rc_timing.py robot dynamics N B [debug_path ...]
 """
 import os
 import sys
@@ -17,7 +17,7 @@ rob, dyn, N, B = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
 R = robots.ROBOTS[rob]()
 R.set_gait_sequence("trot", 0.8)
 lay, P, X, XS, T0 = build_batch(R, dyn, N, B, 0)
-bo = BatchedOCP(R, dyn, N, batch=B, device=0, debug_paths=("admm_timing",))
+bo = BatchedOCP(R, dyn, N, batch=B, device=0, debug_paths=("admm_timing",) + tuple(sys.argv[5:]))
 bo.set_admm_kernel("chain")
 bo.set_params(P)
 bo.set_x(X)
@@ -25,9 +25,9 @@ bo.init_solver()
 st = bo.solve(timed=True)
 T = bo.debug("admm_t", B * 40)[:B * 16].reshape(B, 16)
 it = T[:, 6]
-names = ["P (first)", "C1 chain", "P2", "C2 chain", "P3 + P", "barrier waits"]
+names = ["P (first)", "C1 chain", "P2", "C2 chain", "P3 + P", "barrier / hand-off waits"]
 per = T[:, :6] / it[:, None]
-print(f"{rob} {dyn} N={N} B={B}: phase_ms {st['phase_ms']}")
+print(f"{rob} {dyn} N={N} B={B} workgroups/problem {bo.admm_groups()}: phase_ms {st['phase_ms']}")
 for k, nm in enumerate(names):
     print(f"{nm:14s} mean cycles/iteration {per[:, k].mean():10.1f}  p90 {np.percentile(per[:, k], 90):10.1f}")
 print(f"total cycles/iteration {per.sum(1).mean():.1f}; C1 cycles/step {per[:, 1].mean() / N:.1f}, "
