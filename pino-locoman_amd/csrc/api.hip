@@ -257,7 +257,7 @@ extern "C" int pl_ocp_create(const pl_model* model, const pl_ocp_desc* d, int ba
   h.admm_rc = 0;
   h.rc_waves = 8;
   h.ruiz_fused = !(h.debug_paths & PL_PATH_RUIZ_PER_PASS);
-  h.ch_stride = rc_ch_stride(h.N, h.ndx);
+  h.ch_stride = rc_ch_stride(h.N, h.ndx, h.rc_waves);
   h.chv_stride = rc_chv_stride(h.N, h.ndx);
   h.gait_type = d->gait_type;
   h.gait_period = d->gait_period;

@@ -102,29 +102,33 @@ struct Sb {
   double2 s[KM][8];
 };
 
-// Lane map of the chains (k_admm_rc): RW rows per wave, each split over NS lanes of SG columns
-// (SG even: 16-byte loads); 2 RW NS <= 64 (forward: F and G rows side by side).  PD steps of
-// chain blocks in flight per lane, within a register budget (2 waves per SIMD at W = 8).
-constexpr int rc_pick_ns(int X, int RW) {
-  for (int ns = 8; ns >= 1; --ns)
-    if (X % ns == 0 && (X / ns) % 2 == 0 && 2 * RW * ns <= 64) return ns;
-  return 1;
+// Lane map of the chains (k_admm_rc): RW rows per wave, each split over NS lanes of SG columns;
+// 2 RW NS <= 64 (forward: F and G rows side by side).  NS is a power of two (the row sum is a
+// DPP butterfly inside a quad, r06; the r05 map summed 6 lanes by ds_bpermute, ~40 % of a step)
+// and the stored rows are zero-padded to XP = NS SG columns, SG even (16-byte loads).  PD steps
+// of chain blocks in flight per lane, within a register budget (2 waves per SIMD at W = 8).
+constexpr int rc_pick_ns(int RW) { return 2 * RW * 4 <= 64 ? 4 : (2 * RW * 2 <= 64 ? 2 : 1); }
+constexpr int rc_row_len(int X, int W) {  // XP
+  const int ns = rc_pick_ns((X + W - 1) / W);
+  return (X + 2 * ns - 1) / (2 * ns) * (2 * ns);
 }
 template <int X, int W>
 struct RcChain {
   static constexpr int RW = (X + W - 1) / W;
-  static constexpr int NS = rc_pick_ns(X, RW);
-  static constexpr int SG = X / NS;
+  static constexpr int NS = rc_pick_ns(RW);
+  static constexpr int XP = rc_row_len(X, W);
+  static constexpr int SG = XP / NS;
   static constexpr int PD = (W >= 8 ? 72 : 144) / SG < 2 ? 2 : ((W >= 8 ? 72 : 144) / SG > 10 ? 10 : (W >= 8 ? 72 : 144) / SG);
 };
 
-// An explicit copy out of a prefetch slot before its refill is issued: otherwise the compiler may
-// load the refill into other registers and move it into the slot at the loop latch, which waits
-// vmcnt(0) on the refill and drains the prefetch every chain step.
-__device__ __forceinline__ double slot_copy(double x) {
-  double y;
-  asm volatile("v_mov_b64 %0, %1" : "=v"(y) : "v"(x));
-  return y;
+// x + (x of the lane whose index differs in bit 0 / bit 1): one DPP quad permutation per 32-bit
+// half.  Both partners compute a + b with the same operands, so every lane of the group ends
+// with the same bits.
+template <int CTRL>
+__device__ __forceinline__ double dpp_add(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false);
+  return x + __hiloint2double(hi, lo);
 }
 
 // Workgroup barrier that orders LDS only (lgkmcnt(0) + s_barrier): __syncthreads() would also
@@ -140,12 +144,13 @@ __device__ __forceinline__ void lds_barrier() {
 // ---------------------------------------------------------------------------
 // Chain blocks of node i (one 256-thread workgroup per (problem, node)), from the stored
 // (symmetrised, tiled) factor block that the ADMM kernels use:
-//   d.CH[b] + i * 3 ndx^2:  FR (F_i row-major) | FT (F_i^T row-major) | G (S_i[dx, dx])
-// Every chain lane reads one contiguous row (16-byte loads, one VGPR offset + immediates).
+//   d.CH[b] + i * 3 ndx XP:  FR (F_i row-major) | FT (F_i^T row-major) | G (S_i[dx, dx]),
+// rows of XP >= ndx columns, zero-padded (rc_row_len).
+// Every chain lane reads one contiguous row segment (16-byte loads, one VGPR offset + immediates).
 // F_i[a][k] = sum_{(e, s) in xc(a)} A_e rho_s sum_{(e', l) in cw(s)} A_e' S_i[l][k]
 // (the coupling product the sweep kernels apply as t_s = rho_s a_s(w) . w).
 __global__ __launch_bounds__(256) void k_fred(PlDev d, int N, int nnz, int ndx, int S_stride, int cpl_stride,
-                                              long long ch_stride) {
+                                              long long ch_stride, int XP) {
   extern __shared__ double sc[];  // S_i[:, 0:ndx] dense, sc[l * ndx + k]
   const int b = blockIdx.x / (N + 1), i = blockIdx.x - b * (N + 1);
   typedef const __attribute__((address_space(4))) PlAdmmNode* CNode;
@@ -165,9 +170,13 @@ __global__ __launch_bounds__(256) void k_fred(PlDev d, int N, int nnz, int ndx, 
     sc[q] = (c & 1) ? p.y : p.x;
   }
   __syncthreads();
-  const int X2 = ndx * ndx;
-  double* CH = d.CH + (size_t)b * ch_stride + (size_t)i * 3 * X2;
-  for (int q = threadIdx.x; q < X2; q += 256) CH[2 * X2 + q] = sc[q];  // rows l < ndx of sc: G
+  const int X2 = ndx * ndx, XB = ndx * XP;
+  double* CH = d.CH + (size_t)b * ch_stride + (size_t)i * 3 * XB;
+  for (int q = threadIdx.x; q < XB; q += 256) {  // rows l < ndx of sc: G; zero padding of every part
+    const int l = q / XP, k = q - l * XP;
+    CH[2 * XB + q] = k < ndx ? sc[l * ndx + k] : 0.0;
+    if (k >= ndx) CH[q] = CH[XB + q] = 0.0;
+  }
   if (i >= N) return;
   const uint16_t* P = d.aprog + an[i].prog;
   const double* As = d.As + (size_t)b * nnz + an[i].ent_off;
@@ -189,8 +198,8 @@ __global__ __launch_bounds__(256) void k_fred(PlDev d, int N, int nnz, int ndx, 
       }
       f += As[w & 0xffff] * (rc[s] * acc);
     }
-    CH[a * ndx + k] = f;       // FR: (a, k)
-    CH[X2 + k * ndx + a] = f;  // FT: (k, a)
+    CH[a * XP + k] = f;       // FR: (a, k)
+    CH[XB + k * XP + a] = f;  // FT: (k, a)
   }
 }
 
@@ -243,7 +252,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   // chain vectors, (N + 2) ndx each: delta_i, w_i[dx], e_i, a2_{i-1} (A2[i] = a2_{i-1}), c'_i, h'_i
   const int L = (N + 2) * ndx;
   double* DL = d.chv + (size_t)b * chv_stride;
-  double* WD = DL + L;
+  // DL + L: w_i[dx] until r06 (now kept in LDS by the chains, whist)
   double* EE = DL + 2 * L;
   double* A2 = DL + 3 * L;
   double* CP = DL + 4 * L;
@@ -254,7 +263,6 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   const int oEE = 2 * L, oA2 = 3 * L, oCP = 4 * L, oHP = 5 * L;
   typedef const __attribute__((address_space(4))) PlAdmmNode* CNode;
   const CNode an = (CNode)d.anodes;
-  constexpr int X2 = X * X;
   const int rr = min(lane, ndx - 1);  // chain row / column of the lane (clamped)
 
   auto load_S = [&](int i, int kbase, Sb& R) __attribute__((always_inline)) {
@@ -358,9 +366,35 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
     wsync();
   };
 
+#ifndef PL_RC_SUBTIMING
+#define PL_RC_SUBTIMING 0
+#endif
+#if PL_RC_SUBTIMING  // experiment builds (PL_HIPCC_DEFS=-DPL_RC_SUBTIMING=1): sub-phases of pnode, wave 0 of workgroup 0
+  unsigned long long sacc[7] = {0, 0, 0, 0, 0, 0, 0}, sl = 0;
+  const bool stim = d.dbg != nullptr && blockIdx.x % G == 0 && threadIdx.x < 64;
+  auto SUB = [&](int slot) __attribute__((always_inline)) {
+    if (stim) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (slot >= 0) sacc[slot] += now - sl;
+      sl = now;
+    }
+  };
+  unsigned long long cacc[4] = {0, 0, 0, 0}, cl = 0;
+  auto CSUB = [&](int slot) __attribute__((always_inline)) {
+    if (stim) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (slot >= 0) cacc[slot] += now - cl;
+      cl = now;
+    }
+  };
+#else
+  auto SUB = [&](int) __attribute__((always_inline)) {};
+  auto CSUB = [&](int) __attribute__((always_inline)) {};
+#endif
   // ---- one node of a parallel phase.  mode 0: P only (rhs complete, a2 = 0); 1: P3 + the
   // next iteration's P; 2: P3 only (the launch's last iteration)
   auto pnode = [&](int i, int mode, bool store_delta) __attribute__((always_inline)) {
+    SUB(-1);
     const int nw = an[i].nw, T4 = 4 * an[i].ntile, x_off = an[i].x_off;
     const int eo = an[i].ent_off, ne = an[i].nent;
     const bool term = i == N;
@@ -406,6 +440,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
         if (j * 64 + lane < n2) __builtin_amdgcn_global_load_lds((GP)(g0 + 2 * (j * 64 + lane)), (LP)(asb + 128 * j), 16, 0, 0);
     }
     __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
+    SUB(0);
     const double* asbs = asb + sh;
     auto A = [&](int e) __attribute__((always_inline)) { return e < na ? asbs[e] : Ai[e]; };
     if (mode == 0) {
@@ -463,7 +498,9 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
       }
     }
     wsync();
+    SUB(1);
     matvec(i, R, true);  // y[0..nw) = x~_i
+    SUB(2);
     double kz[MR], ky[MR], kd[MR];
     if (!term) {
       // z~ = A [x~_i; e_{i+1}] over row chunks
@@ -528,6 +565,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
       }
       wsync();
     }
+    SUB(3);
     // update_x and the next rhs'_i = sigma x - q + (own rows)^T (rho z - y); a2_i
     double rn[MV];
 #pragma unroll
@@ -555,6 +593,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
         }
       }
     }
+    SUB(4);
     if (mode == 2) return;
     wsync();
 #pragma unroll
@@ -565,7 +604,9 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
     }
     wsync();
     matvec(i, R, an[i].nunit <= KM);  // y = g_i = S_i rhs'_i: the block is still in R unless it took several passes
+    SUB(5);
     coupling_out(i, A);
+    SUB(6);
   };
 
   // ---- The chains, spread over the whole workgroup: wave w owns rows [r0, r0 + nr) of the
@@ -577,7 +618,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   //   C2 (steps i = N-1..1): lanes q < RW: e_i[r] = w_i[r] - F_i^T[r] . e_{i+1}
   // delta / e are double-buffered in LDS (read one buffer, write the other), so one barrier
   // per step suffices.  Fixed lane -> (row, segment) map and a fixed-order reduction.
-  constexpr int RW = CS::RW, NS = CS::NS, SG = CS::SG, PD = CS::PD;
+  constexpr int RW = CS::RW, NS = CS::NS, SG = CS::SG, PD = CS::PD, XP = CS::XP, XB = X * XP;
   const int r0 = (X * wv) / W, nr = (X * (wv + 1)) / W - r0;
   const int cq = lane / NS, cs = lane - cq * NS;
   const bool cF = cq < RW;
@@ -585,28 +626,77 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   const bool cvalid = cj < nr && cq < 2 * RW;
   const int crow = r0 + min(cj, nr - 1);
   double* cbuf = lds + lm.chn;  // [2][64] shared by the workgroup
-
-  auto reduce_row = [&](double p) __attribute__((always_inline)) {
-    // sum of the NS partials of this lane's row, in segment order
-    double t = __shfl(p, cq * NS, 64);
-#pragma unroll
-    for (int k = 1; k < NS; ++k) t += __shfl(p, cq * NS + k, 64);
-    return t;
+  // The chains' outputs of this wave's rows live in the wave's A-staging area (idle during the
+  // chains): the steps store no vector memory (a store in the step loop made the compiler drain
+  // the chain-block prefetch at every step); publish() writes delta / e out with sc1 stores once
+  // per chain, spread over the wave's lanes.  rc_config keeps the area >= (2N + 3) rows.
+  double* hist = asb;                    // [N + 2][nr]: delta_k (chain_fwd), then e_k (chain_bwd)
+  double* whist = asb + (N + 2) * nr;    // [N + 1][nr]: w_k[dx] from chain_fwd's G rows
+  auto publish = [&](int off, int k0, int k1) __attribute__((always_inline)) {  // k in [k0, k1)
+    wsync();
+    const int cnt = (k1 - k0) * nr;
+    for (int t = lane; t < cnt; t += 64) {
+      const int kk = t / nr, j = t - kk * nr;
+      st_sc1(rchv, off + (k0 + kk) * X + r0 + j, hist[(k0 + kk) * nr + j]);
+    }
   };
 
+  auto reduce_row = [&](double p) __attribute__((always_inline)) {
+    // sum of the NS partials of this lane's row (its NS lanes are one aligned group of a quad)
+    if constexpr (NS >= 2) p = dpp_add<0xB1>(p);  // quad_perm [1, 0, 3, 2]
+    if constexpr (NS >= 4) p = dpp_add<0x4E>(p);  // quad_perm [2, 3, 0, 1]
+    return p;
+  };
+
+  // Each chain runs in blocks of PD steps whose slots refill unconditionally (fetches past the
+  // end are clamped to valid nodes), then a tail without refills: no skipped step inside the
+  // refilling loop, so the compiler's wait counts follow the PD-deep prefetch (a conditional step
+  // there merged skip paths into the loop state and it waited for the newest loads every step).
   auto chain_fwd = [&]() __attribute__((always_inline)) {
     double2 rg[PD][SG / 2];
     double u1[PD], u2[PD];
     // per-lane offsets (constant over the steps) from wave-uniform bases: saddr + voffset loads
-    const int boff = ((cF ? 0 : 2 * X2) + crow * X + cs * SG) / 2;
+    const int boff = ((cF ? 0 : 2 * XB) + crow * XP + cs * SG) / 2;
     const int o1 = (cF ? 4 : 5) * L + crow, o2 = 3 * L + crow;
     auto fetch = [&](int s, int i) __attribute__((always_inline)) {
       const int ig = min(i, N);  // F rows are not used at step N (its block holds G_N only)
-      const double2* pp = reinterpret_cast<const double2*>(CH + (size_t)ig * 3 * X2);
+      const double2* pp = reinterpret_cast<const double2*>(CH + (size_t)ig * 3 * XB);
 #pragma unroll
       for (int k = 0; k < SG / 2; ++k) rg[s][k] = gld(pp, boff + k);
       u1[s] = ld_sc1(rchv, ig * X + o1);        // c'_i (F rows) / h'_i (G rows)
       u2[s] = ld_sc1(rchv, (ig + 1) * X + o2);  // a2_i
+    };
+    auto step = [&](int s, int i, bool refill) __attribute__((always_inline)) {
+      CSUB(-1);
+      const double2* dc = reinterpret_cast<const double2*>(cbuf + (i & 1) * 64) + cs * (SG / 2);
+      double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < SG / 2; ++k) {
+        const double2 t = dc[k];
+        if (k & 1) p1 += rg[s][k].x * t.x + rg[s][k].y * t.y;
+        else p0 += rg[s][k].x * t.x + rg[s][k].y * t.y;
+      }
+      CSUB(0);
+      const double sum = reduce_row(p0 + p1);
+      if (cs == 0 && cvalid) {
+        if (cF) {
+          if (i < N) {
+            const double de = (u1[s] - sum) - u2[s];
+            cbuf[((i + 1) & 1) * 64 + crow] = de;
+            hist[(i + 1) * nr + cj] = de;
+          }
+        } else {
+          whist[i * nr + cj] = u1[s] - sum;  // w_i[dx], read back by this wave's chain_bwd
+        }
+      }
+      // the refill after the slot's last use: old and new values are never live together, so
+      // the compiler keeps one register set per slot (no latch copies that wait for the refill)
+      CSUB(1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (refill) fetch(s, i + PD);
+      CSUB(2);
+      lds_barrier();
+      CSUB(3);
     };
     int z0;  // an opaque 0: keeps the prologue's (iteration-invariant) addresses out of registers across phases
     asm volatile("s_mov_b32 %0, 0" : "=s"(z0));
@@ -614,90 +704,69 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
     for (int s = 0; s < PD; ++s) fetch(s, s + z0);
     if (wv == 0) {
       cbuf[lane] = 0.0;  // delta_0
+      cbuf[64 + lane] = 0.0;  // the padding columns [X, XP) of both buffers stay 0
       if (lane < X) st_sc1(rchv, oDL + lane, 0.0);
     }
     lds_barrier();
-    for (int i0 = 0; i0 <= N; i0 += PD) {
+    int i0 = 0;
+    for (; i0 + PD <= N + 1; i0 += PD) {
 #pragma unroll
-      for (int s = 0; s < PD; ++s) {
-        const int i = i0 + s;
-        if (i <= N) {
-          const double2* dc = reinterpret_cast<const double2*>(cbuf + (i & 1) * 64) + cs * (SG / 2);
-          double p0 = 0.0, p1 = 0.0;
-#pragma unroll
-          for (int k = 0; k < SG / 2; ++k) {
-            const double2 t = dc[k];
-            if (k & 1) p1 += rg[s][k].x * t.x + rg[s][k].y * t.y;
-            else p0 += rg[s][k].x * t.x + rg[s][k].y * t.y;
-          }
-          const double v1 = slot_copy(u1[s]), v2 = slot_copy(u2[s]);
-          __builtin_amdgcn_sched_barrier(0);  // the slot is consumed before its refill is issued (one register set)
-          fetch(s, i + PD);
-          const double sum = reduce_row(p0 + p1);
-          if (cs == 0 && cvalid) {
-            if (cF) {
-              if (i < N) {
-                const double de = (v1 - sum) - v2;
-                cbuf[((i + 1) & 1) * 64 + crow] = de;
-                st_sc1(rchv, oDL + (i + 1) * X + crow, de);
-              }
-            } else {
-              WD[i * X + crow] = v1 - sum;
-            }
-          }
-          lds_barrier();
-        }
-      }
+      for (int s = 0; s < PD; ++s) step(s, i0 + s, true);
     }
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+      if (i0 + s <= N) step(s, i0 + s, false);
+    publish(oDL, 1, N + 1);  // delta_1 .. delta_N (delta_0 = 0 went out in the prologue)
   };
 
   auto chain_bwd = [&]() __attribute__((always_inline)) {
     double2 rg[PD][SG / 2];
-    double u1[PD];
-    const int boff = (X2 + crow * X + cs * SG) / 2;
+    const int boff = (XB + crow * XP + cs * SG) / 2;
     auto fetch = [&](int s, int i) __attribute__((always_inline)) {
       const int ic = max(i, 1);
-      const double2* pp = reinterpret_cast<const double2*>(CH + (size_t)ic * 3 * X2);
+      const double2* pp = reinterpret_cast<const double2*>(CH + (size_t)ic * 3 * XB);
 #pragma unroll
       for (int k = 0; k < SG / 2; ++k) rg[s][k] = gld(pp, boff + k);
-      u1[s] = gld(WD + ic * X, crow);
+    };
+    auto step = [&](int s, int i, bool refill) __attribute__((always_inline)) {
+      const double2* ec = reinterpret_cast<const double2*>(cbuf + ((i + 1) & 1) * 64) + cs * (SG / 2);
+      double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < SG / 2; ++k) {
+        const double2 t = ec[k];
+        if (k & 1) p1 += rg[s][k].x * t.x + rg[s][k].y * t.y;
+        else p0 += rg[s][k].x * t.x + rg[s][k].y * t.y;
+      }
+      const double w = whist[i * nr + cj];
+      const double sum = reduce_row(p0 + p1);
+      if (cF && cs == 0 && cvalid) {
+        const double e = w - sum;
+        cbuf[(i & 1) * 64 + crow] = e;
+        hist[i * nr + cj] = e;
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the refill after the slot's last use (chain_fwd)
+      if (refill) fetch(s, i - PD);
+      lds_barrier();
     };
     int z0;
     asm volatile("s_mov_b32 %0, 0" : "=s"(z0));
 #pragma unroll
     for (int s = 0; s < PD; ++s) fetch(s, N - 1 - s + z0);
     if (cF && cs == 0 && cvalid) {
-      const double e = WD[N * X + crow];
+      const double e = whist[N * nr + cj];
       cbuf[(N & 1) * 64 + crow] = e;
       st_sc1(rchv, oEE + N * X + crow, e);
     }
     lds_barrier();
-    for (int j0 = 0; j0 < N - 1; j0 += PD) {
+    int j0 = 0;  // e_i for i = N-1 .. 1: steps j = N - 1 - i
+    for (; j0 + PD <= N - 1; j0 += PD) {
 #pragma unroll
-      for (int s = 0; s < PD; ++s) {
-        const int i = N - 1 - (j0 + s);  // e_i for i = N-1 .. 1
-        if (i >= 1) {
-          const double2* ec = reinterpret_cast<const double2*>(cbuf + ((i + 1) & 1) * 64) + cs * (SG / 2);
-          double p0 = 0.0, p1 = 0.0;
-#pragma unroll
-          for (int k = 0; k < SG / 2; ++k) {
-            const double2 t = ec[k];
-            if (k & 1) p1 += rg[s][k].x * t.x + rg[s][k].y * t.y;
-            else p0 += rg[s][k].x * t.x + rg[s][k].y * t.y;
-          }
-          const double v1 = slot_copy(u1[s]);
-          __builtin_amdgcn_sched_barrier(0);
-          fetch(s, i - PD);
-          const double sum = reduce_row(p0 + p1);
-          if (cF && cs == 0 && cvalid) {
-            const double e = v1 - sum;
-            cbuf[(i & 1) * 64 + crow] = e;
-            st_sc1(rchv, oEE + i * X + crow, e);
-          }
-          lds_barrier();
-        }
-      }
+      for (int s = 0; s < PD; ++s) step(s, N - 1 - (j0 + s), true);
     }
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+      if (j0 + s < N - 1) step(s, N - 1 - (j0 + s), false);
+    publish(oEE, 1, N);  // e_1 .. e_{N-1} (e_N went out in the prologue)
   };
 
   // optional phase timing (PL_ADMM_TIMING=1: s_memtime on wave 0 of workgroup 0, cycles into
@@ -731,7 +800,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   // fan-in e (e = 1: the first P, e = it + 2: iteration it's P3): false if workgroup 0 gave up
   auto fan_in = [&](unsigned e) __attribute__((always_inline)) {
     if (G == 1) {
-      __syncthreads();
+      drain();  // the sc1 stores have reached L2 before another wave's sc1 loads
       return true;
     }
     drain();
@@ -744,7 +813,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   // fan-out of iteration it's chains (workgroup 0 publishes, the others wait)
   auto fan_out = [&](int it) __attribute__((always_inline)) {
     if (G == 1) {
-      __syncthreads();
+      drain();
       return true;
     }
     if (g == 0) {
@@ -782,6 +851,11 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   if (tim && wv == 0 && lane == 0) {
     for (int k = 0; k < 6; ++k) d.dbg[(size_t)b * 16 + k] += (double)tacc[k];
     d.dbg[(size_t)b * 16 + 6] += niter;
+#if PL_RC_SUBTIMING
+    for (int k = 0; k < 7; ++k) d.dbg[(size_t)b * 16 + 8 + k] += (double)sacc[k];
+    if (b == 0)
+      for (int k = 0; k < 4; ++k) d.dbg[16 + k] += (double)cacc[k];  // B = 1 runs: chain_fwd step sub-phases
+#endif
   }
   // the complete rhs for the next launch / kernel: rhs_i[dx] += a2_{i-1} (workgroup 0, all nodes)
   for (int i = wv; i <= N; i += W) {
@@ -851,7 +925,7 @@ void launch_rc_t(PlOcpHandle* h, int niter, int check, const RcCfg& c) {
 
 }  // namespace
 
-long long rc_ch_stride(int N, int ndx) { return (long long)(N + 1) * 3 * ndx * ndx; }
+long long rc_ch_stride(int N, int ndx, int W) { return (long long)(N + 1) * 3 * ndx * rc_row_len(ndx, W); }
 
 // Workgroups per problem of k_admm_rc: enough for one round of node phases, as long as the
 // batch's workgroups are all resident at once (one per CU: the kernel's LDS), which the
@@ -868,7 +942,8 @@ int rc_chv_stride(int N, int ndx) { return 6 * (N + 2) * ndx; }
 bool admm_rc_supported(const PlOcpHandle* h) {
   // the chain blocks F_i = C_i S_i[:, dx] assume one coupling row per dx_{i+1} column
   return !h->fac_gc && (h->ndx == 24 || h->ndx == 30 || h->ndx == 36 || h->ndx == 48) && (h->rc_waves == 4 || h->rc_waves == 8) && h->nw_max <= 64 * MV && h->nrow_max <= 64 * MR && h->ncpl_max <= 64 &&
-         rc_config(h, h->rc_waves).lds <= 160 * 1024;
+         rc_config(h, h->rc_waves).lds <= 160 * 1024 &&
+         rc_config(h, h->rc_waves).lm.asb_cap >= (2 * h->N + 3) * ((h->ndx + h->rc_waves - 1) / h->rc_waves);  // chain history
 }
 
 void launch_fred(PlOcpHandle* h) {
@@ -879,7 +954,7 @@ void launch_fred(PlOcpHandle* h) {
     attr = true;
   }
   hipLaunchKernelGGL(k_fred, dim3(h->B * (h->N + 1)), dim3(256), lds, h->stream, h->d, h->N, h->nnz, h->ndx,
-                     h->S_stride, std::max(h->ncpl_max, 1), h->ch_stride);
+                     h->S_stride, std::max(h->ncpl_max, 1), h->ch_stride, rc_row_len(h->ndx, h->rc_waves));
 }
 
 void launch_admm_rc(PlOcpHandle* h, int niter, int check) {

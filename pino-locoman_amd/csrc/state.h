@@ -364,7 +364,7 @@ void launch_admm_rc(PlOcpHandle* h, int niter, int check);
 void launch_lag_hess(PlOcpHandle* h);
 void launch_fred(PlOcpHandle* h);
 void launch_acpl(PlOcpHandle* h);
-long long rc_ch_stride(int N, int ndx);
+long long rc_ch_stride(int N, int ndx, int W);
 int rc_chv_stride(int N, int ndx);
 int rc_groups(const PlOcpHandle* h);
 void launch_check(PlOcpHandle* h, int it, int final_check);

@@ -32,3 +32,12 @@ for k, nm in enumerate(names):
     print(f"{nm:14s} mean cycles/iteration {per[:, k].mean():10.1f}  p90 {np.percentile(per[:, k], 90):10.1f}")
 print(f"total cycles/iteration {per.sum(1).mean():.1f}; C1 cycles/step {per[:, 1].mean() / N:.1f}, "
       f"C2 cycles/step {per[:, 3].mean() / (N - 1):.1f}")
+sub = T[:, 8:15] / it[:, None]
+if sub.sum() > 0:  # PL_RC_SUBTIMING build: node sub-phases of wave 0 (node 0), cycles per iteration
+    for nm, k in zip(["loads", "coupling + u", "matvec x~", "rows / columns", "x update", "matvec g", "coupling out"], range(7)):
+        print(f"  node 0 {nm:16s} {sub[:, k].mean():10.1f}")
+full = bo.debug("admm_t", B * 40)
+if B == 1 and full[16:20].sum() > 0:  # chain_fwd step sub-phases (wave 0), cycles per step
+    nsteps = it[0] * (N + 1)
+    for nm, k in zip(["lds + fma", "reduce + stores", "refill issue", "barrier"], range(4)):
+        print(f"  C1 step {nm:16s} {full[16 + k] / nsteps:10.1f}")
