@@ -121,6 +121,20 @@ struct RcChain {
   static constexpr int PD = (W >= 8 ? 72 : 144) / SG < 2 ? 2 : ((W >= 8 ? 72 : 144) / SG > 10 ? 10 : (W >= 8 ? 72 : 144) / SG);
 };
 
+// Chain blocks in the chains' lane order (r06): per node a forward part [W][SG/2][LF] and a
+// backward part [W][SG/2][LB] of double2, LF = 2 RW NS lanes (F rows, then G rows), LB = RW NS
+// (F^T rows), so the 16-byte load k of wave w is one contiguous run over its lanes (the
+// row-major r05 blocks put every load's lanes on ~16 cache lines: the L1 request rate bound
+// the chain steps).  Columns past X are zero.
+struct RcMap {
+  int W, RW, NS, XP, SG, LF, LB, fwd, node;  // fwd / node: doubles per part / per node
+};
+constexpr RcMap rc_map(int X, int W) {
+  const int RW = (X + W - 1) / W, NS = rc_pick_ns(RW), XP = rc_row_len(X, W), SG = XP / NS;
+  const int LF = 2 * RW * NS, LB = RW * NS;
+  return RcMap{W, RW, NS, XP, SG, LF, LB, W * SG * LF, W * SG * (LF + LB)};
+}
+
 // x + (x of the lane whose index differs in bit 0 / bit 1): one DPP quad permutation per 32-bit
 // half.  Both partners compute a + b with the same operands, so every lane of the group ends
 // with the same bits.
@@ -143,15 +157,13 @@ __device__ __forceinline__ void lds_barrier() {
 
 // ---------------------------------------------------------------------------
 // Chain blocks of node i (one 256-thread workgroup per (problem, node)), from the stored
-// (symmetrised, tiled) factor block that the ADMM kernels use:
-//   d.CH[b] + i * 3 ndx XP:  FR (F_i row-major) | FT (F_i^T row-major) | G (S_i[dx, dx]),
-// rows of XP >= ndx columns, zero-padded (rc_row_len).
-// Every chain lane reads one contiguous row segment (16-byte loads, one VGPR offset + immediates).
+// (symmetrised, tiled) factor block that the ADMM kernels use: F_i, F_i^T and G_i = S_i[dx, dx]
+// in the chains' lane order (RcMap), d.CH[b] + i * node doubles.
 // F_i[a][k] = sum_{(e, s) in xc(a)} A_e rho_s sum_{(e', l) in cw(s)} A_e' S_i[l][k]
 // (the coupling product the sweep kernels apply as t_s = rho_s a_s(w) . w).
 __global__ __launch_bounds__(256) void k_fred(PlDev d, int N, int nnz, int ndx, int S_stride, int cpl_stride,
-                                              long long ch_stride, int XP) {
-  extern __shared__ double sc[];  // S_i[:, 0:ndx] dense, sc[l * ndx + k]
+                                              long long ch_stride, RcMap mp) {
+  extern __shared__ double sc[];  // S_i[:, 0:ndx] dense, sc[l * ndx + k]; then F_i
   const int b = blockIdx.x / (N + 1), i = blockIdx.x - b * (N + 1);
   typedef const __attribute__((address_space(4))) PlAdmmNode* CNode;
   const CNode an = (CNode)d.anodes;
@@ -170,36 +182,50 @@ __global__ __launch_bounds__(256) void k_fred(PlDev d, int N, int nnz, int ndx, 
     sc[q] = (c & 1) ? p.y : p.x;
   }
   __syncthreads();
-  const int X2 = ndx * ndx, XB = ndx * XP;
-  double* CH = d.CH + (size_t)b * ch_stride + (size_t)i * 3 * XB;
-  for (int q = threadIdx.x; q < XB; q += 256) {  // rows l < ndx of sc: G; zero padding of every part
-    const int l = q / XP, k = q - l * XP;
-    CH[2 * XB + q] = k < ndx ? sc[l * ndx + k] : 0.0;
-    if (k >= ndx) CH[q] = CH[XB + q] = 0.0;
-  }
-  if (i >= N) return;
-  const uint16_t* P = d.aprog + an[i].prog;
-  const double* As = d.As + (size_t)b * nnz + an[i].ent_off;
-  const double* rc = d.rhoc + ((size_t)b * (N + 1) + i) * cpl_stride;
-  const uint32_t* xc = reinterpret_cast<const uint32_t*>(P + an[i].xcp);
-  const uint32_t* cw = reinterpret_cast<const uint32_t*>(P + an[i].cwp);
-  const uint16_t* xcptr = P + an[i].xcptr;
-  const uint16_t* cwptr = P + an[i].cwptr;
-  for (int q = threadIdx.x; q < X2; q += 256) {
-    const int a = q / ndx, k = q - a * ndx;
-    double f = 0.0;
-    for (int qq = xcptr[a]; qq < xcptr[a + 1]; ++qq) {
-      const uint32_t w = xc[qq];
-      const int s = (int)(w >> 16);
-      double acc = 0.0;
-      for (int q2 = cwptr[s]; q2 < cwptr[s + 1]; ++q2) {
-        const uint32_t w2 = cw[q2];
-        acc += As[w2 & 0xffff] * sc[(int)(w2 >> 16) * ndx + k];
+  double* fs = sc + nw * ndx;  // F_i, fs[a * ndx + k]
+  const int X2 = ndx * ndx;
+  if (i < N) {
+    const uint16_t* P = d.aprog + an[i].prog;
+    const double* As = d.As + (size_t)b * nnz + an[i].ent_off;
+    const double* rc = d.rhoc + ((size_t)b * (N + 1) + i) * cpl_stride;
+    const uint32_t* xc = reinterpret_cast<const uint32_t*>(P + an[i].xcp);
+    const uint32_t* cw = reinterpret_cast<const uint32_t*>(P + an[i].cwp);
+    const uint16_t* xcptr = P + an[i].xcptr;
+    const uint16_t* cwptr = P + an[i].cwptr;
+    for (int q = threadIdx.x; q < X2; q += 256) {
+      const int a = q / ndx, k = q - a * ndx;
+      double f = 0.0;
+      for (int qq = xcptr[a]; qq < xcptr[a + 1]; ++qq) {
+        const uint32_t w = xc[qq];
+        const int s = (int)(w >> 16);
+        double acc = 0.0;
+        for (int q2 = cwptr[s]; q2 < cwptr[s + 1]; ++q2) {
+          const uint32_t w2 = cw[q2];
+          acc += As[w2 & 0xffff] * sc[(int)(w2 >> 16) * ndx + k];
+        }
+        f += As[w & 0xffff] * (rc[s] * acc);
       }
-      f += As[w & 0xffff] * (rc[s] * acc);
+      fs[q] = f;
     }
-    CH[a * XP + k] = f;       // FR: (a, k)
-    CH[XB + k * XP + a] = f;  // FT: (k, a)
+  } else {
+    for (int q = threadIdx.x; q < X2; q += 256) fs[q] = 0.0;  // F rows are not used at node N
+  }
+  __syncthreads();
+  // lane order of the chains (RcMap): entry e -> (part, wave w, load k, lane, half h)
+  double* CH = d.CH + (size_t)b * ch_stride + (size_t)i * mp.node;
+  const int hs = mp.SG / 2;
+  for (int e = threadIdx.x; e < mp.node; e += 256) {
+    const bool fwd = e < mp.fwd;
+    const int L = fwd ? mp.LF : mp.LB, e2 = (fwd ? e : e - mp.fwd) >> 1, h = e & 1;
+    const int lane = e2 % L, wk = e2 / L, k = wk % hs, w = wk / hs;
+    const int cq = lane / mp.NS, cs = lane - cq * mp.NS;
+    const bool rowF = !fwd || cq < mp.RW;
+    const int cj = rowF ? cq : cq - mp.RW;
+    const int r0 = (ndx * w) / mp.W, nr = (ndx * (w + 1)) / mp.W - r0;
+    const int row = r0 + min(cj, nr - 1), col = cs * mp.SG + 2 * k + h;
+    double v = 0.0;
+    if (col < ndx) v = !fwd ? fs[col * ndx + row] : (rowF ? fs[row * ndx + col] : sc[row * ndx + col]);
+    CH[e] = v;
   }
 }
 
@@ -618,7 +644,9 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   //   C2 (steps i = N-1..1): lanes q < RW: e_i[r] = w_i[r] - F_i^T[r] . e_{i+1}
   // delta / e are double-buffered in LDS (read one buffer, write the other), so one barrier
   // per step suffices.  Fixed lane -> (row, segment) map and a fixed-order reduction.
-  constexpr int RW = CS::RW, NS = CS::NS, SG = CS::SG, PD = CS::PD, XP = CS::XP, XB = X * XP;
+  constexpr int RW = CS::RW, NS = CS::NS, SG = CS::SG, PD = CS::PD;
+  constexpr RcMap MP = rc_map(X, W);
+  constexpr int LF = MP.LF, LB = MP.LB;
   const int r0 = (X * wv) / W, nr = (X * (wv + 1)) / W - r0;
   const int cq = lane / NS, cs = lane - cq * NS;
   const bool cF = cq < RW;
@@ -655,14 +683,15 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   auto chain_fwd = [&]() __attribute__((always_inline)) {
     double2 rg[PD][SG / 2];
     double u1[PD], u2[PD];
-    // per-lane offsets (constant over the steps) from wave-uniform bases: saddr + voffset loads
-    const int boff = ((cF ? 0 : 2 * XB) + crow * XP + cs * SG) / 2;
+    // per-lane offsets (constant over the steps) from wave-uniform bases: saddr + voffset loads;
+    // load k of the wave is one contiguous run of LF 16-byte entries
+    const int boff = wv * (SG / 2) * LF + min(lane, LF - 1);
     const int o1 = (cF ? 4 : 5) * L + crow, o2 = 3 * L + crow;
     auto fetch = [&](int s, int i) __attribute__((always_inline)) {
       const int ig = min(i, N);  // F rows are not used at step N (its block holds G_N only)
-      const double2* pp = reinterpret_cast<const double2*>(CH + (size_t)ig * 3 * XB);
+      const double2* pp = reinterpret_cast<const double2*>(CH + (size_t)ig * MP.node);
 #pragma unroll
-      for (int k = 0; k < SG / 2; ++k) rg[s][k] = gld(pp, boff + k);
+      for (int k = 0; k < SG / 2; ++k) rg[s][k] = gld(pp, boff + k * LF);
       u1[s] = ld_sc1(rchv, ig * X + o1);        // c'_i (F rows) / h'_i (G rows)
       u2[s] = ld_sc1(rchv, (ig + 1) * X + o2);  // a2_i
     };
@@ -721,12 +750,12 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
 
   auto chain_bwd = [&]() __attribute__((always_inline)) {
     double2 rg[PD][SG / 2];
-    const int boff = (XB + crow * XP + cs * SG) / 2;
+    const int boff = MP.fwd / 2 + wv * (SG / 2) * LB + min(lane, LB - 1);
     auto fetch = [&](int s, int i) __attribute__((always_inline)) {
       const int ic = max(i, 1);
-      const double2* pp = reinterpret_cast<const double2*>(CH + (size_t)ic * 3 * XB);
+      const double2* pp = reinterpret_cast<const double2*>(CH + (size_t)ic * MP.node);
 #pragma unroll
-      for (int k = 0; k < SG / 2; ++k) rg[s][k] = gld(pp, boff + k);
+      for (int k = 0; k < SG / 2; ++k) rg[s][k] = gld(pp, boff + k * LB);
     };
     auto step = [&](int s, int i, bool refill) __attribute__((always_inline)) {
       const double2* ec = reinterpret_cast<const double2*>(cbuf + ((i + 1) & 1) * 64) + cs * (SG / 2);
@@ -925,7 +954,7 @@ void launch_rc_t(PlOcpHandle* h, int niter, int check, const RcCfg& c) {
 
 }  // namespace
 
-long long rc_ch_stride(int N, int ndx, int W) { return (long long)(N + 1) * 3 * ndx * rc_row_len(ndx, W); }
+long long rc_ch_stride(int N, int ndx, int W) { return (long long)(N + 1) * rc_map(ndx, W).node; }
 
 // Workgroups per problem of k_admm_rc: enough for one round of node phases, as long as the
 // batch's workgroups are all resident at once (one per CU: the kernel's LDS), which the
@@ -947,14 +976,14 @@ bool admm_rc_supported(const PlOcpHandle* h) {
 }
 
 void launch_fred(PlOcpHandle* h) {
-  const size_t lds = (size_t)h->nw_max * h->ndx * sizeof(double);
+  const size_t lds = (size_t)(h->nw_max + h->ndx) * h->ndx * sizeof(double);
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)k_fred, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   hipLaunchKernelGGL(k_fred, dim3(h->B * (h->N + 1)), dim3(256), lds, h->stream, h->d, h->N, h->nnz, h->ndx,
-                     h->S_stride, std::max(h->ncpl_max, 1), h->ch_stride, rc_row_len(h->ndx, h->rc_waves));
+                     h->S_stride, std::max(h->ncpl_max, 1), h->ch_stride, rc_map(h->ndx, h->rc_waves));
 }
 
 void launch_admm_rc(PlOcpHandle* h, int niter, int check) {

@@ -37,7 +37,7 @@ if sub.sum() > 0:  # PL_RC_SUBTIMING build: node sub-phases of wave 0 (node 0), 
     for nm, k in zip(["loads", "coupling + u", "matvec x~", "rows / columns", "x update", "matvec g", "coupling out"], range(7)):
         print(f"  node 0 {nm:16s} {sub[:, k].mean():10.1f}")
 full = bo.debug("admm_t", B * 40)
-if B == 1 and full[16:20].sum() > 0:  # chain_fwd step sub-phases (wave 0), cycles per step
+if B == 1 and sub.sum() > 0 and full[16:20].sum() > 0:  # PL_RC_SUBTIMING build: chain_fwd step sub-phases (wave 0), cycles per step
     nsteps = it[0] * (N + 1)
     for nm, k in zip(["lds + fma", "reduce + stores", "refill issue", "barrier"], range(4)):
         print(f"  C1 step {nm:16s} {full[16 + k] / nsteps:10.1f}")
