@@ -73,11 +73,15 @@ constexpr int RC_SC1 = 16;  // cache-policy bits of the buffer ops: sc1
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rc_rsrc(const double* base, int count) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0, count * 8, 0x00020000);
 }
+// SC: the launch runs several workgroups per problem (the hand-offs need sc1); with one
+// workgroup per problem the same accesses are plain (L1 / L2 as in r05)
+template <bool SC>
 __device__ __forceinline__ double ld_sc1(__amdgpu_buffer_rsrc_t r, int idx) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, idx * 8, 0, RC_SC1));
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, idx * 8, 0, SC ? RC_SC1 : 0));
 }
+template <bool SC>
 __device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, int idx, double v) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, idx * 8, 0, RC_SC1);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, idx * 8, 0, SC ? RC_SC1 : 0);
 }
 
 // hand-off words of one problem (d.rcsync, zeroed before every launch)
@@ -230,7 +234,7 @@ __global__ __launch_bounds__(256) void k_fred(PlDev d, int N, int nnz, int ndx, 
 }
 
 // ---------------------------------------------------------------------------
-template <int W, int X>
+template <int W, int X, bool SC>
 __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, int m, int nnz, int S_stride,
                                                        int cpl_stride, long long ch_stride, int chv_stride, RcLds lm,
                                                        int niter, int check, double sigma, double alpha, int G) {
@@ -385,10 +389,10 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
           const uint32_t w = xc[qq];
           c += A(w & 0xffff) * tcpl[w >> 16];
         }
-        st_sc1(rchv, oCP + i * ndx + lane, c);
+        st_sc1<SC>(rchv, oCP + i * ndx + lane, c);
       }
     }
-    if (lane < ndx) st_sc1(rchv, oHP + i * ndx + lane, y[lane]);
+    if (lane < ndx) st_sc1<SC>(rchv, oHP + i * ndx + lane, y[lane]);
     wsync();
   };
 
@@ -452,8 +456,8 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
         lu[mm] = us[r];
       }
     }
-    const double dl = mode ? ld_sc1(rchv, oDL + i * ndx + rr) : 0.0;
-    const double ee = (mode && !term) ? ld_sc1(rchv, oEE + (i + 1) * ndx + rr) : 0.0;
+    const double dl = mode ? ld_sc1<SC>(rchv, oDL + i * ndx + rr) : 0.0;
+    const double ee = (mode && !term) ? ld_sc1<SC>(rchv, oEE + (i + 1) * ndx + rr) : 0.0;
     const int na = min(ne, cap);
     const int sh = (int)(((size_t)Ai >> 3) & 1);  // 16-byte alignment of the DMA source
     {
@@ -476,7 +480,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
         if (c < nw) v[c] = rh[mm];
         else if (c < T4) v[c] = 0.0;
       }
-      if (lane < ndx) st_sc1(rchv, oA2 + (i + 1) * ndx + lane, 0.0);
+      if (lane < ndx) st_sc1<SC>(rchv, oA2 + (i + 1) * ndx + lane, 0.0);
       wsync();
       matvec(i, R, true);
       coupling_out(i, A);
@@ -603,12 +607,12 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
         rn[mm] = sigma * xnew - qo[mm] + (term ? 0.0 : acc[c]);
         gst(xa, x_off + c, xnew);
         if (store_delta) gst(dxs, x_off + c, xnew - xo[mm]);
-        if (mode == 2) st_sc1(rrhs, x_off + c, rn[mm]);  // read by workgroup 0's closing pass
+        if (mode == 2) st_sc1<SC>(rrhs, x_off + c, rn[mm]);  // read by workgroup 0's closing pass
         else gst(rhs, x_off + c, rn[mm]);
       }
     }
     if (!term) {
-      if (lane < ndx) st_sc1(rchv, oA2 + (i + 1) * ndx + lane, acc[nw + lane]);
+      if (lane < ndx) st_sc1<SC>(rchv, oA2 + (i + 1) * ndx + lane, acc[nw + lane]);
 #pragma unroll
       for (int mm = 0; mm < MR; ++mm) {
         const int r = lane + 64 * mm;
@@ -665,7 +669,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
     const int cnt = (k1 - k0) * nr;
     for (int t = lane; t < cnt; t += 64) {
       const int kk = t / nr, j = t - kk * nr;
-      st_sc1(rchv, off + (k0 + kk) * X + r0 + j, hist[(k0 + kk) * nr + j]);
+      st_sc1<SC>(rchv, off + (k0 + kk) * X + r0 + j, hist[(k0 + kk) * nr + j]);
     }
   };
 
@@ -692,8 +696,8 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
       const double2* pp = reinterpret_cast<const double2*>(CH + (size_t)ig * MP.node);
 #pragma unroll
       for (int k = 0; k < SG / 2; ++k) rg[s][k] = gld(pp, boff + k * LF);
-      u1[s] = ld_sc1(rchv, ig * X + o1);        // c'_i (F rows) / h'_i (G rows)
-      u2[s] = ld_sc1(rchv, (ig + 1) * X + o2);  // a2_i
+      u1[s] = ld_sc1<SC>(rchv, ig * X + o1);        // c'_i (F rows) / h'_i (G rows)
+      u2[s] = ld_sc1<SC>(rchv, (ig + 1) * X + o2);  // a2_i
     };
     auto step = [&](int s, int i, bool refill) __attribute__((always_inline)) {
       CSUB(-1);
@@ -734,7 +738,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
     if (wv == 0) {
       cbuf[lane] = 0.0;  // delta_0
       cbuf[64 + lane] = 0.0;  // the padding columns [X, XP) of both buffers stay 0
-      if (lane < X) st_sc1(rchv, oDL + lane, 0.0);
+      if (lane < X) st_sc1<SC>(rchv, oDL + lane, 0.0);
     }
     lds_barrier();
     int i0 = 0;
@@ -784,7 +788,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
     if (cF && cs == 0 && cvalid) {
       const double e = whist[N * nr + cj];
       cbuf[(N & 1) * 64 + crow] = e;
-      st_sc1(rchv, oEE + N * X + crow, e);
+      st_sc1<SC>(rchv, oEE + N * X + crow, e);
     }
     lds_barrier();
     int j0 = 0;  // e_i for i = N-1 .. 1: steps j = N - 1 - i
@@ -854,7 +858,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   };
   const int i0 = g * W + wv, istep = G * W;  // this wave's nodes
   T(-1);
-  if (g == 0 && wv == 0 && lane < ndx) st_sc1(rchv, oA2 + lane, 0.0);  // a2_{-1}
+  if (g == 0 && wv == 0 && lane < ndx) st_sc1<SC>(rchv, oA2 + lane, 0.0);  // a2_{-1}
   for (int i = i0; i <= N; i += istep) pnode(i, 0, false);
   T(0);
   if (!fan_in(1)) { give_up(); return; }
@@ -890,7 +894,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_admm_rc(PlDev d, int N, int n, in
   for (int i = wv; i <= N; i += W) {
     if (i >= 1 && lane < ndx) {
       const int c = an[i].x_off + lane;
-      rhs[c] = ld_sc1(rrhs, c) + ld_sc1(rchv, oA2 + i * ndx + lane);
+      rhs[c] = ld_sc1<SC>(rrhs, c) + ld_sc1<SC>(rchv, oA2 + i * ndx + lane);
     }
   }
   if (wv == 0 && lane == 0) {
@@ -942,14 +946,20 @@ template <int W, int X>
 void launch_rc_t(PlOcpHandle* h, int niter, int check, const RcCfg& c) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)k_admm_rc<W, X>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_admm_rc<W, X, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_admm_rc<W, X, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   const int G = rc_groups(h);
   if (G > 1) (void)hipMemsetAsync(h->d.rcsync, 0, (size_t)h->B * PL_RC_SYNC * sizeof(unsigned), h->stream);
-  hipLaunchKernelGGL((k_admm_rc<W, X>), dim3(h->B * G), dim3(64 * W), c.lds, h->stream, h->d, h->N, h->n, h->m, h->nnz,
-                     h->S_stride, std::max(h->ncpl_max, 1), h->ch_stride, h->chv_stride, c.lm, niter, check,
-                     h->set.sigma, h->set.alpha, G);
+  if (G > 1)
+    hipLaunchKernelGGL((k_admm_rc<W, X, true>), dim3(h->B * G), dim3(64 * W), c.lds, h->stream, h->d, h->N, h->n, h->m,
+                       h->nnz, h->S_stride, std::max(h->ncpl_max, 1), h->ch_stride, h->chv_stride, c.lm, niter, check,
+                       h->set.sigma, h->set.alpha, G);
+  else
+    hipLaunchKernelGGL((k_admm_rc<W, X, false>), dim3(h->B), dim3(64 * W), c.lds, h->stream, h->d, h->N, h->n, h->m,
+                       h->nnz, h->S_stride, std::max(h->ncpl_max, 1), h->ch_stride, h->chv_stride, c.lm, niter, check,
+                       h->set.sigma, h->set.alpha, 1);
 }
 
 }  // namespace
