@@ -38,6 +38,12 @@ struct JacEmit {
     }
     ++r;
   }
+  // a row block holding none of the column's remaining entries is not computed (r06)
+  __device__ bool skip_block(int n) {
+    if (ptr < end && rowidx[ptr] < r + n) return false;
+    r += n;
+    return true;
+  }
 };
 
 __device__ inline void node_inputs(const PlDev& d, const PlNode& nd, const PlNode& nn, const double* x,

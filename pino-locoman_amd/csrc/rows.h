@@ -146,6 +146,14 @@ PL_HD void chol_solve(const double* L, int n, double* x) {
 // so the caller took the torque tangent from a primal pass instead of the dual tree pass:
 // lin_base holds the 6 base torques' tangents and the first nj tangent slots of kstore the
 // joint torques' (k_eval_jac_lin); every other kinematic tangent of such a column is zero.
+// An emitter may skip whole row blocks: emit.skip_block(n) returns true (and advances past the n
+// rows) when none of them is wanted -- the Jacobian's column emitter, whose column has entries in
+// a few rows only (k_eval.hip JacEmit).  Emitters without the member compute every row.
+template <class E>
+PL_HD auto emit_skip(E& e, int n, int) -> decltype(e.skip_block(n)) { return e.skip_block(n); }
+template <class E>
+PL_HD bool emit_skip(E&, int, long) { return false; }
+
 template <class S, int DYN, class Emit>
 PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double* p, const VecIn<S>& dx,
                      const VecIn<S>& u, const VecIn<S>& dxn, Emit& emit, S* kstore, int kstride,
@@ -329,6 +337,7 @@ PL_HD void node_rows(const PlModel& M, const PlOcpConst& O, int i, const double*
   for (int bi = 0; bi < nb; ++bi) {
     const PlRowBlock B = O.blk[type][bi];
     const int k = B.arg;
+    if (emit_skip(emit, B.count, 0)) continue;  // B.count: the rows the switch below emits
     switch (B.kind) {
       case PL_RB_INIT:
         for (int r = 0; r < O.ndx; ++r) emit(dx[r], 0.0, 0.0);
