@@ -93,6 +93,13 @@ template <class T>
 __device__ __forceinline__ T gld(const T* base, int idx) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (unsigned)idx * (unsigned)sizeof(T));
 }
+// the same as a non-temporal (streaming) load: the factor blocks are read once per sweep
+__device__ __forceinline__ double2 gld_nt(const double2* base, int idx) {
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  const v2d v = __builtin_nontemporal_load(
+      reinterpret_cast<const v2d*>(reinterpret_cast<const char*>(base) + (unsigned)idx * (unsigned)sizeof(double2)));
+  return make_double2(v.x, v.y);
+}
 template <class T>
 __device__ __forceinline__ void gst(T* base, int idx, T v) {
   *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (unsigned)idx * (unsigned)sizeof(T)) = v;

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     for (int k = 0; k < KM; ++k) {
       const int kk = min(kbase + k, K - 1);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) R.s[k][j] = gld(p, (kk * 8 + j) * 64 + lane);
+      for (int j = 0; j < 8; ++j) R.s[k][j] = gld_nt(p, (kk * 8 + j) * 64 + lane);
     }
   };
   auto prefetch_E = [&](int kind1, int i1, Early& E) __attribute__((always_inline)) {
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
         if (last_pass) {  // uniform; always true for blocks of <= KM slots per lane
           const int kq = min(k, Kn - 1);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) R.s[k][j] = gld(pn, (kq * 8 + j) * 64 + lane);
+          for (int j = 0; j < 8; ++j) R.s[k][j] = gld_nt(pn, (kq * 8 + j) * 64 + lane);
         }
       }
     };
