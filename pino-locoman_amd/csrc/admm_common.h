@@ -94,6 +94,9 @@ __device__ __forceinline__ T gld(const T* base, int idx) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (unsigned)idx * (unsigned)sizeof(T));
 }
 // the same as a non-temporal (streaming) load: the factor blocks are read once per sweep
+__device__ __forceinline__ double gld_nt(const double* base, int idx) {
+  return __builtin_nontemporal_load(reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + (unsigned)idx * 8u));
+}
 __device__ __forceinline__ double2 gld_nt(const double2* base, int idx) {
   typedef double v2d __attribute__((ext_vector_type(2)));
   const v2d v = __builtin_nontemporal_load(

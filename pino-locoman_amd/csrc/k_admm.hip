@@ -203,7 +203,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     const int ia = fa ? i1 - 1 : i1;
     const int eo = an[ia].ent_off, ne = an[ia].nent;
 #pragma unroll
-    for (int k = 0; k < ASR; ++k) las[k] = gld(As, eo + (bw ? min(lane + 64 * k, ne - 1) : 0));
+    for (int k = 0; k < ASR; ++k) las[k] = gld_nt(As, eo + (bw ? min(lane + 64 * k, ne - 1) : 0));
   };
   auto prefetch_LR = [&](int kind1, int i1, LateR& LR) __attribute__((always_inline)) {
     const bool bw = bwd_kind(kind1);
@@ -211,11 +211,11 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
 #pragma unroll
     for (int mm = 0; mm < MR; ++mm) {
       const int r = ro + (bw ? min(lane + 64 * mm, max(nr - 1, 0)) : 0);
-      LR.z[mm] = gld(za, r);
-      LR.y[mm] = gld(ya, r);
-      LR.rho[mm] = gld(rho, r);
-      LR.l[mm] = gld(ls, r);
-      LR.u[mm] = gld(us, r);
+      LR.z[mm] = gld_nt(za, r);
+      LR.y[mm] = gld_nt(ya, r);
+      LR.rho[mm] = gld_nt(rho, r);
+      LR.l[mm] = gld_nt(ls, r);
+      LR.u[mm] = gld_nt(us, r);
     }
   };
   auto prefetch_LC = [&](int kind1, int i1, LateC& LC) __attribute__((always_inline)) {
@@ -224,8 +224,8 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
 #pragma unroll
     for (int mm = 0; mm < MV; ++mm) {
       const int j = xo + (need ? min(lane + 64 * mm, nw1 - 1) : 0);
-      LC.x[mm] = gld(xa, j);
-      LC.q[mm] = gld(qs, j);
+      LC.x[mm] = gld_nt(xa, j);
+      LC.q[mm] = gld_nt(qs, j);
     }
   };
 
