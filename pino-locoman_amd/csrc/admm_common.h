@@ -94,6 +94,8 @@ __device__ __forceinline__ T gld(const T* base, int idx) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (unsigned)idx * (unsigned)sizeof(T));
 }
 // the same as a non-temporal (streaming) load: the factor blocks are read once per sweep
+template <bool NT, class T>
+__device__ __forceinline__ T gldx(const T* base, int idx);
 __device__ __forceinline__ double gld_nt(const double* base, int idx) {
   return __builtin_nontemporal_load(reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + (unsigned)idx * 8u));
 }
@@ -102,6 +104,12 @@ __device__ __forceinline__ double2 gld_nt(const double2* base, int idx) {
   const v2d v = __builtin_nontemporal_load(
       reinterpret_cast<const v2d*>(reinterpret_cast<const char*>(base) + (unsigned)idx * (unsigned)sizeof(double2)));
   return make_double2(v.x, v.y);
+}
+// a plain (gld) or non-temporal (gld_nt) load, chosen at compile time
+template <bool NT, class T>
+__device__ __forceinline__ T gldx(const T* base, int idx) {
+  if constexpr (NT) return gld_nt(base, idx);
+  else return gld(base, idx);
 }
 template <class T>
 __device__ __forceinline__ void gst(T* base, int idx, T v) {

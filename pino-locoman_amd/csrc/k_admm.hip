@@ -78,7 +78,7 @@ struct AdmmLds {
 
 }  // namespace
 
-template <int PPW, int ASR, bool TIMING>
+template <int PPW, int ASR, bool TIMING, bool NT>
 __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int n, int m, int nnz, int ndx,
                                                       int S_stride, int cpl_stride, AdmmLds lm, int niter, int check,
                                                       int fwd_asb, double sigma, double alpha) {
@@ -134,6 +134,10 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
   double* bt = d.bt + (size_t)b * n;
   double* dxs = d.dxs + (size_t)b * n;
   double* dys = d.dys + (size_t)b * m;
+  // NT: the batch's factor far exceeds the 256 MB Infinity Cache (admm_config), so the streams
+  // (factor blocks, A, the row / column operands) are non-temporal loads; below it the sweeps'
+  // re-reads partly hit the cache and plain loads are kept (Go2 centroidal_vel at B = 1024:
+  // 328 MB of factor, nt was 2 % slower)
   // node table: uniform reads through the constant address space are scalar loads
   typedef const __attribute__((address_space(4))) PlAdmmNode* CNode;
   CNode an = (CNode)d.anodes;
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     for (int k = 0; k < KM; ++k) {
       const int kk = min(kbase + k, K - 1);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) R.s[k][j] = gld_nt(p, (kk * 8 + j) * 64 + lane);
+      for (int j = 0; j < 8; ++j) R.s[k][j] = gldx<NT>(p, (kk * 8 + j) * 64 + lane);
     }
   };
   auto prefetch_E = [&](int kind1, int i1, Early& E) __attribute__((always_inline)) {
@@ -203,7 +207,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
     const int ia = fa ? i1 - 1 : i1;
     const int eo = an[ia].ent_off, ne = an[ia].nent;
 #pragma unroll
-    for (int k = 0; k < ASR; ++k) las[k] = gld_nt(As, eo + (bw ? min(lane + 64 * k, ne - 1) : 0));
+    for (int k = 0; k < ASR; ++k) las[k] = gldx<NT>(As, eo + (bw ? min(lane + 64 * k, ne - 1) : 0));
   };
   auto prefetch_LR = [&](int kind1, int i1, LateR& LR) __attribute__((always_inline)) {
     const bool bw = bwd_kind(kind1);
@@ -211,11 +215,11 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
 #pragma unroll
     for (int mm = 0; mm < MR; ++mm) {
       const int r = ro + (bw ? min(lane + 64 * mm, max(nr - 1, 0)) : 0);
-      LR.z[mm] = gld_nt(za, r);
-      LR.y[mm] = gld_nt(ya, r);
-      LR.rho[mm] = gld_nt(rho, r);
-      LR.l[mm] = gld_nt(ls, r);
-      LR.u[mm] = gld_nt(us, r);
+      LR.z[mm] = gldx<NT>(za, r);
+      LR.y[mm] = gldx<NT>(ya, r);
+      LR.rho[mm] = gldx<NT>(rho, r);
+      LR.l[mm] = gldx<NT>(ls, r);
+      LR.u[mm] = gldx<NT>(us, r);
     }
   };
   auto prefetch_LC = [&](int kind1, int i1, LateC& LC) __attribute__((always_inline)) {
@@ -224,8 +228,8 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
 #pragma unroll
     for (int mm = 0; mm < MV; ++mm) {
       const int j = xo + (need ? min(lane + 64 * mm, nw1 - 1) : 0);
-      LC.x[mm] = gld_nt(xa, j);
-      LC.q[mm] = gld_nt(qs, j);
+      LC.x[mm] = gldx<NT>(xa, j);
+      LC.q[mm] = gldx<NT>(qs, j);
     }
   };
 
@@ -319,7 +323,7 @@ __global__ __launch_bounds__(64 * PPW, 1) void k_admm(PlDev d, int B, int N, int
         if (last_pass) {  // uniform; always true for blocks of <= KM slots per lane
           const int kq = min(k, Kn - 1);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) R.s[k][j] = gld_nt(pn, (kq * 8 + j) * 64 + lane);
+          for (int j = 0; j < 8; ++j) R.s[k][j] = gldx<NT>(pn, (kq * 8 + j) * 64 + lane);
         }
       }
     };
@@ -837,6 +841,7 @@ struct AdmmCfg {
   AdmmLds lm;
   int ppw;
   size_t lds;
+  bool nt;  // non-temporal streams: the batch's factor > 2 x the 256 MB Infinity Cache
 };
 
 AdmmCfg admm_config(const PlOcpHandle* h) {
@@ -881,20 +886,27 @@ AdmmCfg admm_config(const PlOcpHandle* h) {
   lm.asb_cap = cap;
   lm.per_wave = o + cap;
   c.lds = (size_t)(lm.prog_dbl + c.ppw * lm.per_wave) * sizeof(double);
+  c.nt = (double)h->B * h->S_stride * sizeof(double) > 512.0 * 1024 * 1024;
   return c;
+}
+
+template <int PPW, int ASR, bool TIMING, bool NT>
+void launch_admm_nt(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)k_admm<PPW, ASR, TIMING, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const int grid = (h->B + PPW - 1) / PPW;
+  hipLaunchKernelGGL((k_admm<PPW, ASR, TIMING, NT>), dim3(grid), dim3(64 * PPW), c.lds, h->stream, h->d, h->B, h->N,
+                     h->n, h->m, h->nnz, h->ndx, h->S_stride, std::max(h->ncpl_max, 1), c.lm, niter, check,
+                     h->admm_fwd_asb, h->set.sigma, h->set.alpha);
 }
 
 template <int PPW, int ASR, bool TIMING = false>
 void launch_admm_t(PlOcpHandle* h, int niter, int check, const AdmmCfg& c) {
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)k_admm<PPW, ASR, TIMING>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  const int grid = (h->B + PPW - 1) / PPW;
-  hipLaunchKernelGGL((k_admm<PPW, ASR, TIMING>), dim3(grid), dim3(64 * PPW), c.lds, h->stream, h->d, h->B, h->N, h->n,
-                     h->m, h->nnz, h->ndx, h->S_stride, std::max(h->ncpl_max, 1), c.lm, niter, check, h->admm_fwd_asb,
-                     h->set.sigma, h->set.alpha);
+  if (c.nt) launch_admm_nt<PPW, ASR, TIMING, true>(h, niter, check, c);
+  else launch_admm_nt<PPW, ASR, TIMING, false>(h, niter, check, c);
 }
 
 template <int ASR>
